@@ -1,0 +1,305 @@
+"""arpack-ng_amd — MI355X-native implicitly restarted Lanczos/Arnoldi behind
+arpack-ng's reverse-communication interface.
+
+The product is the C-ABI library ``libarpack_hip.so`` (declared in
+``include/arpack_hip.h``).  This module is the Python host-side mirror of the
+reference's interface for the path: thin ctypes bindings with the reference's
+names and argument meaning (``dsaupd``/``dseupd`` behave like the Fortran
+routines of SRC/dsaupd.f / SRC/dseupd.f, driven exactly like
+TESTS/icb_arpack_c.c does), plus the native extension (device CSR operators and
+the on-GPU driver).
+
+There is no CPU fallback: if the HIP library is missing, every entry point
+raises.  PyTorch is only used as a device-memory allocator for the caller-side
+arrays (resid, V, workd) in device-pointer mode.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libarpack_hip.so")
+
+_lib = None
+
+
+class ArpackError(RuntimeError):
+    """Raised for negative `info` codes (SRC/dsaupd.f:243-276)."""
+
+    def __init__(self, routine, info, extra=None):
+        super().__init__(f"{routine} returned info={info}")
+        self.routine = routine
+        self.info = info
+        self.extra = extra or {}
+
+
+def build(jobs: int = 8) -> str:
+    """Compile libarpack_hip.so for gfx950 in-tree (hipcc, no GPU needed)."""
+    subprocess.run(["make", "-C", HERE, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} not built: the HIP engine is required (no CPU fallback); "
+                "run arpack_ng_amd.build() / `make -C arpack-ng_amd`")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+_I = C.c_int
+_PI = C.POINTER(C.c_int)
+_PD = C.c_void_p  # double* (host or device)
+
+
+def _declare(L):
+    L.arpack_hip_version.restype = C.c_char_p
+    L.arpack_hip_device_count.restype = C.c_int
+    L.dsaupd_c.argtypes = [_PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I,
+                           _PI, _PI, _PD, _PD, _I, _PI]
+    L.dseupd_c.argtypes = [_I, C.c_char_p, _PI, _PD, _PD, _I, C.c_double, C.c_char_p, _I,
+                           C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I, _PI, _PI, _PD, _PD, _I,
+                           _PI]
+    L.arpack_hip_dsaupd_csr.argtypes = [C.c_void_p] + L.dsaupd_c.argtypes
+    L.arpack_hip_csr_create.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64, C.c_void_p,
+                                        C.c_void_p, C.c_void_p]
+    L.arpack_hip_csr_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_csr_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_csr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.arpack_hip_csr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_gen_laplace2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
+    L.arpack_hip_gen_laplace3d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
+    L.arpack_hip_gen_banded_sym.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64,
+                                            C.c_int64, C.c_uint32, C.c_int, C.c_int]
+    L.arpack_hip_set_stream.argtypes = [C.c_void_p]
+    L.stat_c.argtypes = [_PI] * 5 + [C.POINTER(C.c_float)] * 26
+    L.arpack_hip_kit_dstqrb.argtypes = [_I, _PD, _PD, _PD, _PD]
+    L.arpack_hip_kit_dsteqr.argtypes = [_I, _PD, _PD, _PD, _I, _PD]
+    L.arpack_hip_kit_dlartg.argtypes = [C.c_double, C.c_double] + [C.POINTER(C.c_double)] * 3
+    L.arpack_hip_kit_dsortr.argtypes = [C.c_char_p, _I, _I, _PD, _PD]
+    L.arpack_hip_kit_dsapps_host.argtypes = [_I, _I, _PD, _PD, _I, _PD, _I]
+    L.arpack_hip_kit_dlarnv.argtypes = [_PI, _I, _PD]
+
+
+def version() -> str:
+    return lib().arpack_hip_version().decode()
+
+
+def device_count() -> int:
+    return lib().arpack_hip_device_count()
+
+
+# ----------------------------------------------------------------------------- arrays
+def _ptr(a):
+    """Raw address of a numpy array or a torch tensor (host or device)."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    raise TypeError(type(a))
+
+
+def _ip(a):
+    return a.ctypes.data_as(_PI)
+
+
+def stats():
+    """stat_c(): /timing/ counters of the last solve (stat.h:8-21)."""
+    L = lib()
+    ints = [C.c_int() for _ in range(5)]
+    fl = [C.c_float() for _ in range(26)]
+    L.stat_c(*[C.byref(i) for i in ints], *[C.byref(f) for f in fl])
+    return dict(zip(["nopx", "nbx", "nrorth", "nitref", "nrstrt"], [i.value for i in ints]))
+
+
+# ------------------------------------------------------------------- CSR operator
+class CSR:
+    """A CSR matrix resident in HBM (the `ido=+-1` OP served on the GPU)."""
+
+    def __init__(self, handle, owner=True):
+        self.h = C.c_void_p(handle)
+        n = C.c_int64()
+        nnz = C.c_int64()
+        lib().arpack_hip_csr_info(self.h, C.byref(n), C.byref(nnz))
+        self.n, self.nnz = n.value, nnz.value
+        self._owner = owner
+
+    def __del__(self):
+        try:
+            if self._owner and self.h and _lib is not None:
+                _lib.arpack_hip_csr_destroy(self.h)
+                self.h = C.c_void_p(0)
+        except Exception:
+            pass
+
+    @classmethod
+    def from_arrays(cls, rowptr, col, val):
+        rowptr = np.ascontiguousarray(rowptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        h = C.c_void_p()
+        rc = lib().arpack_hip_csr_create(C.byref(h), len(rowptr) - 1, len(col), rowptr.ctypes.data,
+                                         col.ctypes.data, val.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("arpack_hip_csr_create failed")
+        return cls(h.value)
+
+    @classmethod
+    def laplace2d(cls, m, scale=1.0):
+        h = C.c_void_p()
+        if lib().arpack_hip_gen_laplace2d(C.byref(h), m, scale) != 0:
+            raise RuntimeError("laplace2d generation failed")
+        return cls(h.value)
+
+    @classmethod
+    def laplace3d(cls, m, scale=1.0):
+        h = C.c_void_p()
+        if lib().arpack_hip_gen_laplace3d(C.byref(h), m, scale) != 0:
+            raise RuntimeError("laplace3d generation failed")
+        return cls(h.value)
+
+    @classmethod
+    def banded_sym(cls, n, seed=1234, bandwidth=4096, per_row=25, r0=0, r1=None):
+        h = C.c_void_p()
+        r1 = n if r1 is None else r1
+        if lib().arpack_hip_gen_banded_sym(C.byref(h), n, r0, r1, seed, bandwidth, per_row) != 0:
+            raise RuntimeError("banded_sym generation failed")
+        return cls(h.value)
+
+    def download(self):
+        rowptr = np.empty(self.n + 1, np.int64)
+        col = np.empty(self.nnz, np.int32)
+        val = np.empty(self.nnz, np.float64)
+        lib().arpack_hip_csr_download(self.h, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data)
+        return rowptr, col, val
+
+    def matvec_device(self, x, y):
+        """y = A x for device buffers (torch tensors on cuda)."""
+        if lib().arpack_hip_csr_spmv(self.h, _ptr(x), _ptr(y)) != 0:
+            raise RuntimeError("spmv failed")
+
+
+# ------------------------------------------------------------- RCI (reference API)
+class SymRci:
+    """State of one dsaupd/dseupd solve, mirroring the reference's argument list
+    (SRC/dsaupd.f:182-186).  `device=True` allocates resid/V/workd in HBM
+    (torch tensors) so the caller's OP works on device pointers; otherwise
+    numpy host arrays (the engine mirrors them in HBM)."""
+
+    def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300,
+                 ishift=1, v0=None, device=False):
+        self.n, self.nev, self.ncv = n, nev, ncv
+        self.which, self.bmat, self.tol = which, bmat, float(tol)
+        self.device = device
+        self.ido = np.zeros(1, np.int32)
+        self.info = np.zeros(1, np.int32)
+        self.iparam = np.zeros(11, np.int32)
+        self.ipntr = np.zeros(11, np.int32)
+        self.iparam[0] = ishift
+        self.iparam[2] = mxiter
+        self.iparam[6] = mode
+        self.lworkl = ncv * ncv + 8 * ncv
+        self.workl = np.zeros(self.lworkl)
+        self.ldv = n
+        if device:
+            import torch
+            dev = torch.device("cuda")
+            self.resid = torch.zeros(n, dtype=torch.float64, device=dev)
+            self.v = torch.zeros(ncv * n, dtype=torch.float64, device=dev)
+            self.workd = torch.zeros(3 * n, dtype=torch.float64, device=dev)
+            if v0 is not None:
+                self.resid.copy_(torch.as_tensor(np.asarray(v0, np.float64)).to(dev))
+        else:
+            self.resid = np.zeros(n) if v0 is None else np.array(v0, np.float64, copy=True)
+            self.v = np.zeros(ncv * n)
+            self.workd = np.zeros(3 * n)
+        self.info[0] = 0 if v0 is None else 1
+
+    def aupd(self):
+        """One dsaupd_c call; returns ido."""
+        lib().dsaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev,
+                       self.tol, _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                       _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
+                       self.lworkl, _ip(self.info))
+        return int(self.ido[0])
+
+    def aupd_csr(self, A: CSR):
+        """Run to completion with OP = A on the GPU (arpack_hip_dsaupd_csr)."""
+        lib().arpack_hip_dsaupd_csr(A.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                    self.which.encode(), self.nev, self.tol, _ptr(self.resid),
+                                    self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam),
+                                    _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
+                                    self.lworkl, _ip(self.info))
+        return int(self.ido[0])
+
+    def slice(self, k):
+        """workd slice ipntr[k] (1-based offset) of length n."""
+        o = int(self.ipntr[k]) - 1
+        return self.workd[o:o + self.n]
+
+    def eupd(self, rvec=True, howmny="A", sigma=0.0, z=None):
+        nconv = int(self.iparam[4])
+        d = np.zeros(self.nev)
+        if z is None:
+            if self.device:
+                import torch
+                z = torch.zeros(self.nev * self.n, dtype=torch.float64, device="cuda")
+            else:
+                z = np.zeros(self.nev * self.n)
+        select = np.zeros(self.ncv, np.int32)
+        info = np.zeros(1, np.int32)
+        lib().dseupd_c(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z),
+                       self.n, sigma, self.bmat.encode(), self.n, self.which.encode(), self.nev,
+                       self.tol, _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                       _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
+                       self.lworkl, _ip(info))
+        if info[0] < 0:
+            raise ArpackError("dseupd", int(info[0]))
+        return d[:nconv], z, nconv
+
+    @property
+    def ritz(self):
+        o = int(self.ipntr[5]) - 1
+        return self.workl[o:o + self.ncv].copy()
+
+
+def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,
+          device=False):
+    """Drive the RCI loop with a user OP (callable y = op(x) on workd slices), like
+    TESTS/icb_arpack_c.c:60-65.  With `op` a CSR, the loop runs entirely on the
+    GPU (arpack_hip_dsaupd_csr).  Returns (d, Z, info-dict)."""
+    ncv = ncv or min(n, max(2 * nev + 1, 20))
+    s = SymRci(n, nev, ncv, which, tol, mxiter=mxiter, v0=v0, device=device)
+    if isinstance(op, CSR):
+        s.aupd_csr(op)
+    else:
+        while True:
+            ido = s.aupd()
+            if ido in (-1, 1):
+                x = s.slice(0)
+                y = op(x)
+                s.slice(1)[:] = y
+            elif ido == 99:
+                break
+            else:
+                raise ArpackError("dsaupd", int(s.info[0]), {"ido": ido})
+    if s.info[0] < 0:
+        raise ArpackError("dsaupd", int(s.info[0]))
+    res = dict(info=int(s.info[0]), iters=int(s.iparam[2]), nconv=int(s.iparam[4]),
+               nopx=int(s.iparam[8]), nrorth=int(s.iparam[10]), ritz=s.ritz)
+    d, z, nconv = s.eupd(rvec=rvec)
+    if rvec:
+        if device:
+            z = z.view(s.nev, n)[:nconv].cpu().numpy().T
+        else:
+            z = z.reshape(s.nev, n)[:nconv].T
+    return d, (z if rvec else None), res

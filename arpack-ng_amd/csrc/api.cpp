@@ -1,0 +1,288 @@
+// C-ABI layer: the reference's ICB entry points (ICB/arpack.h), the Fortran
+// symbols (dsaupd_ ...), stat_c/debug_c, and the arpack_hip_* extension.
+//
+// Argument checking, the workl layout and the iparam/info post-processing
+// follow SRC/dsaupd.f:473-690 exactly; everything between ido = 0 and ido = 99
+// is the SymSolver coroutine (sym.cpp).
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/arpack_hip.h"
+#include "engine.hpp"
+
+const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A);
+
+namespace ahip {
+
+Stats g_stats;
+uint64_t g_dseed = 0;
+static bool g_dseed_init = false;
+static hipStream_t g_stream = nullptr;
+static std::mutex g_mu;
+static std::unordered_map<const void*, std::unique_ptr<SymSolver>> g_sym;
+
+hipStream_t default_stream() { return g_stream; }
+
+uint64_t seed48_from_iseed(const int is[4]) {
+    return ((uint64_t)(is[0] & 4095) << 36) | ((uint64_t)(is[1] & 4095) << 24) |
+           ((uint64_t)(is[2] & 4095) << 12) | (uint64_t)(is[3] & 4095);
+}
+void iseed_from_seed48(uint64_t s, int is[4]) {
+    is[0] = (int)((s >> 36) & 4095);
+    is[1] = (int)((s >> 24) & 4095);
+    is[2] = (int)((s >> 12) & 4095);
+    is[3] = (int)(s & 4095);
+}
+uint64_t lcg_advance(uint64_t seed, uint64_t steps) {
+    const uint64_t mask = (1ull << 48) - 1;
+    uint64_t base = 33952834046453ull, p = 1;
+    while (steps) {
+        if (steps & 1) p = (p * base) & mask;
+        base = (base * base) & mask;
+        steps >>= 1;
+    }
+    return (seed * p) & mask;
+}
+
+static void ensure_seed() {
+    if (!g_dseed_init) {  // SRC/dgetv0.f:202-208: iseed = (1,3,5,7) once per process
+        const int is[4] = {1, 3, 5, 7};
+        g_dseed = seed48_from_iseed(is);
+        g_dseed_init = true;
+    }
+}
+
+// dsaupd argument checks (SRC/dsaupd.f:501-543); returns ierr
+static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lworkl, int mode,
+                     int ishift, int mxiter) {
+    int ierr = 0;
+    if (n <= 0) ierr = -1;
+    else if (nev <= 0) ierr = -2;
+    else if (ncv <= nev || ncv > n) ierr = -3;
+    if (mxiter <= 0) ierr = -4;
+    if (which != la::Which::LM && which != la::Which::SM && which != la::Which::LA &&
+        which != la::Which::SA && which != la::Which::BE)
+        ierr = -5;
+    if (bmat != 'I' && bmat != 'G') ierr = -6;
+    if (lworkl < ncv * ncv + 8 * ncv) ierr = -7;
+    if (mode < 1 || mode > 5) ierr = -10;
+    else if (mode == 1 && bmat == 'G') ierr = -11;
+    else if (ishift < 0 || ishift > 1) ierr = -12;
+    else if (nev == 1 && which == la::Which::BE) ierr = -13;
+    return ierr;
+}
+
+static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
+                     double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
+                     double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    SymSolver* S = nullptr;
+    if (*ido == 0) {
+        ensure_seed();
+        g_stats = Stats{};  // dstats (SRC/dstats.f)
+        const la::Which w = la::parse_which(which);
+        const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
+        int ierr = sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
+        if (csr && (mode != 1 || bmat[0] != 'I' || csr->n != n)) ierr = (ierr ? ierr : -11);
+        if (ierr != 0) {
+            *info = ierr;
+            *ido = 99;
+            return;
+        }
+        if (*tol <= 0.0) *tol = la::kEps;
+        auto up = std::make_unique<SymSolver>();
+        S = up.get();
+        S->bmat = bmat[0];
+        S->which = w;
+        S->n = n;
+        S->ncv = ncv;
+        S->mode = mode;
+        S->ishift = ishift;
+        S->mxiter = mxiter;
+        S->nev0 = nev;
+        S->np = ncv - nev;
+        S->lworkl = lworkl;
+        S->info = *info;
+        // workl layout (SRC/dsaupd.f:566-595)
+        std::memset(workl, 0, sizeof(double) * (size_t)(ncv * ncv + 8 * ncv));
+        S->ih = 0;
+        S->iritz = S->ih + 2 * ncv;
+        S->ibounds = S->iritz + ncv;
+        S->iq = S->ibounds + ncv;
+        S->iw = S->iq + ncv * ncv;
+        const int next = S->iw + 3 * ncv;
+        ipntr[3] = next + 1;
+        ipntr[4] = S->ih + 1;
+        ipntr[5] = S->iritz + 1;
+        ipntr[6] = S->ibounds + 1;
+        ipntr[10] = S->iw + 1;
+        if (S->a.attach(n, ncv, resid, v, ldv, workd) != 0 ||
+            dev::ws_create(S->ws, n, ncv, S->a.stream) != hipSuccess) {
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
+        if (csr) {
+            S->free_run = true;
+            S->csr = csr;
+        }
+        S->tol = *tol;
+        S->iparam = iparam;
+        S->ipntr = ipntr;
+        S->workl = workl;
+        S->root.emplace(S->run());
+        start_root(*S->root, S->ctx);
+        g_sym[v] = std::move(up);
+    } else {
+        auto it = g_sym.find(v);
+        if (it == g_sym.end()) {
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
+        S = it->second.get();
+        S->tol = *tol;  // the ICB passes tol by value on every call (SRC/icbads.F90:14)
+        S->iparam = iparam;
+        S->ipntr = ipntr;
+        S->workl = workl;
+        // bring the caller's results of the previous request into HBM
+        const RciReq& r = S->ctx.req;
+        if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
+            S->a.h2d_workd(r.y, n);
+            if (r.ido == 1 && S->mode == 2) S->a.h2d_workd(r.x, n);
+        }
+    }
+    for (;;) {
+        S->ctx.leaf.resume();
+        if (S->ctx.done) break;
+        const RciReq r = S->ctx.req;
+        if (S->free_run && (r.ido == -1 || r.ido == 1)) {
+            dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            continue;
+        }
+        // hand the request to the caller
+        if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
+            S->a.d2h_workd(r.x, n);
+            if (r.ido == 1 && r.bx >= 0 && S->mode >= 3) S->a.d2h_workd(r.bx, n);
+            ipntr[0] = (int)(r.x + 1);
+            ipntr[1] = (int)(r.y + 1);
+            if (r.bx >= 0) ipntr[2] = (int)(r.bx + 1);
+        }
+        S->a.sync();
+        *ido = r.ido;
+        return;
+    }
+    // ido = 99: dsaupd post-processing (SRC/dsaupd.f:613-627)
+    *ido = 99;
+    iparam[2] = S->mxiter;
+    iparam[4] = S->np;
+    iparam[8] = g_stats.nopx;
+    iparam[9] = g_stats.nbx;
+    iparam[10] = g_stats.nrorth;
+    int inf = S->info;
+    if (inf >= 0 && inf == 2) inf = 3;
+    *info = inf;
+    S->a.download_all();
+    S->a.sync();
+    g_sym.erase(v);
+}
+
+}  // namespace ahip
+
+using namespace ahip;
+
+extern "C" {
+
+void dsaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, double tol,
+              double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr, double* workd,
+              double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr);
+}
+
+void dsaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, double* tol,
+             double* resid, int* ncv, double* v, int* ldv, int* iparam, int* ipntr, double* workd,
+             double* workl, int* lworkl, int* info, size_t, size_t) {
+    sym_aupd(ido, bmat, *n, which, *nev, tol, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl,
+             *lworkl, info, nullptr);
+}
+
+void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, int* ido, char const* bmat, int n,
+                           char const* which, int nev, double tol, double* resid, int ncv,
+                           double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                           double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, ahip_csr_view(A));
+}
+
+void sstats_c(void) { g_stats = Stats{}; }
+
+void stat_c(int* nopx, int* nbx, int* nrorth, int* nitref, int* nrstrt, float* tsaupd,
+            float* tsaup2, float* tsaitr, float* tseigt, float* tsgets, float* tsapps,
+            float* tsconv, float* tnaupd, float* tnaup2, float* tnaitr, float* tneigh,
+            float* tngets, float* tnapps, float* tnconv, float* tcaupd, float* tcaup2,
+            float* tcaitr, float* tceigh, float* tcgets, float* tcapps, float* tcconv,
+            float* tmvopx, float* tmvbx, float* tgetv0, float* titref, float* trvec) {
+    *nopx = g_stats.nopx;
+    *nbx = g_stats.nbx;
+    *nrorth = g_stats.nrorth;
+    *nitref = g_stats.nitref;
+    *nrstrt = g_stats.nrstrt;
+    // the reference's default build links second_NONE.f: every timer reads 0
+    for (float* t : {tsaupd, tsaup2, tsaitr, tseigt, tsgets, tsapps, tsconv, tnaupd, tnaup2, tnaitr,
+                     tneigh, tngets, tnapps, tnconv, tcaupd, tcaup2, tcaitr, tceigh, tcgets, tcapps,
+                     tcconv, tmvopx, tmvbx, tgetv0, titref, trvec})
+        if (t) *t = 0.0f;
+}
+
+void debug_c(int, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
+             int, int, int, int, int, int, int) {
+    // message levels only affect printing (debug.h); printing is out of scope
+}
+
+const char* arpack_hip_version(void) { return "arpack-hip 0.1 (gfx950, arpack-ng 3.9.1 ICB)"; }
+
+int arpack_hip_device_count(void) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return c;
+}
+
+void arpack_hip_set_stream(void* stream) { g_stream = (hipStream_t)stream; }
+
+// ---- host kit exports (CPU-testable) ----
+int arpack_hip_kit_dstqrb(int n, double* d, double* e, double* z, double* work) {
+    return la::stqrb(n, d, e, z, work);
+}
+int arpack_hip_kit_dsteqr(int n, double* d, double* e, double* z, int ldz, double* work) {
+    return la::steqr(n, d, e, z, n, ldz, work, false);
+}
+void arpack_hip_kit_dlartg(double f, double g, double* c, double* s, double* r) {
+    la::lartg(f, g, *c, *s, *r);
+}
+void arpack_hip_kit_dsortr(char const* which, int apply, int n, double* x1, double* x2) {
+    la::dsortr(la::parse_which(which), apply != 0, n, x1, x2);
+}
+void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h, int ldh, double* q,
+                                int ldq) {
+    la::dsapps_host(kev, np, shift, h, ldh, q, ldq);
+}
+void arpack_hip_kit_dlarnv(int* iseed, int n, double* x) {
+    // host reference of the device generator (same arithmetic)
+    uint64_t s = seed48_from_iseed(iseed);
+    const uint64_t mask = (1ull << 48) - 1, a = 33952834046453ull;
+    for (int i = 0; i < n; ++i) {
+        s = (s * a) & mask;
+        x[i] = 2.0 * ((double)s * 0x1p-48) - 1.0;
+    }
+    iseed_from_seed48(s, iseed);
+}
+
+}  // extern "C"

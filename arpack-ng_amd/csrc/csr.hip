@@ -1,0 +1,280 @@
+// Device CSR operator (the `ido = +-1` user OP served on the GPU) and the
+// synthetic-operator generators used by the benchmarks and parity tests.
+//
+// Generators build the matrices directly in HBM (count -> exclusive scan ->
+// fill), deterministically from a counter-based hash, so the CPU baseline and
+// every GPU count see bit-identical operators (BASELINE.md §3 "Inputs").
+//
+//  laplace2d   5-pt 2-D Laplacian, m x m grid (EXAMPLES/SIMPLE/dssimp.f:484-538
+//              operator shape; `scale` = 1/h^2 = (m+1)^2 reproduces dssimp)
+//  laplace3d   7-pt 3-D Laplacian, m^3 (BASELINE config 4)
+//  banded_sym  the north-star symmetric CSR: pairs (i, i+d), 1 <= d < B, are
+//              present with probability per_row/4096 (~2*per_row nnz/row),
+//              off-diagonal values -k/4096 (k in 1..4096), diagonal
+//              -sum(offdiag) + U[0,16) on a 2^-8 grid.  All values are on
+//              power-of-two grids, so row sums are exact in any order and a
+//              row-block of the matrix generated on one GPU is bit-identical
+//              to the same rows generated anywhere else.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "device.hpp"
+#include "../../include/arpack_hip.h"
+
+struct arpack_hip_csr {
+    ahip::dev::Csr A;
+    int64_t* rowptr = nullptr;
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    int64_t row_begin = 0;  // global index of local row 0 (sharded generators)
+    int64_t ncols = 0;
+};
+
+namespace ahip::gen {
+
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t pair_hash(uint32_t seedmix, uint32_t a, uint32_t d) {
+    return mix32(mix32(a ^ seedmix) + d * 0x9E3779B9u);
+}
+__host__ __device__ __forceinline__ double offdiag_value(uint32_t h) {
+    return -(double)((mix32(h ^ 0x68e31da4u) >> 20) + 1u) * 0x1p-12;
+}
+__host__ __device__ __forceinline__ double diag_shift(uint32_t seed, uint32_t i) {
+    return (double)(mix32(i ^ mix32(seed ^ 0x5bd1e995u)) >> 20) * 0x1p-8;
+}
+
+// ---- banded symmetric (north star) -----------------------------------------
+__global__ void k_band_count(int64_t n, int64_t r0, int64_t r1, uint32_t seed, int B, int per_row,
+                             int64_t* __restrict__ cnt) {
+    const uint32_t sm = mix32(seed);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < r1 - r0; li += stride) {
+        const int64_t i = r0 + li;
+        int64_t c = 1;
+        for (int d = 1; d < B; ++d) {
+            if (i - d >= 0 && (pair_hash(sm, (uint32_t)(i - d), (uint32_t)d) >> 20) < (uint32_t)per_row) ++c;
+            if (i + d < n && (pair_hash(sm, (uint32_t)i, (uint32_t)d) >> 20) < (uint32_t)per_row) ++c;
+        }
+        cnt[li] = c;
+    }
+}
+
+__global__ void k_band_fill(int64_t n, int64_t r0, int64_t r1, uint32_t seed, int B, int per_row,
+                            const int64_t* __restrict__ rp, int32_t* __restrict__ col,
+                            double* __restrict__ val) {
+    const uint32_t sm = mix32(seed);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < r1 - r0; li += stride) {
+        const int64_t i = r0 + li;
+        int64_t k = rp[li];
+        double sum = 0.0;
+        for (int d = B - 1; d >= 1; --d) {  // lower part, increasing column
+            if (i - d < 0) continue;
+            const uint32_t h = pair_hash(sm, (uint32_t)(i - d), (uint32_t)d);
+            if ((h >> 20) < (uint32_t)per_row) {
+                const double v = offdiag_value(h);
+                col[k] = (int32_t)(i - d);
+                val[k] = v;
+                sum += v;
+                ++k;
+            }
+        }
+        const int64_t kd = k++;
+        for (int d = 1; d < B; ++d) {
+            if (i + d >= n) break;
+            const uint32_t h = pair_hash(sm, (uint32_t)i, (uint32_t)d);
+            if ((h >> 20) < (uint32_t)per_row) {
+                const double v = offdiag_value(h);
+                col[k] = (int32_t)(i + d);
+                val[k] = v;
+                sum += v;
+                ++k;
+            }
+        }
+        col[kd] = (int32_t)i;
+        val[kd] = -sum + diag_shift(seed, (uint32_t)i);
+    }
+}
+
+// ---- Laplacians -----------------------------------------------------------------
+__global__ void k_lap_count(int64_t m, int dim, int64_t* __restrict__ cnt) {
+    const int64_t n = dim == 2 ? m * m : m * m * m;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t x = i % m, y = (i / m) % m, z = dim == 3 ? i / (m * m) : 0;
+        int64_t c = 1 + (x > 0) + (x < m - 1) + (y > 0) + (y < m - 1);
+        if (dim == 3) c += (z > 0) + (z < m - 1);
+        cnt[i] = c;
+    }
+}
+
+__global__ void k_lap_fill(int64_t m, int dim, double scale, const int64_t* __restrict__ rp,
+                           int32_t* __restrict__ col, double* __restrict__ val) {
+    const int64_t n = dim == 2 ? m * m : m * m * m;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const double off = -1.0 * scale, dg = (dim == 2 ? 4.0 : 6.0) * scale;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t x = i % m, y = (i / m) % m, z = dim == 3 ? i / (m * m) : 0;
+        int64_t k = rp[i];
+        auto put = [&](int64_t j, double v) { col[k] = (int32_t)j; val[k] = v; ++k; };
+        if (dim == 3 && z > 0) put(i - m * m, off);
+        if (y > 0) put(i - m, off);
+        if (x > 0) put(i - 1, off);
+        put(i, dg);
+        if (x < m - 1) put(i + 1, off);
+        if (y < m - 1) put(i + m, off);
+        if (dim == 3 && z < m - 1) put(i + m * m, off);
+    }
+}
+
+}  // namespace ahip::gen
+
+namespace {
+
+int pick_group(int64_t n, int64_t nnz) {
+    const double avg = n > 0 ? (double)nnz / (double)n : 1.0;
+    if (avg <= 6) return 4;
+    if (avg <= 14) return 8;
+    if (avg <= 48) return 16;
+    if (avg <= 100) return 32;
+    return 64;
+}
+
+int grid_of(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    return (int)(g < 1 ? 1 : g);
+}
+
+// counts[0..rows) -> rowptr[0..rows] (exclusive scan, rowptr[rows] = nnz)
+int64_t scan_counts(int64_t rows, int64_t* counts_then_rowptr_tmp, int64_t* rowptr) {
+    void* tmp = nullptr;
+    size_t bytes = 0;
+    (void)hipMemset(counts_then_rowptr_tmp + rows, 0, sizeof(int64_t));
+    (void)hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1);
+    (void)hipMalloc(&tmp, bytes);
+    (void)hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(tmp);
+    int64_t nnz = 0;
+    (void)hipMemcpy(&nnz, rowptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost);
+    return nnz;
+}
+
+arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, int32_t* col, double* val) {
+    auto* A = new arpack_hip_csr;
+    A->rowptr = rp;
+    A->col = col;
+    A->val = val;
+    A->ncols = ncols;
+    A->A.n = rows;
+    A->A.nnz = nnz;
+    A->A.rowptr = rp;
+    A->A.col = col;
+    A->A.val = val;
+    A->A.group = pick_group(rows, nnz);
+    return A;
+}
+
+}  // namespace
+
+extern "C" {
+
+int arpack_hip_csr_create(arpack_hip_csr** out, int64_t n, int64_t nnz, const int64_t* rowptr,
+                          const int32_t* col, const double* val) {
+    int64_t* rp = nullptr;
+    int32_t* c = nullptr;
+    double* v = nullptr;
+    if (hipMalloc(&rp, sizeof(int64_t) * (n + 1)) || hipMalloc(&c, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) ||
+        hipMalloc(&v, sizeof(double) * (nnz > 0 ? nnz : 1)))
+        return -1;
+    (void)hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault);
+    if (nnz > 0) {
+        (void)hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault);
+        (void)hipMemcpy(v, val, sizeof(double) * nnz, hipMemcpyDefault);
+    }
+    *out = finish(n, n, nnz, rp, c, v);
+    return 0;
+}
+
+void arpack_hip_csr_destroy(arpack_hip_csr* A) {
+    if (!A) return;
+    (void)hipFree(A->rowptr);
+    (void)hipFree(A->col);
+    (void)hipFree(A->val);
+    delete A;
+}
+
+int arpack_hip_csr_info(const arpack_hip_csr* A, int64_t* n, int64_t* nnz) {
+    *n = A->A.n;
+    *nnz = A->A.nnz;
+    return 0;
+}
+
+int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* col, double* val) {
+    (void)hipMemcpy(rowptr, A->rowptr, sizeof(int64_t) * (A->A.n + 1), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(col, A->col, sizeof(int32_t) * A->A.nnz, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(val, A->val, sizeof(double) * A->A.nnz, hipMemcpyDeviceToHost);
+    return 0;
+}
+
+int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
+    ahip::dev::csr_spmv(nullptr, A->A, x, y);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale) {
+    const int64_t n = dim == 2 ? m * m : m * m * m;
+    int64_t *cnt = nullptr, *rp = nullptr;
+    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, cnt);
+    const int64_t nnz = scan_counts(n, cnt, rp);
+    (void)hipFree(cnt);
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, scale, rp, col,
+                       val);
+    (void)hipDeviceSynchronize();
+    *out = finish(n, n, nnz, rp, col, val);
+    return 0;
+}
+
+int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 2, scale); }
+int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 3, scale); }
+
+int arpack_hip_gen_banded_sym(arpack_hip_csr** out, int64_t n, int64_t r0, int64_t r1, uint32_t seed,
+                              int bandwidth, int per_row) {
+    if (r1 <= r0 || r1 > n || bandwidth < 2) return -1;
+    const int64_t rows = r1 - r0;
+    int64_t *cnt = nullptr, *rp = nullptr;
+    if (hipMalloc(&cnt, sizeof(int64_t) * (rows + 1)) || hipMalloc(&rp, sizeof(int64_t) * (rows + 1))) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_band_count, dim3(grid_of(rows)), dim3(256), 0, nullptr, n, r0, r1, seed,
+                       bandwidth, per_row, cnt);
+    const int64_t nnz = scan_counts(rows, cnt, rp);
+    (void)hipFree(cnt);
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_band_fill, dim3(grid_of(rows)), dim3(256), 0, nullptr, n, r0, r1, seed,
+                       bandwidth, per_row, rp, col, val);
+    (void)hipDeviceSynchronize();
+    *out = finish(rows, n, nnz, rp, col, val);
+    (*out)->row_begin = r0;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"
+
+const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A) { return &A->A; }

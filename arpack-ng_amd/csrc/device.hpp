@@ -1,0 +1,106 @@
+// Device (HBM-resident) half of the engine: launchers for the n-length kernels.
+//
+// Data layout in HBM:
+//   V      n x ncv, column-major, leading dimension ld (the caller's ldv in
+//          device-pointer mode, n rounded up to a multiple of 2 in host mode)
+//   resid  n, workd 3n (ARPACK slices ipj=0, irj=n, ivj=2n)
+//   part   nblk x stride doubles: per-block partial sums of the two-stage,
+//          fixed-order (hence bitwise reproducible) reductions
+//   LzState  the device-resident scalar state of the current Lanczos step:
+//          the DGKS decision (rnorm vs 0.717*wnorm, SRC/dsaitr.f:656,753) is
+//          taken ON THE DEVICE by the finalize kernel, so a whole restart
+//          cycle can be enqueued without a host round trip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ahip::dev {
+
+constexpr int kBlock = 256;
+constexpr int kMaxRedBlocks = 1024;
+
+// Scalar state of the current step j (device memory).
+struct LzState {
+    double rnorm;   // B-norm of the current residual (beta of the next step)
+    double wnorm;   // B-norm of OP*v_j
+    double alpha;   // h(j,2) being assembled (CGS coefficient + DGKS corrections)
+    double beta;    // h(j,1)
+    int dgks;       // 0: none pending, 1: first refinement pending, 2: second
+    int zero;       // residual must be zeroed (refinement failed twice)
+    int abort;      // rnorm == 0 at the start of step abort_j: host restart needed
+    int abort_j;
+    int nrorth;     // counters accumulated on device, drained by the host
+    int nitref;
+    int pad[2];
+};
+
+// Finalize phases (which logic the single-block finalize kernel applies).
+enum FinPhase : int {
+    kFinNorm = 0,     // st.rnorm = sqrt|w'u|                      (getv0, after V*Q)
+    kFinCgs = 1,      // coef0 = V'u, st.wnorm, st.alpha, st.beta  (SRC/dsaitr.f:551-594)
+    kFinPostCgs = 2,  // st.rnorm, DGKS decision, coef1 = V'r      (SRC/dsaitr.f:634-695)
+    kFinDgks1 = 3,    // first refinement check, coef2             (SRC/dsaitr.f:730-771)
+    kFinDgks2 = 4,    // second refinement check / give up         (SRC/dsaitr.f:753-781)
+    kFinRaw = 5,      // just store the sums (host reads them)
+    kFinCoef = 6,     // coef0 = first m-1 sums, state untouched   (getv0 CGS)
+};
+
+struct Workspace {
+    hipStream_t stream = nullptr;
+    int nblk = 0;        // partial-sum blocks for this n
+    int stride = 0;      // >= ncv + 2
+    double* part = nullptr;   // nblk * stride
+    double* sums = nullptr;   // stride (raw sums of the last finalize)
+    double* coef = nullptr;   // 3 * stride : CGS, DGKS-1, DGKS-2 coefficient vectors
+    double* rec = nullptr;    // 2 * (ncv+1): alpha_j, beta_j per step
+    double* q = nullptr;      // ncv * ncv  (V*Q matrix for dsapps / eupd)
+    LzState* st = nullptr;
+    LzState* st_host = nullptr;  // pinned mirror
+    double* host_scratch = nullptr;  // pinned, >= 4*stride doubles
+};
+
+int choose_nblk(int64_t n);
+hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s);
+void ws_destroy(Workspace& ws);
+
+// v_j = r / rnorm -> V(:,j) (+ optional copies); aborts the cycle if rnorm==0.
+void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double* copy1,
+           double* scale_inplace, int j);
+// partial sums of [V(:,0:j)' u ; w' u]  (w == u allowed); gate=-1: always,
+// else only if st.dgks == gate.
+void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
+          const double* w, int gate);
+// rout = rin - V(:,0:j) * coef[which]; if spec: partials of [V' rout ; rout' rout]
+void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
+            const double* rin, double* rout, bool spec, int gate);
+// single-block fixed-order finalize of m = j+1 sums and the phase logic
+void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate);
+// resid = 0 if st.zero
+void zero_if(const Workspace& ws, int64_t n, double* r);
+// V(:,0:kev) = V(:,0:kplusp) * Q(:,0:kev) in place (row-local) and
+// r = sigmak*r + betak*Vnew(:,kev); partial r'r for the new rnorm.
+void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp, int kev,
+               double sigmak, double betak, double* r);
+// Z(:,0:nz) = V(:,0:k) * M(k x nz) (M in ws.q, ld k); Z may alias V.
+void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k, int nz,
+             double* Z, int64_t ldz);
+// dlarnv(idist=2) continuation: x[m] = 2*(seed*a^(m+1) mod 2^48)/2^48 - 1
+void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x);
+void copy(hipStream_t s, int64_t n, const double* src, double* dst);
+void scal(hipStream_t s, int64_t n, double a, double* x);
+void fill(hipStream_t s, int64_t n, double a, double* x);
+// y = alpha*y + beta*x
+void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const double* x);
+
+// ------------------------------- CSR operator --------------------------------
+struct Csr {
+    int64_t n = 0, nnz = 0;
+    const int64_t* rowptr = nullptr;  // n+1
+    const int32_t* col = nullptr;     // nnz
+    const double* val = nullptr;      // nnz
+    int group = 16;                   // lanes per row for the vector kernel
+};
+void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y);
+
+}  // namespace ahip::dev

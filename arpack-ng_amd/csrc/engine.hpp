@@ -1,0 +1,108 @@
+// Engine internals shared by the symmetric solver, the post-processing and the
+// C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <optional>
+
+#include "dense.hpp"
+#include "device.hpp"
+#include "rci.hpp"
+
+namespace ahip {
+
+// /timing/ common-block counters (stat.h:8-21); the timers of the reference
+// are dead in its default build (UTIL/second_NONE.f:31) and are reported as 0.
+struct Stats {
+    int nopx = 0, nbx = 0, nrorth = 0, nitref = 0, nrstrt = 0;
+};
+extern Stats g_stats;
+
+// dgetv0's process-wide SAVEd LAPACK seed (SRC/dgetv0.f:202-208), kept as the
+// 48-bit integer the four base-4096 digits encode.
+extern uint64_t g_dseed;
+uint64_t seed48_from_iseed(const int iseed[4]);
+void iseed_from_seed48(uint64_t s, int iseed[4]);
+uint64_t lcg_advance(uint64_t seed, uint64_t steps);  // seed * a^steps mod 2^48
+
+// Caller-visible arrays in one place. `dev_*` are what the kernels use: the
+// caller's own buffers in device-pointer mode, engine-owned mirrors in
+// host-pointer mode.
+struct Arrays {
+    bool host_mode = true;
+    int64_t n = 0;
+    int ncv = 0;
+    double* h_resid = nullptr;
+    double* h_v = nullptr;
+    int h_ldv = 0;
+    double* h_workd = nullptr;
+    double* d_resid = nullptr;
+    double* d_v = nullptr;
+    int64_t d_ld = 0;
+    double* d_workd = nullptr;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+
+    // fails with a negative code if pointer kinds are mixed
+    int attach(int64_t n, int ncv, double* resid, double* v, int ldv, double* workd);
+    void release();
+    void upload_resid();
+    void download_all();           // V, resid, workd -> caller (host mode)
+    void d2h_workd(int64_t off, int64_t len);
+    void h2d_workd(int64_t off, int64_t len);
+    void sync();
+};
+
+bool is_device_pointer(const void* p);
+hipStream_t default_stream();  // set through arpack_hip_set_stream()
+
+// Symmetric implicitly restarted Lanczos (dsaupd family).
+class SymSolver {
+public:
+    // configuration fixed at ido == 0 (SRC/dsaupd.f:473-596)
+    char bmat = 'I';
+    la::Which which = la::Which::LM;
+    int n = 0, ncv = 0, mode = 1, ishift = 1, mxiter = 0;
+    int nev0 = 0, np = 0;     // dsaupd's nev0 / np (updated by the loop)
+    int lworkl = 0;
+    // per-call
+    double tol = 0.0;
+    int* iparam = nullptr;
+    int* ipntr = nullptr;
+    double* workl = nullptr;   // host view of the caller's workl
+    int info = 0;
+
+    Arrays a;
+    dev::Workspace ws;
+    RciCtx ctx;
+    std::optional<Task> root;
+
+    // free-running mode (arpack_hip_dsaupd_csr): OP requests are served by
+    // an on-device CSR operator without returning to the caller.
+    bool free_run = false;
+    const dev::Csr* csr = nullptr;
+
+    // workl offsets (0-based) of h, ritz, bounds, q, w
+    int ih = 0, iritz = 0, ibounds = 0, iq = 0, iw = 0;
+    double rnorm = 0.0;  // host copy of dsaup2's rnorm
+
+    ~SymSolver();
+    Task run();
+
+private:
+    Task getv0(bool initv, int j, int itry, int& ierr);
+    Task saitr(int k, int npk, int& iinfo);
+    void sapps(int kev, int npk);
+    RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
+    RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp);
+    void read_state();
+    void write_state();
+    double* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
+public:
+    const double* op_x = nullptr;  // device pointers of the pending OP request
+    double* op_y = nullptr;
+};
+
+}  // namespace ahip

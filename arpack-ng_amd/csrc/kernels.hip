@@ -1,0 +1,624 @@
+// HIP kernels (gfx950 / CDNA4) for the n-length half of the IRL/IRA cycle.
+//
+// All of these are HBM-bandwidth bound (<= 2 flop/byte): the
+// design goal is one coalesced pass over V per Gram-Schmidt sweep, with every
+// reduction done as per-block partials (fixed order, no float atomics, so the
+// result is bitwise reproducible run to run) plus a single-block finalize.
+//
+//   place      v_j = r/rnorm                          SRC/dsaitr.f:438-464
+//   dots       [V' u ; w' u]   (CGS coefficients)     SRC/dsaitr.f:551-575
+//   update     r = r - V c, fused with the DGKS        SRC/dsaitr.f:582-583,
+//              coefficients [V' r ; r' r] of the       680-692 (speculative: the
+//              NEXT sweep, which the reference takes   reference re-orthogonalises
+//              in ~99.8% of steps)                     in 430 of 431 steps)
+//   finalize   partial sums -> scalars + the DGKS decision (0.717 rule)
+//   vq_update  V <- V*Q, r <- sigma*r + beta*v_{kev+1} SRC/dsapps.f:450-493
+//   larnv      dlarnv(idist=2) continuation on device  SRC/dgetv0.f:234-236
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "device.hpp"
+
+namespace ahip::dev {
+
+namespace {
+
+constexpr double kSafminD = DBL_MIN;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Reduce CH per-thread accumulators over the block and write them (plus an
+// optional extra value) as this block's partial row.
+template <int CH>
+__device__ __forceinline__ void block_partials(double (&acc)[CH], int jc, double extra,
+                                               bool with_extra, double* prow, int extra_slot) {
+    __shared__ double red[kBlock / 64][CH + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        if (k < jc) {
+            const double s = wave_sum(acc[k]);
+            if (lane == 0) red[wave][k] = s;
+        }
+    }
+    if (with_extra) {
+        const double s = wave_sum(extra);
+        if (lane == 0) red[wave][CH] = s;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < jc) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w][t];
+        prow[t] = s;
+    }
+    if (with_extra && t == kBlock - 1) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w][CH];
+        prow[extra_slot] = s;
+    }
+}
+
+__device__ __forceinline__ bool gate_closed(const LzState* st, int gate) {
+    if (st->abort) return true;
+    return gate >= 0 && st->dgks != gate;
+}
+
+// ------------------------------------------------------------------ place ---
+__global__ __launch_bounds__(kBlock) void k_place(int64_t n, const double* __restrict__ r,
+                                                  double* __restrict__ vcol,
+                                                  double* __restrict__ copy1,
+                                                  double* __restrict__ sc,
+                                                  LzState* __restrict__ st, int j) {
+    if (st->abort) return;
+    const double rn = st->rnorm;
+    if (!(rn > 0.0)) {  // invariant subspace: restart needed (SRC/dsaitr.f:378)
+        if (blockIdx.x == 0 && threadIdx.x == 0) { st->abort = 1; st->abort_j = j; }
+        return;
+    }
+    // v = r * (1/rnorm), or dlascl's careful factors when rnorm < safmin
+    double m0 = 1.0 / rn, m1 = 1.0, m2 = 1.0;
+    if (rn < kSafminD) {
+        // dlascl('G', cfrom=rn, cto=1): rn*safmin underflows, so scale up first
+        const double big = 1.0 / kSafminD;
+        m0 = big;
+        const double c2 = rn * big;
+        m1 = 1.0 / c2;
+        m2 = 1.0;
+    }
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const double v = r[i] * m0 * m1 * m2;
+        vcol[i] = v;
+        if (copy1) copy1[i] = v;
+        if (sc) sc[i] = sc[i] * m0 * m1 * m2;
+    }
+}
+
+// ------------------------------------------------------------------- dots ---
+template <int CH>
+__global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, int jc,
+                                                 const double* __restrict__ V, int64_t ld,
+                                                 const double* __restrict__ u,
+                                                 const double* __restrict__ w, int same,
+                                                 int with_w, double* __restrict__ part,
+                                                 int pstride, int wslot,
+                                                 const LzState* __restrict__ st, int gate) {
+    if (gate_closed(st, gate)) return;
+    double acc[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) acc[k] = 0.0;
+    double aw = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const double* Vb = V + (int64_t)j0 * ld;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const double ui = u[i];
+        if (with_w) aw += (same ? ui : w[i]) * ui;
+#pragma unroll
+        for (int k = 0; k < CH; ++k)
+            if (k < jc) acc[k] += Vb[i + (int64_t)k * ld] * ui;
+    }
+    block_partials<CH>(acc, jc, aw, with_w != 0, part + (int64_t)blockIdx.x * pstride + j0,
+                       wslot - j0);
+}
+
+// ----------------------------------------------------------------- update ---
+// rout = rin - V(:,0:j) c ; spec: partials of [V' rout ; rout' rout]
+template <int CH>
+__global__ __launch_bounds__(kBlock) void k_update_fused(
+    int64_t n, int j, const double* __restrict__ V, int64_t ld, const double* __restrict__ c,
+    const double* rin, double* rout, int spec, double* __restrict__ part, int pstride,
+    const LzState* __restrict__ st, int gate) {
+    if (gate_closed(st, gate)) return;
+    double acc[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) acc[k] = 0.0;
+    double rr = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double vrow[CH];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            vrow[k] = (k < j) ? V[i + (int64_t)k * ld] : 0.0;
+            if (k < j) s += vrow[k] * c[k];
+        }
+        const double r = rin[i] - s;
+        rout[i] = r;
+        if (spec) {
+            rr += r * r;
+#pragma unroll
+            for (int k = 0; k < CH; ++k)
+                if (k < j) acc[k] += vrow[k] * r;
+        }
+    }
+    if (spec) block_partials<CH>(acc, j, rr, true, part + (int64_t)blockIdx.x * pstride, j);
+}
+
+// generic (any j): no fused dots
+__global__ __launch_bounds__(kBlock) void k_update_generic(int64_t n, int j,
+                                                           const double* __restrict__ V,
+                                                           int64_t ld,
+                                                           const double* __restrict__ c,
+                                                           const double* rin, double* rout,
+                                                           const LzState* __restrict__ st,
+                                                           int gate) {
+    if (gate_closed(st, gate)) return;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double s = 0.0;
+        for (int k = 0; k < j; ++k) s += V[i + (int64_t)k * ld] * c[k];
+        rout[i] = rin[i] - s;
+    }
+}
+
+// --------------------------------------------------------------- finalize ---
+__global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
+                                                   int pstride, int m, int phase, int j,
+                                                   int rstart, int gate, double* __restrict__ sums,
+                                                   double* __restrict__ coef, int cstride,
+                                                   double* __restrict__ rec,
+                                                   LzState* __restrict__ st) {
+    if (gate_closed(st, gate)) return;
+    __shared__ double s_sum[256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int k = wave; k < m; k += 16) {
+        double s = 0.0;
+        for (int b = lane; b < nblk; b += 64) s += part[(int64_t)b * pstride + k];
+        s = wave_sum(s);
+        if (lane == 0) s_sum[k] = s;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < m) sums[t] = s_sum[t];
+    const int jm = m - 1;  // index of the w'u / r'r slot
+    if (phase == kFinCgs) {
+        if (t < jm) coef[t] = s_sum[t];
+        if (t == 0) {
+            st->zero = 0;
+            st->dgks = 0;
+            st->wnorm = sqrt(fabs(s_sum[jm]));
+            st->alpha = s_sum[jm - 1];
+            st->beta = (j == 1 || rstart) ? 0.0 : st->rnorm;
+            rec[2 * (j - 1)] = st->alpha;
+            rec[2 * (j - 1) + 1] = st->beta;
+        }
+        return;
+    }
+    if (phase == kFinNorm) {
+        if (t == 0) st->rnorm = sqrt(fabs(s_sum[jm]));
+        return;
+    }
+    if (phase == kFinRaw) return;
+    if (phase == kFinCoef) {
+        if (t < jm) coef[t] = s_sum[t];
+        return;
+    }
+    // refinement phases share the "speculative coefficients" layout
+    __shared__ int s_take;
+    if (t == 0) {
+        const double rn = sqrt(fabs(s_sum[jm]));
+        int take = 0;  // 1: store next-sweep coefficients into coef slot
+        if (phase == kFinPostCgs) {
+            st->rnorm = rn;
+            if (rn > 0.717 * st->wnorm) {
+                st->dgks = 0;
+            } else {
+                st->dgks = 1;
+                st->nrorth += 1;
+                take = 1;
+            }
+        } else if (phase == kFinDgks1) {
+            if (rn > 0.717 * st->rnorm) {
+                st->rnorm = rn;
+                st->dgks = 0;
+            } else {
+                st->nitref += 1;
+                st->rnorm = rn;
+                st->dgks = 2;
+                take = 2;
+            }
+        } else {  // kFinDgks2
+            if (rn > 0.717 * st->rnorm) {
+                st->rnorm = rn;
+            } else {
+                st->nitref += 1;
+                st->zero = 1;
+                st->rnorm = 0.0;
+            }
+            st->dgks = 0;
+        }
+        if (take) {
+            st->alpha += s_sum[jm - 1];
+            if (j == 1 || rstart) st->beta = 0.0;
+        }
+        rec[2 * (j - 1)] = st->alpha;
+        rec[2 * (j - 1) + 1] = st->beta;
+        s_take = take;
+    }
+    __syncthreads();
+    const int take = s_take;
+    if (take && t < jm) coef[take * cstride + t] = s_sum[t];
+}
+
+__global__ void k_zero_if(int64_t n, double* r, const LzState* st) {
+    if (st->abort || !st->zero) return;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) r[i] = 0.0;
+}
+
+// -------------------------------------------------------------- V*Q update --
+template <int MAXK>
+__global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, double* V, int64_t ld,
+                                                      int kplusp, int kev,
+                                                      const double* __restrict__ Q, int ldq,
+                                                      double sigmak, double betak,
+                                                      double* __restrict__ r,
+                                                      double* __restrict__ part, int pstride) {
+    double rr = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const bool next = betak > 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double v[MAXK];
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) v[k] = (k < kplusp) ? V[i + (int64_t)k * ld] : 0.0;
+        double vnext = 0.0;
+        if (next) {
+#pragma unroll
+            for (int k = 0; k < MAXK; ++k)
+                if (k < kplusp) vnext += v[k] * Q[k + (int64_t)kev * ldq];
+        }
+        for (int l = 0; l < kev; ++l) {
+            double o = 0.0;
+#pragma unroll
+            for (int k = 0; k < MAXK; ++k)
+                if (k < kplusp) o += v[k] * Q[k + (int64_t)l * ldq];
+            V[i + (int64_t)l * ld] = o;
+        }
+        double ri = sigmak * r[i];
+        if (next) {
+            V[i + (int64_t)kev * ld] = vnext;
+            ri += betak * vnext;
+        }
+        r[i] = ri;
+        rr += ri * ri;
+    }
+    double acc[1] = {0.0};
+    block_partials<1>(acc, 0, rr, true, part + (int64_t)blockIdx.x * pstride, 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_vq_update_generic(
+    int64_t n, double* V, int64_t ld, int kplusp, int kev, const double* __restrict__ Q,
+    int ldq, double sigmak, double betak, double* __restrict__ r, double* __restrict__ tmp,
+    double* __restrict__ part, int pstride) {
+    // tmp: n x (kev+1) scratch (column-major, ld n) — used when kplusp > 64
+    double rr = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const bool next = betak > 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        for (int l = 0; l <= kev; ++l) {
+            double o = 0.0;
+            for (int k = 0; k < kplusp; ++k) o += V[i + (int64_t)k * ld] * Q[k + (int64_t)l * ldq];
+            tmp[i + (int64_t)l * n] = o;
+        }
+        for (int l = 0; l < kev; ++l) V[i + (int64_t)l * ld] = tmp[i + (int64_t)l * n];
+        double ri = sigmak * r[i];
+        if (next) {
+            const double vn = tmp[i + (int64_t)kev * n];
+            V[i + (int64_t)kev * ld] = vn;
+            ri += betak * vn;
+        }
+        r[i] = ri;
+        rr += ri * ri;
+    }
+    double acc[1] = {0.0};
+    block_partials<1>(acc, 0, rr, true, part + (int64_t)blockIdx.x * pstride, 0);
+}
+
+// Z = V(:,0:k) * M(k x nz) ; row-local, so Z may alias V (rows held in registers)
+template <int MAXK>
+__global__ __launch_bounds__(kBlock) void k_vq_gemm(int64_t n, const double* V, int64_t ld,
+                                                    int k, int nz, const double* __restrict__ M,
+                                                    double* Z, int64_t ldz) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double v[MAXK];
+#pragma unroll
+        for (int t = 0; t < MAXK; ++t) v[t] = (t < k) ? V[i + (int64_t)t * ld] : 0.0;
+        for (int l = 0; l < nz; ++l) {
+            double o = 0.0;
+#pragma unroll
+            for (int t = 0; t < MAXK; ++t)
+                if (t < k) o += v[t] * M[t + (int64_t)l * k];
+            Z[i + (int64_t)l * ldz] = o;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ larnv ---
+// 48-bit multiplicative congruential generator of LAPACK dlaruv:
+// x_{m} = seed * a^m mod 2^48, a = 33952834046453; dlarnv(idist=2) returns
+// 2*x/2^48 - 1 (exact in double: 48 bits < 53).
+constexpr uint64_t kLcgA = 33952834046453ull;
+constexpr uint64_t kMask48 = (1ull << 48) - 1;
+
+__device__ __forceinline__ uint64_t mulmod48(uint64_t a, uint64_t b) { return (a * b) & kMask48; }
+
+__global__ void k_larnv(int64_t n, uint64_t seed, double* __restrict__ x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        // a^(i+1) by square-and-multiply
+        uint64_t e = (uint64_t)i + 1, base = kLcgA, p = 1;
+        while (e) {
+            if (e & 1) p = mulmod48(p, base);
+            base = mulmod48(base, base);
+            e >>= 1;
+        }
+        const uint64_t xm = mulmod48(seed, p);
+        x[i] = 2.0 * ((double)xm * 0x1p-48) - 1.0;
+    }
+}
+
+// ------------------------------------------------------------ elementwise ---
+__global__ void k_copy(int64_t n, const double* __restrict__ s, double* __restrict__ d) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] = s[i];
+}
+__global__ void k_scal(int64_t n, double a, double* x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= a;
+}
+__global__ void k_fill(int64_t n, double a, double* x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a;
+}
+__global__ void k_axpby(int64_t n, double alpha, double* y, double beta, const double* x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        y[i] = alpha * y[i] + beta * x[i];
+}
+
+// ---------------------------------------------------------------- CSR SpMV ---
+// Vector kernel: G lanes per row (G | 64); lane k walks entries k, k+G, ...
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_csr_vector(int64_t n, const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const double* __restrict__ x,
+                                                       double* __restrict__ y) {
+    const int lane = threadIdx.x % G;
+    const int64_t rows_per_block = kBlock / G;
+    const int64_t stride = (int64_t)gridDim.x * rows_per_block;
+    for (int64_t row = (int64_t)blockIdx.x * rows_per_block + threadIdx.x / G; row < n;
+         row += stride) {
+        const int64_t b = rp[row], e = rp[row + 1];
+        double s = 0.0;
+        for (int64_t k = b + lane; k < e; k += G) s += val[k] * x[col[k]];
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, G);
+        if (lane == 0) y[row] = s;
+    }
+}
+
+__global__ void k_ger_cols(int64_t n, int k, const double* __restrict__ x,
+                           const double* __restrict__ w, double* Z, int64_t ldz) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double xi = x[i];
+        for (int l = 0; l < k; ++l) Z[i + (int64_t)l * ldz] += xi * w[l];
+    }
+}
+
+inline int grid_for(int64_t n, int per_block = kBlock, int cap = 8192) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+}  // namespace
+
+// ================================================================ launchers ==
+
+int choose_nblk(int64_t n) {
+    int64_t b = (n + kBlock - 1) / kBlock;
+    if (b > kMaxRedBlocks) b = kMaxRedBlocks;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
+    ws.stream = s;
+    ws.nblk = choose_nblk(n);
+    ws.stride = ncv + 2;
+    hipError_t e;
+    if ((e = hipMalloc(&ws.part, sizeof(double) * (size_t)ws.nblk * ws.stride))) return e;
+    if ((e = hipMalloc(&ws.sums, sizeof(double) * (size_t)ws.stride))) return e;
+    if ((e = hipMalloc(&ws.coef, sizeof(double) * 3 * (size_t)ws.stride))) return e;
+    if ((e = hipMalloc(&ws.rec, sizeof(double) * 2 * (size_t)(ncv + 1)))) return e;
+    if ((e = hipMalloc(&ws.q, sizeof(double) * (size_t)ncv * ncv))) return e;
+    if ((e = hipMalloc(&ws.st, sizeof(LzState)))) return e;
+    if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
+    if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
+        return e;
+    (void)hipMemsetAsync(ws.st, 0, sizeof(LzState), s);
+    memset(ws.st_host, 0, sizeof(LzState));
+    (void)hipMemsetAsync(ws.coef, 0, sizeof(double) * 3 * (size_t)ws.stride, s);
+    return hipSuccess;
+}
+
+void ws_destroy(Workspace& ws) {
+    if (ws.part) (void)hipFree(ws.part);
+    if (ws.sums) (void)hipFree(ws.sums);
+    if (ws.coef) (void)hipFree(ws.coef);
+    if (ws.rec) (void)hipFree(ws.rec);
+    if (ws.q) (void)hipFree(ws.q);
+    if (ws.st) (void)hipFree(ws.st);
+    if (ws.st_host) (void)hipHostFree(ws.st_host);
+    if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
+    ws = Workspace{};
+}
+
+void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double* copy1,
+           double* sc, int j) {
+    hipLaunchKernelGGL(k_place, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
+                       sc, ws.st, j);
+}
+
+template <int CH>
+static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const double* V,
+                        int64_t ld, const double* u, const double* w, int with_w, int wslot,
+                        int gate) {
+    hipLaunchKernelGGL(k_dots<CH>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j0, jc, V, ld, u,
+                       w, (int)(w == u), with_w, ws.part, ws.stride, wslot, ws.st, gate);
+}
+
+void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
+          const double* w, int gate) {
+    if (j == 0) {
+        launch_dots<1>(ws, n, 0, 0, V, ld, u, w, 1, 0, gate);
+        return;
+    }
+    for (int j0 = 0; j0 < j; j0 += 32) {
+        const int jc = (j - j0 < 32) ? j - j0 : 32;
+        const int ww = (j0 == 0) ? 1 : 0;
+        if (jc <= 8) launch_dots<8>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
+        else if (jc <= 16) launch_dots<16>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
+        else launch_dots<32>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
+    }
+}
+
+void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
+            const double* rin, double* rout, bool spec, int gate) {
+    const double* c = ws.coef + (size_t)which * ws.stride;
+    const int sp = spec ? 1 : 0;
+    if (j <= 8) {
+        hipLaunchKernelGGL(k_update_fused<8>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V, ld,
+                           c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
+    } else if (j <= 16) {
+        hipLaunchKernelGGL(k_update_fused<16>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V,
+                           ld, c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
+    } else if (j <= 32) {
+        hipLaunchKernelGGL(k_update_fused<32>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V,
+                           ld, c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
+    } else {
+        hipLaunchKernelGGL(k_update_generic, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V, ld,
+                           c, rin, rout, ws.st, gate);
+        if (spec) dots(ws, n, j, V, ld, rout, rout, gate);
+    }
+}
+
+void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, ws.stride, m,
+                       (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
+}
+
+void zero_if(const Workspace& ws, int64_t n, double* r) {
+    hipLaunchKernelGGL(k_zero_if, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
+}
+
+void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp, int kev,
+               double sigmak, double betak, double* r) {
+    const int g = ws.nblk;
+    if (kplusp <= 16)
+        hipLaunchKernelGGL(k_vq_update<16>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
+                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+    else if (kplusp <= 32)
+        hipLaunchKernelGGL(k_vq_update<32>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
+                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+    else if (kplusp <= 64)
+        hipLaunchKernelGGL(k_vq_update<64>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
+                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+    else {
+        double* tmp = nullptr;
+        (void)hipMallocAsync(&tmp, sizeof(double) * (size_t)n * (kev + 1), ws.stream);
+        hipLaunchKernelGGL(k_vq_update_generic, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp,
+                           kev, ws.q, kplusp, sigmak, betak, r, tmp, ws.part, ws.stride);
+        (void)hipFreeAsync(tmp, ws.stream);
+    }
+}
+
+void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k, int nz, double* Z,
+             int64_t ldz) {
+    const int g = grid_for(n);
+    if (k <= 16)
+        hipLaunchKernelGGL(k_vq_gemm<16>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
+                           ldz);
+    else if (k <= 32)
+        hipLaunchKernelGGL(k_vq_gemm<32>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
+                           ldz);
+    else if (k <= 64)
+        hipLaunchKernelGGL(k_vq_gemm<64>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
+                           ldz);
+    else
+        hipLaunchKernelGGL(k_vq_gemm<128>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
+                           ldz);
+}
+
+void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x) {
+    hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, x);
+}
+
+void copy(hipStream_t s, int64_t n, const double* src, double* dst) {
+    hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, src, dst);
+}
+void scal(hipStream_t s, int64_t n, double a, double* x) {
+    hipLaunchKernelGGL(k_scal, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+}
+void fill(hipStream_t s, int64_t n, double a, double* x) {
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+}
+void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const double* x) {
+    hipLaunchKernelGGL(k_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, n, alpha, y, beta, x);
+}
+
+void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
+              int64_t ldz) {
+    hipLaunchKernelGGL(k_ger_cols, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
+}
+
+void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    const int G = A.group;
+    const int rows_per_block = kBlock / G;
+    int64_t g = (A.n + rows_per_block - 1) / rows_per_block;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    switch (G) {
+        case 4: hipLaunchKernelGGL(k_csr_vector<4>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 8: hipLaunchKernelGGL(k_csr_vector<8>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 16: hipLaunchKernelGGL(k_csr_vector<16>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 32: hipLaunchKernelGGL(k_csr_vector<32>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        default: hipLaunchKernelGGL(k_csr_vector<64>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+    }
+}
+
+}  // namespace ahip::dev

@@ -1,0 +1,472 @@
+// Symmetric implicitly restarted Lanczos: the dsaupd -> dsaup2 -> dsaitr /
+// dgetv0 / dsapps control flow, re-hosted as coroutines that drive the HIP
+// kernels of kernels.hip.  Host work is O(ncv^2) per restart cycle; all
+// n-length data stays in HBM.
+//
+// Reference map:
+//   SymSolver::run    SRC/dsaupd.f:408-690 + SRC/dsaup2.f:179-851
+//   SymSolver::saitr  SRC/dsaitr.f:204-853   (Lanczos steps, CGS + DGKS)
+//   SymSolver::getv0  SRC/dgetv0.f:119-421   (start / restart vector)
+//   SymSolver::sapps  SRC/dsapps.f:131-518   (shifts on T host-side, V*Q on device)
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace ahip {
+
+namespace {
+inline void ck(hipError_t e) { (void)e; }
+}  // namespace
+
+// ------------------------------------------------------------------ Arrays ---
+
+bool is_device_pointer(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+int Arrays::attach(int64_t nn, int nc, double* resid, double* v, int ldv, double* workd) {
+    n = nn;
+    ncv = nc;
+    const bool dr = is_device_pointer(resid), dv = is_device_pointer(v), dw = is_device_pointer(workd);
+    if (dr != dv || dv != dw) return -1;
+    host_mode = !dr;
+    h_resid = resid;
+    h_v = v;
+    h_ldv = ldv;
+    h_workd = workd;
+    stream = default_stream();
+    if (!stream) {
+        ck(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        own_stream = true;
+    }
+    if (host_mode) {
+        d_ld = (n + 1) & ~int64_t(1);
+        if (hipMalloc(&d_v, sizeof(double) * (size_t)d_ld * ncv) != hipSuccess) return -2;
+        if (hipMalloc(&d_resid, sizeof(double) * (size_t)n) != hipSuccess) return -2;
+        if (hipMalloc(&d_workd, sizeof(double) * 3 * (size_t)n) != hipSuccess) return -2;
+        ck(hipMemsetAsync(d_v, 0, sizeof(double) * (size_t)d_ld * ncv, stream));
+        ck(hipMemsetAsync(d_workd, 0, sizeof(double) * 3 * (size_t)n, stream));
+        ck(hipMemsetAsync(d_resid, 0, sizeof(double) * (size_t)n, stream));
+    } else {
+        d_v = v;
+        d_ld = ldv;
+        d_resid = resid;
+        d_workd = workd;
+    }
+    return 0;
+}
+
+void Arrays::release() {
+    if (host_mode) {
+        if (d_v) ck(hipFree(d_v));
+        if (d_resid) ck(hipFree(d_resid));
+        if (d_workd) ck(hipFree(d_workd));
+    }
+    if (own_stream && stream) ck(hipStreamDestroy(stream));
+    d_v = d_resid = d_workd = nullptr;
+    stream = nullptr;
+    own_stream = false;
+}
+
+void Arrays::upload_resid() {
+    if (host_mode) ck(hipMemcpyAsync(d_resid, h_resid, sizeof(double) * n, hipMemcpyHostToDevice, stream));
+}
+
+void Arrays::d2h_workd(int64_t off, int64_t len) {
+    if (host_mode && off >= 0)
+        ck(hipMemcpyAsync(h_workd + off, d_workd + off, sizeof(double) * len, hipMemcpyDeviceToHost, stream));
+}
+
+void Arrays::h2d_workd(int64_t off, int64_t len) {
+    if (host_mode && off >= 0)
+        ck(hipMemcpyAsync(d_workd + off, h_workd + off, sizeof(double) * len, hipMemcpyHostToDevice, stream));
+}
+
+void Arrays::download_all() {
+    if (!host_mode) return;
+    ck(hipMemcpy2DAsync(h_v, sizeof(double) * h_ldv, d_v, sizeof(double) * d_ld, sizeof(double) * n, ncv,
+                        hipMemcpyDeviceToHost, stream));
+    ck(hipMemcpyAsync(h_resid, d_resid, sizeof(double) * n, hipMemcpyDeviceToHost, stream));
+    ck(hipMemcpyAsync(h_workd, d_workd, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, stream));
+}
+
+void Arrays::sync() { ck(hipStreamSynchronize(stream)); }
+
+// ------------------------------------------------------------- SymSolver ---
+
+SymSolver::~SymSolver() {
+    root.reset();
+    dev::ws_destroy(ws);
+    a.release();
+}
+
+RciAwait SymSolver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
+    op_x = nullptr;
+    op_y = nullptr;
+    return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+RciAwait SymSolver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp) {
+    op_x = xp;
+    op_y = yp;
+    return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+void SymSolver::read_state() {
+    ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
+    a.sync();
+}
+
+void SymSolver::write_state() {
+    ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
+}
+
+// dgetv0: generate (or take) a start vector, force it into range(OP), and for
+// j > 1 B-orthogonalise it against V(:,1:j-1) with <= 5 refinement sweeps.
+// On exit st.rnorm and this->rnorm hold its B-norm.
+Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
+    const int64_t nn = n;
+    double* wd = a.d_workd;
+    ierr = 0;
+    if (!initv) {  // dlarnv(idist=2, iseed, n, resid) — SRC/dgetv0.f:234-237
+        dev::larnv_uniform(ws, nn, g_dseed, a.d_resid);
+        g_dseed = lcg_advance(g_dseed, (uint64_t)nn);
+    }
+    if (itry == 1) {  // force into the range of OP (SRC/dgetv0.f:245-251)
+        g_stats.nopx += 1;
+        dev::copy(a.stream, nn, a.d_resid, wd);
+        co_await op(-1, 0, nn, -1, wd, wd + nn);
+        dev::copy(a.stream, nn, wd + nn, a.d_resid);
+    } else if (bmat == 'G') {
+        dev::copy(a.stream, nn, a.d_resid, wd + nn);
+    }
+    // B-norm of the start vector (SRC/dgetv0.f:279-306)
+    if (bmat == 'G') {
+        g_stats.nbx += 1;
+        if (itry == 1) dev::copy(a.stream, nn, a.d_resid, wd + nn);
+        co_await rci(2, nn, 0);
+    } else {
+        dev::copy(a.stream, nn, a.d_resid, wd);
+    }
+    ws.st_host->abort = 0;
+    write_state();
+    dev::dots(ws, nn, 0, a.d_v, a.d_ld, wd, a.d_resid, -1);
+    dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+    read_state();
+    double rnorm0 = ws.st_host->rnorm;
+    rnorm = rnorm0;
+    if (j == 1) co_return;
+
+    // iterative classical Gram-Schmidt against V(:,1:j-1) (SRC/dgetv0.f:326-397)
+    for (int iter = 0;;) {
+        dev::dots(ws, nn, j - 1, a.d_v, a.d_ld, wd, a.d_resid, -1);
+        dev::finalize(ws, j, dev::kFinCoef, 0, 0, -1);
+        dev::update(ws, nn, j - 1, a.d_v, a.d_ld, 0, a.d_resid, a.d_resid, bmat != 'G', -1);
+        if (bmat == 'G') {
+            g_stats.nbx += 1;
+            dev::copy(a.stream, nn, a.d_resid, wd + nn);
+            co_await rci(2, nn, 0);
+            dev::dots(ws, nn, 0, a.d_v, a.d_ld, wd, a.d_resid, -1);
+            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+        } else {
+            dev::copy(a.stream, nn, a.d_resid, wd);
+            dev::finalize(ws, j, dev::kFinNorm, 0, 0, -1);
+        }
+        read_state();
+        rnorm = ws.st_host->rnorm;
+        if (rnorm > 0.717 * rnorm0) break;
+        ++iter;
+        if (iter <= 5) {
+            rnorm0 = rnorm;
+            continue;
+        }
+        dev::fill(a.stream, nn, 0.0, a.d_resid);
+        rnorm = 0.0;
+        ws.st_host->rnorm = 0.0;
+        write_state();
+        ierr = -1;
+        break;
+    }
+    co_return;
+}
+
+// dsaitr: extend a k-step Lanczos factorization to k+npk steps.
+Task SymSolver::saitr(int k, int npk, int& iinfo) {
+    const int64_t nn = n;
+    double* wd = a.d_workd;
+    const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
+    const bool bI = (bmat == 'I');
+    iinfo = 0;
+    int j = k + 1;
+    bool restart_pending = !(rnorm > 0.0);
+    int rstart_j = -1;  // step at which a restart happened (h(j,1) = 0)
+
+    for (;;) {
+        while (j <= k + npk) {
+            int rstart = 0;
+            if (restart_pending) {
+                // invariant subspace: new start vector orthogonal to V_j (SRC/dsaitr.f:378-427)
+                g_stats.nrstrt += 1;
+                int itry = 1, ierr = 0;
+                for (;;) {
+                    co_await getv0(false, j, itry, ierr);
+                    if (ierr >= 0) break;
+                    if (++itry <= 3) continue;
+                    iinfo = j - 1;
+                    co_return;
+                }
+                restart_pending = false;
+                rstart = 1;
+                rstart_j = j;
+                ws.st_host->abort = 0;
+                ws.st_host->rnorm = rnorm;
+                write_state();
+            }
+            // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
+            dev::place(ws, nn, a.d_resid, vcol(j), free_run ? nullptr : wd + ivj,
+                       bI ? nullptr : wd + ipj, j);
+            // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
+            g_stats.nopx += 1;
+            co_await op(1, ivj, irj, ipj, free_run ? vcol(j) : wd + ivj, wd + irj);
+            // STEP 4: B*OP*v_j (skipped in mode 2: WORKD(IVJ) holds A*v_j)
+            const double* u;
+            if (mode == 2) {
+                u = wd + ivj;
+            } else if (!bI) {
+                g_stats.nbx += 1;
+                co_await rci(2, irj, ipj);
+                u = wd + ipj;
+            } else {
+                u = wd + irj;
+            }
+            // wnorm and the CGS coefficients h = V_j' B r (SRC/dsaitr.f:538-594)
+            dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
+            dev::finalize(ws, j + 1, dev::kFinCgs, j, rstart, -1);
+            // r_j = OP*v_j - V_j h; for bmat='I' the same pass also produces the
+            // DGKS coefficients V_j' r_j and r_j' r_j (SRC/dsaitr.f:582-639)
+            dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1);
+            if (bI) {
+                dev::finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+                // refinement sweeps, each gated on the device-side decision
+                dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1);
+                dev::finalize(ws, j + 1, dev::kFinDgks1, j, rstart, 1);
+                dev::update(ws, nn, j, a.d_v, a.d_ld, 2, a.d_resid, a.d_resid, true, 2);
+                dev::finalize(ws, j + 1, dev::kFinDgks2, j, rstart, 2);
+                dev::zero_if(ws, nn, a.d_resid);
+            } else {
+                // generalized problem: every B*r is a reverse-communication request,
+                // so the refinement decisions are taken on the host.
+                g_stats.nbx += 1;
+                dev::copy(a.stream, nn, a.d_resid, wd + irj);
+                co_await rci(2, irj, ipj);
+                dev::dots(ws, nn, j, a.d_v, a.d_ld, wd + ipj, a.d_resid, -1);
+                dev::finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+                read_state();
+                for (int sweep = 1; sweep <= 2 && ws.st_host->dgks == sweep; ++sweep) {
+                    dev::update(ws, nn, j, a.d_v, a.d_ld, sweep, a.d_resid, a.d_resid, false, sweep);
+                    g_stats.nbx += 1;
+                    dev::copy(a.stream, nn, a.d_resid, wd + irj);
+                    co_await rci(2, irj, ipj);
+                    dev::dots(ws, nn, j, a.d_v, a.d_ld, wd + ipj, a.d_resid, -1);
+                    dev::finalize(ws, j + 1, sweep == 1 ? dev::kFinDgks1 : dev::kFinDgks2, j, rstart, sweep);
+                    read_state();
+                }
+                dev::zero_if(ws, nn, a.d_resid);
+                // workd(ipj) must hold B*r for the next step (SRC/dsaitr.f:361)
+                if (ws.st_host->zero) dev::fill(a.stream, nn, 0.0, wd + ipj);
+            }
+            ++j;
+            if (!free_run) {
+                read_state();
+                rnorm = ws.st_host->rnorm;
+                if (!(rnorm > 0.0)) restart_pending = true;
+            }
+        }
+        read_state();
+        if (ws.st_host->abort) {  // free-running cycle hit rnorm == 0 at step abort_j
+            const int ja = ws.st_host->abort_j;
+            g_stats.nopx -= (k + npk) - ja + 1;  // those OP*x were never applied
+            j = ja;
+            restart_pending = true;
+            continue;
+        }
+        break;
+    }
+    rnorm = ws.st_host->rnorm;
+    g_stats.nrorth += ws.st_host->nrorth;
+    g_stats.nitref += ws.st_host->nitref;
+    ws.st_host->nrorth = ws.st_host->nitref = 0;
+    write_state();
+    // assemble h(k+1:k+np, 1:2) from the per-step device records
+    double* rec = ws.host_scratch;
+    ck(hipMemcpyAsync(rec, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost, a.stream));
+    a.sync();
+    double* h = workl + ih;
+    for (int jj = k + 1; jj <= k + npk; ++jj) {
+        h[(jj - 1) + ncv] = rec[2 * (jj - 1)];
+        h[jj - 1] = rec[2 * (jj - 1) + 1];
+    }
+    (void)rstart_j;
+    co_return;
+}
+
+// dsapps: bulge chase on the host, V*Q and the residual update on the device.
+void SymSolver::sapps(int kev, int npk) {
+    const int kplusp = kev + npk;
+    double* h = workl + ih;
+    double* q = workl + iq;
+    la::dsapps_host(kev, npk, workl + iritz, h, ncv, q, ncv);
+    if (npk == 0) return;
+    // compact Q(:, 1:kev+1) into the device workspace (ld = kplusp)
+    double* qs = ws.host_scratch;  // reuse pinned scratch if large enough
+    std::vector<double> qbuf((size_t)kplusp * (kev + 1));
+    for (int c = 0; c <= kev && c < kplusp; ++c)
+        for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
+    (void)qs;
+    ck(hipMemcpyAsync(ws.q, qbuf.data(), sizeof(double) * qbuf.size(), hipMemcpyHostToDevice, a.stream));
+    const double sigmak = q[(kplusp - 1) + (size_t)(kev - 1) * ncv];
+    const double betak = h[kev];  // h(kev+1,1)
+    dev::vq_update(ws, n, a.d_v, a.d_ld, kplusp, kev, sigmak, betak, a.d_resid);
+    a.sync();  // qbuf lifetime
+}
+
+Task SymSolver::run() {
+    // ---- dsaup2 initialisation (SRC/dsaup2.f:258-317)
+    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    int nev = nev0;
+    const int np0 = np;
+    const int kplusp = nev0 + np0;
+    int nconv = 0, iter = 0;
+    const bool initv = (info != 0);
+    info = 0;
+    double* h = workl + ih;
+    double* ritz = workl + iritz;
+    double* bounds = workl + ibounds;
+    double* wl = workl + iw;
+    int ierr = 0;
+    int sinfo = 0;
+
+    if (initv) a.upload_resid();
+    co_await getv0(initv, 1, 1, ierr);
+    if (rnorm == 0.0) {
+        info = -9;
+        goto done;
+    }
+    ws.st_host->rnorm = rnorm;
+    ws.st_host->abort = 0;
+    write_state();
+
+    co_await saitr(0, nev0, sinfo);
+    if (sinfo > 0) {
+        np = sinfo;
+        mxiter = iter;
+        info = -9999;
+        goto done;
+    }
+
+    for (;;) {  // MAIN LANCZOS ITERATION LOOP (SRC/dsaup2.f:400-821)
+        ++iter;
+        co_await saitr(nev, np, sinfo);
+        if (sinfo > 0) {
+            np = sinfo;
+            mxiter = iter;
+            info = -9999;
+            goto done;
+        }
+        if (la::dseigt(rnorm, kplusp, h, ncv, ritz, bounds, wl) != 0) {
+            info = -8;
+            goto done;
+        }
+        std::memcpy(wl + kplusp, ritz, sizeof(double) * kplusp);
+        std::memcpy(wl + 2 * kplusp, bounds, sizeof(double) * kplusp);
+        nev = nev0;
+        np = np0;
+        la::dsgets(ishift, which, nev, np, ritz, bounds, wl);
+        std::memcpy(wl + np, bounds + np, sizeof(double) * nev);
+        nconv = la::dsconv(nev, ritz + np, wl + np, tol);
+        {
+            const int nptemp = np;
+            for (int jj = 0; jj < nptemp; ++jj)
+                if (bounds[jj] == 0.0) {
+                    --np;
+                    ++nev;
+                }
+        }
+        if (nconv >= nev0 || iter > mxiter || np == 0) {
+            // prepare to exit: sort converged Ritz values first (SRC/dsaup2.f:536-667)
+            if (which == la::Which::BE) {
+                la::dsortr(la::Which::SA, true, kplusp, ritz, bounds);
+                const int nevd2 = nev0 / 2, nevm2 = nev0 - nevd2;
+                if (nev > 1) {
+                    np = kplusp - nev0;
+                    const int cnt = std::min(nevd2, np);
+                    const int dst = std::max(kplusp - nevd2, kplusp - np);
+                    for (int t = 0; t < cnt; ++t) {
+                        std::swap(ritz[nevm2 + t], ritz[dst + t]);
+                        std::swap(bounds[nevm2 + t], bounds[dst + t]);
+                    }
+                }
+            } else {
+                la::Which wp = la::Which::SM;
+                if (which == la::Which::LM) wp = la::Which::SM;
+                if (which == la::Which::SM) wp = la::Which::LM;
+                if (which == la::Which::LA) wp = la::Which::SA;
+                if (which == la::Which::SA) wp = la::Which::LA;
+                la::dsortr(wp, true, kplusp, ritz, bounds);
+            }
+            for (int jj = 0; jj < nev0; ++jj) bounds[jj] /= std::max(eps23, std::fabs(ritz[jj]));
+            la::dsortr(la::Which::LA, true, nev0, bounds, ritz);
+            for (int jj = 0; jj < nev0; ++jj) bounds[jj] *= std::max(eps23, std::fabs(ritz[jj]));
+            if (which == la::Which::BE) la::dsortr(la::Which::LA, true, nconv, ritz, bounds);
+            else la::dsortr(which, true, nconv, ritz, bounds);
+            h[0] = rnorm;  // communicates rnorm to dseupd (SRC/dsaup2.f:645)
+            if (iter > mxiter && nconv < nev) info = 1;
+            if (np == 0 && nconv < nev0) info = 2;
+            np = nconv;
+            mxiter = iter;
+            nev = nconv;
+            goto done;
+        } else if (nconv < nev && ishift == 1) {
+            // anti-stagnation: grow nev (SRC/dsaup2.f:669-694)
+            const int nevbef = nev;
+            nev += std::min(nconv, np / 2);
+            if (nev == 1 && kplusp >= 6) nev = kplusp / 2;
+            else if (nev == 1 && kplusp > 2) nev = 2;
+            np = kplusp - nev;
+            if (nevbef < nev) la::dsgets(ishift, which, nev, np, ritz, bounds, wl);
+        }
+        if (ishift == 0) {  // user shifts through reverse communication (ido = 3)
+            iparam[7] = np;
+            co_await rci(3, -1, -1);
+            std::memcpy(ritz, wl, sizeof(double) * np);
+        }
+        sapps(nev, np);
+        // B-norm of the updated residual (SRC/dsaup2.f:773-809)
+        if (bmat == 'G') {
+            g_stats.nbx += 1;
+            dev::copy(a.stream, n, a.d_resid, a.d_workd + n);
+            co_await rci(2, n, 0);
+            dev::dots(ws, n, 0, a.d_v, a.d_ld, a.d_workd, a.d_resid, -1);
+            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+        } else {
+            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
+        }
+        read_state();
+        rnorm = ws.st_host->rnorm;
+    }
+done:
+    nev0 = nev;
+    iparam[2] = mxiter;
+    co_return;
+}
+
+}  // namespace ahip

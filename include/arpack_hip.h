@@ -1,0 +1,121 @@
+/*
+ * arpack_hip.h — drop-in C-ABI of the MI355X-native IRL/IRA engine.
+ *
+ * The first block re-exports, unchanged, the ISO_C_BINDING entry points of
+ * arpack-ng (reference: ICB/arpack.h:10-21, implemented by SRC/icbads.F90:3-92,
+ * SRC/icbadn.F90, SRC/icbazn.F90), plus the statistics/debug hooks
+ * (ICB/stat_c.h, ICB/debug_c.h).  Existing callers re-link against
+ * libarpack_hip.so and keep their reverse-communication loop as is:
+ *
+ *   - host pointers (malloc'ed resid/v/workd): the engine mirrors V, resid and
+ *     workd in HBM and copies only the workd slice named by ipntr across PCIe
+ *     at each ido = -1/1/2 return;
+ *   - device pointers (hipMalloc'ed resid/v/workd): zero-copy; the caller's OP
+ *     kernel reads workd[ipntr[0]-1] and writes workd[ipntr[1]-1] on device.
+ *     Before calling *aupd_c again the caller must have finished its OP (or
+ *     share the engine's stream via arpack_hip_set_stream).
+ *   workl, iparam, ipntr, select, d, workev are host memory.
+ *
+ * The second block (arpack_hip_*) is the native extension: a device CSR
+ * operator and an entry that serves every OP*x request on the GPU without
+ * returning to the caller (used by bench.py and the multi-GPU layer).
+ */
+#ifndef ARPACK_HIP_H
+#define ARPACK_HIP_H
+
+#include <stdint.h>
+
+#ifndef a_int
+#define a_int int /* LP64, arpackdef.h.in:6-14 with INTERFACE64=0 */
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference ICB (ICB/arpack.h:16-17; SRC/icbads.F90:3-92) ------------------ */
+void dsaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
+              double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
+              a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info);
+void dseupd_c(a_int rvec, char const* howmny, a_int const* select, double* d, double* z,
+              a_int ldz, double sigma, char const* bmat, a_int n, char const* which,
+              a_int nev, double tol, double* resid, a_int ncv, double* v, a_int ldv,
+              a_int* iparam, a_int* ipntr, double* workd, double* workl, a_int lworkl,
+              a_int* info);
+
+/* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
+ *      argument by reference + hidden trailing CHARACTER lengths ---------------- */
+void dsaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
+             double* tol, double* resid, a_int* ncv, double* v, a_int* ldv, a_int* iparam,
+             a_int* ipntr, double* workd, double* workl, a_int* lworkl, a_int* info,
+             size_t bmat_len, size_t which_len);
+void dseupd_(a_int* rvec, char const* howmny, a_int* select, double* d, double* z,
+             a_int* ldz, double* sigma, char const* bmat, a_int* n, char const* which,
+             a_int* nev, double* tol, double* resid, a_int* ncv, double* v, a_int* ldv,
+             a_int* iparam, a_int* ipntr, double* workd, double* workl, a_int* lworkl,
+             a_int* info, size_t howmny_len, size_t bmat_len, size_t which_len);
+
+/* ---- statistics / debug (ICB/stat_c.h, ICB/debug_c.h; stat.h:8-21) ---------- */
+void sstats_c(void);
+void stat_c(a_int* nopx, a_int* nbx, a_int* nrorth, a_int* nitref, a_int* nrstrt,
+            float* tsaupd, float* tsaup2, float* tsaitr, float* tseigt, float* tsgets,
+            float* tsapps, float* tsconv, float* tnaupd, float* tnaup2, float* tnaitr,
+            float* tneigh, float* tngets, float* tnapps, float* tnconv, float* tcaupd,
+            float* tcaup2, float* tcaitr, float* tceigh, float* tcgets, float* tcapps,
+            float* tcconv, float* tmvopx, float* tmvbx, float* tgetv0, float* titref,
+            float* trvec);
+void debug_c(a_int logfil, a_int ndigit, a_int mgetv0, a_int msaupd, a_int msaup2,
+             a_int msaitr, a_int mseigt, a_int msapps, a_int msgets, a_int mseupd,
+             a_int mnaupd, a_int mnaup2, a_int mnaitr, a_int mneigh, a_int mnapps,
+             a_int mngets, a_int mneupd, a_int mcaupd, a_int mcaup2, a_int mcaitr,
+             a_int mceigh, a_int mcapps, a_int mcgets, a_int mceupd);
+
+/* ---- native extension ---------------------------------------------------------- */
+typedef struct arpack_hip_csr arpack_hip_csr;
+
+/* Version / capability probe: returns a static string. */
+const char* arpack_hip_version(void);
+/* Number of visible GPUs (0 on a CPU-only host; never initialises a context). */
+int arpack_hip_device_count(void);
+/* Share a HIP stream (hipStream_t) with the engine; NULL = engine-owned stream. */
+void arpack_hip_set_stream(void* stream);
+
+/* Register a CSR matrix (rowptr int64[n+1], col int32[nnz], val f64[nnz]).
+ * Pointers may be host or device; host data is copied to HBM. */
+int arpack_hip_csr_create(arpack_hip_csr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
+                          const int32_t* col, const double* val);
+void arpack_hip_csr_destroy(arpack_hip_csr* A);
+/* y = A x on device (x, y device pointers). */
+int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y);
+
+/* dsaupd_c with OP = A served on the GPU: same arguments and results as
+ * dsaupd_c (mode 1, bmat 'I'), but returns only with ido = 99 (or ido = 3 when
+ * iparam[0] = 0 asks for user shifts). */
+void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, a_int* ido, char const* bmat, a_int n,
+                           char const* which, a_int nev, double tol, double* resid, a_int ncv,
+                           double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
+                           double* workl, a_int lworkl, a_int* info);
+
+/* Synthetic operators generated directly in HBM (bench/test workloads, see
+ * DESIGN.md §5).  Each allocates device CSR arrays owned by *A. */
+int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale);
+int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale);
+int arpack_hip_gen_banded_sym(arpack_hip_csr** A, int64_t n, int64_t row_begin,
+                              int64_t row_end, uint32_t seed, int bandwidth, int per_row);
+/* Copy a registered CSR back to host buffers (sizes from arpack_hip_csr_info). */
+int arpack_hip_csr_info(const arpack_hip_csr* A, int64_t* n, int64_t* nnz);
+int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* col, double* val);
+
+/* Host-side small-dense kit exports (CPU-testable, no GPU needed). */
+int arpack_hip_kit_dstqrb(int n, double* d, double* e, double* z, double* work);
+int arpack_hip_kit_dsteqr(int n, double* d, double* e, double* z, int ldz, double* work);
+void arpack_hip_kit_dlartg(double f, double g, double* c, double* s, double* r);
+void arpack_hip_kit_dsortr(char const* which, int apply, int n, double* x1, double* x2);
+void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h, int ldh,
+                                double* q, int ldq);
+void arpack_hip_kit_dlarnv(int* iseed, int n, double* x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARPACK_HIP_H */

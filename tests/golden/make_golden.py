@@ -1,0 +1,96 @@
+"""Generate the committed golden fixtures from the REAL reference (oracle/_ref).
+
+Run in the build container (where /root/reference exists):
+    make -C oracle && python tests/golden/make_golden.py
+
+Each fixture holds the inputs (operator spec, v0, parameters) and the reference's
+outputs (Ritz values, iparam, stats, eigenvectors where small).  Matrices come
+from oracle/matrices.py, which mirrors the device generators bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import glob
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import matrices as M  # noqa: E402
+from oracle import ref  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def csr_op(rowptr, col, val):
+    A = M.to_scipy(rowptr, col, val)
+    return lambda x, *_: A @ x
+
+
+def run_sym(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, **extra):
+    rowptr, col, val = mat
+    n = len(rowptr) - 1
+    if v0 is None:
+        v0, _ = M.dlarnv_uniform(n)
+    r = ref.dsaupd_solve(csr_op(rowptr, col, val), n, nev, ncv, which, tol, v0=v0,
+                         mxiter=mxiter, return_state=True)
+    assert r["info"] >= 0, r
+    out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
+               mxiter=mxiter, v0=v0, info=r["info"], iparam=r["iparam"], d=r["d"],
+               nopx=r["stats"]["nopx"], nrorth=r["stats"]["nrorth"],
+               nitref=r["stats"]["nitref"], ritz=r["workl"][2 * ncv:3 * ncv],
+               bounds=r["workl"][3 * ncv:4 * ncv], resid_norm=np.linalg.norm(r["resid"]))
+    if keep_z:
+        out["z"] = r["z"]
+    out.update(extra)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(name, "info", r["info"], "iparam", r["iparam"][[2, 4, 8, 10]], "d", r["d"][:4], "...")
+    return r
+
+
+def g7_dlarnv():
+    lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
+                                 "scipy.libs", "libscipy_openblas*.so"))[0]
+    L = C.CDLL(lib)
+    iseed = np.array([1, 3, 5, 7], np.int32)
+    x = np.zeros(1000)
+    L.scipy_dlarnv_(C.byref(C.c_int(2)), iseed.ctypes.data_as(C.POINTER(C.c_int)),
+                    C.byref(C.c_int(1000)), x.ctypes.data_as(C.POINTER(C.c_double)))
+    ours, seed = M.dlarnv_uniform(1000)
+    assert np.array_equal(x, ours) and tuple(iseed) == tuple(seed), "dlarnv restatement drifted"
+    np.savez_compressed(os.path.join(OUT, "g7_dlarnv.npz"), x=x, iseed_out=iseed,
+                        iseed_in=np.array([1, 3, 5, 7], np.int32))
+    print("g7_dlarnv ok, seed ->", iseed)
+
+
+def g1_fresh_process_check():
+    """info=0 in a fresh process == info=1 with the dlarnv(1,3,5,7) stream."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np\nfrom oracle import ref, matrices as M\n"
+            "A = M.to_scipy(*M.laplace2d(10, 121.0))\n"
+            "r = ref.dsaupd_solve(lambda x,*_: A@x, 100, 4, 20, 'LM', 0.0)\n"
+            "print(repr(r['d'].tolist()), int(r['iparam'][2]), int(r['iparam'][8]))" % ROOT)
+    return ref.run_fresh(code)
+
+
+if __name__ == "__main__":
+    g7_dlarnv()
+    r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
+                 keep_z=True)
+    fresh = g1_fresh_process_check()
+    assert fresh.strip() == "%r %d %d" % (r1["d"].tolist(), r1["iparam"][2], r1["iparam"][8]), fresh
+    print("g1 fresh-process info=0 run identical to info=1 + dlarnv stream")
+    run_sym("g2_icb_ds", M.diag(1000), ["diag", 1000], 9, 19, "LM", 1e-6, keep_z=True,
+            mxiter=10000)
+    run_sym("g3_lap3d", M.laplace3d(20), ["laplace3d", 20, 1.0], 10, 30, "LA", 1e-10,
+            keep_z=True)
+    run_sym("g4_banded", M.banded_sym(20000, 1234, 512, 25), ["banded_sym", 20000, 1234, 512, 25],
+            10, 30, "LA", 1e-8, keep_z=False)
+    run_sym("g5_lap2d_sa", M.laplace2d(30), ["laplace2d", 30, 1.0], 6, 20, "SA", 1e-7,
+            keep_z=False, mxiter=3000)
+    run_sym("g6_lap2d_be", M.laplace2d(30), ["laplace2d", 30, 1.0], 6, 20, "BE", 1e-7,
+            keep_z=False, mxiter=3000)
+    run_sym("g8_banded_capped", M.banded_sym(20000, 1234, 512, 25),
+            ["banded_sym", 20000, 1234, 512, 25], 10, 30, "LA", 1e-14, mxiter=5)
