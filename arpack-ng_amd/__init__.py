@@ -10,8 +10,9 @@ TESTS/icb_arpack_c.c does), plus the native extension (device CSR operators and
 the on-GPU driver).
 
 There is no CPU fallback: if the HIP library is missing, every entry point
-raises.  PyTorch is only used as a device-memory allocator for the caller-side
-arrays (resid, V, workd) in device-pointer mode.
+raises.  Device-pointer mode uses buffers allocated through the engine's own
+HIP runtime (DeviceBuffer); PyTorch is only used for torch.distributed (gloo)
+control traffic in the multi-process launcher.
 """
 from __future__ import annotations
 
@@ -78,9 +79,18 @@ def _declare(L):
     L.arpack_hip_csr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_gen_laplace2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
     L.arpack_hip_gen_laplace3d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
+    L.arpack_hip_gen_anderson.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int, C.c_double,
+                                          C.c_uint32]
     L.arpack_hip_gen_banded_sym.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64,
                                             C.c_int64, C.c_uint32, C.c_int, C.c_int]
     L.arpack_hip_set_stream.argtypes = [C.c_void_p]
+    L.arpack_hip_malloc.argtypes = [C.c_size_t]
+    L.arpack_hip_malloc.restype = C.c_void_p
+    L.arpack_hip_free.argtypes = [C.c_void_p]
+    L.arpack_hip_memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.arpack_hip_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    L.dsaupd_.argtypes = [_PI, C.c_char_p, _PI, C.c_char_p, _PI, C.POINTER(C.c_double), _PD, _PI,
+                          _PD, _PI, _PI, _PI, _PD, _PD, _PI, _PI, C.c_size_t, C.c_size_t]
     L.stat_c.argtypes = [_PI] * 5 + [C.POINTER(C.c_float)] * 26
     L.arpack_hip_kit_dstqrb.argtypes = [_I, _PD, _PD, _PD, _PD]
     L.arpack_hip_kit_dsteqr.argtypes = [_I, _PD, _PD, _PD, _I, _PD]
@@ -99,10 +109,59 @@ def device_count() -> int:
 
 
 # ----------------------------------------------------------------------------- arrays
+class DeviceBuffer:
+    """A float64 buffer in HBM, allocated through the engine's own HIP runtime
+    (arpack_hip_malloc), so no second GPU runtime is needed in the process."""
+
+    def __init__(self, n, dtype=np.float64):
+        self.dtype = np.dtype(dtype)
+        self.n = int(n)
+        self.nbytes = self.n * self.dtype.itemsize
+        self.ptr = lib().arpack_hip_malloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"arpack_hip_malloc({self.nbytes}) failed")
+        lib().arpack_hip_memset(self.ptr, 0, self.nbytes)
+
+    @classmethod
+    def from_numpy(cls, a):
+        a = np.ascontiguousarray(a)
+        b = cls(a.size, a.dtype)
+        lib().arpack_hip_memcpy(b.ptr, a.ctypes.data, b.nbytes)
+        return b
+
+    def numpy(self, offset=0, count=None):
+        count = self.n - offset if count is None else count
+        out = np.empty(count, self.dtype)
+        lib().arpack_hip_memcpy(out.ctypes.data, self.ptr + offset * self.dtype.itemsize,
+                                count * self.dtype.itemsize)
+        return out
+
+    def write(self, a, offset=0):
+        a = np.ascontiguousarray(a, self.dtype)
+        lib().arpack_hip_memcpy(self.ptr + offset * self.dtype.itemsize, a.ctypes.data, a.nbytes)
+
+    def at(self, offset):
+        """Device address of element `offset`."""
+        return self.ptr + offset * self.dtype.itemsize
+
+    def __len__(self):
+        return self.n
+
+    def __del__(self):
+        try:
+            if self.ptr and _lib is not None:
+                _lib.arpack_hip_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
 def _ptr(a):
-    """Raw address of a numpy array or a torch tensor (host or device)."""
+    """Raw address of a numpy array (host) or a DeviceBuffer / torch tensor (device)."""
     if isinstance(a, np.ndarray):
         return a.ctypes.data
+    if isinstance(a, DeviceBuffer):
+        return a.ptr
     if hasattr(a, "data_ptr"):
         return a.data_ptr()
     raise TypeError(type(a))
@@ -168,6 +227,13 @@ class CSR:
         return cls(h.value)
 
     @classmethod
+    def anderson(cls, m, dim=3, disorder=16.0, seed=1234):
+        h = C.c_void_p()
+        if lib().arpack_hip_gen_anderson(C.byref(h), m, dim, disorder, seed) != 0:
+            raise RuntimeError("anderson generation failed")
+        return cls(h.value)
+
+    @classmethod
     def banded_sym(cls, n, seed=1234, bandwidth=4096, per_row=25, r0=0, r1=None):
         h = C.c_void_p()
         r1 = n if r1 is None else r1
@@ -183,8 +249,10 @@ class CSR:
         return rowptr, col, val
 
     def matvec_device(self, x, y):
-        """y = A x for device buffers (torch tensors on cuda)."""
-        if lib().arpack_hip_csr_spmv(self.h, _ptr(x), _ptr(y)) != 0:
+        """y = A x for device addresses (ints) or DeviceBuffers."""
+        xp = x if isinstance(x, int) else _ptr(x)
+        yp = y if isinstance(y, int) else _ptr(y)
+        if lib().arpack_hip_csr_spmv(self.h, xp, yp) != 0:
             raise RuntimeError("spmv failed")
 
 
@@ -196,8 +264,9 @@ class SymRci:
     numpy host arrays (the engine mirrors them in HBM)."""
 
     def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300,
-                 ishift=1, v0=None, device=False):
+                 ishift=1, v0=None, device=False, icb=False):
         self.n, self.nev, self.ncv = n, nev, ncv
+        self.icb = icb
         self.which, self.bmat, self.tol = which, bmat, float(tol)
         self.device = device
         self.ido = np.zeros(1, np.int32)
@@ -211,13 +280,11 @@ class SymRci:
         self.workl = np.zeros(self.lworkl)
         self.ldv = n
         if device:
-            import torch
-            dev = torch.device("cuda")
-            self.resid = torch.zeros(n, dtype=torch.float64, device=dev)
-            self.v = torch.zeros(ncv * n, dtype=torch.float64, device=dev)
-            self.workd = torch.zeros(3 * n, dtype=torch.float64, device=dev)
+            self.resid = DeviceBuffer(n)
+            self.v = DeviceBuffer(ncv * n)
+            self.workd = DeviceBuffer(3 * n)
             if v0 is not None:
-                self.resid.copy_(torch.as_tensor(np.asarray(v0, np.float64)).to(dev))
+                self.resid.write(np.asarray(v0, np.float64))
         else:
             self.resid = np.zeros(n) if v0 is None else np.array(v0, np.float64, copy=True)
             self.v = np.zeros(ncv * n)
@@ -225,11 +292,24 @@ class SymRci:
         self.info[0] = 0 if v0 is None else 1
 
     def aupd(self):
-        """One dsaupd_c call; returns ido."""
-        lib().dsaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev,
-                       self.tol, _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
-                       _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
-                       self.lworkl, _ip(self.info))
+        """One dsaupd call; returns ido.  Uses the Fortran entry dsaupd_ (tol by
+        reference, so tol <= 0 becomes eps for the rest of the solve exactly as in
+        SRC/dsaupd.f:550) unless icb=True selects dsaupd_c (tol by value on every
+        call, SRC/icbads.F90:14)."""
+        if self.icb:
+            lib().dsaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(),
+                           self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
+                           self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        else:
+            tol = C.c_double(self.tol)
+            lib().dsaupd_(_ip(self.ido), self.bmat.encode(), C.byref(C.c_int(self.n)),
+                          self.which.encode(), C.byref(C.c_int(self.nev)), C.byref(tol),
+                          _ptr(self.resid), C.byref(C.c_int(self.ncv)), _ptr(self.v),
+                          C.byref(C.c_int(self.ldv)), _ip(self.iparam), _ip(self.ipntr),
+                          _ptr(self.workd), self.workl.ctypes.data, C.byref(C.c_int(self.lworkl)),
+                          _ip(self.info), 1, 2)
+            self.tol = tol.value
         return int(self.ido[0])
 
     def aupd_csr(self, A: CSR):
@@ -239,22 +319,23 @@ class SymRci:
                                     self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam),
                                     _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
                                     self.lworkl, _ip(self.info))
+        if self.tol <= 0.0:  # the solve used eps (SRC/dsaupd.f:550); keep it for dseupd
+            self.tol = float(np.finfo(np.float64).eps / 2)
         return int(self.ido[0])
 
     def slice(self, k):
-        """workd slice ipntr[k] (1-based offset) of length n."""
+        """workd slice ipntr[k] (1-based offset) of length n: a numpy view in
+        host mode, the device address (int) in device mode."""
         o = int(self.ipntr[k]) - 1
+        if isinstance(self.workd, DeviceBuffer):
+            return self.workd.at(o)
         return self.workd[o:o + self.n]
 
     def eupd(self, rvec=True, howmny="A", sigma=0.0, z=None):
         nconv = int(self.iparam[4])
         d = np.zeros(self.nev)
         if z is None:
-            if self.device:
-                import torch
-                z = torch.zeros(self.nev * self.n, dtype=torch.float64, device="cuda")
-            else:
-                z = np.zeros(self.nev * self.n)
+            z = DeviceBuffer(self.nev * self.n) if self.device else np.zeros(self.nev * self.n)
         select = np.zeros(self.ncv, np.int32)
         info = np.zeros(1, np.int32)
         lib().dseupd_c(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z),
@@ -275,8 +356,9 @@ class SymRci:
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,
           device=False):
     """Drive the RCI loop with a user OP (callable y = op(x) on workd slices), like
-    TESTS/icb_arpack_c.c:60-65.  With `op` a CSR, the loop runs entirely on the
-    GPU (arpack_hip_dsaupd_csr).  Returns (d, Z, info-dict)."""
+    TESTS/icb_arpack_c.c:60-65.  In device mode `op(x_addr, y_addr)` receives device
+    addresses.  With `op` a CSR, the loop runs entirely on the GPU
+    (arpack_hip_dsaupd_csr).  Returns (d, Z, info-dict)."""
     ncv = ncv or min(n, max(2 * nev + 1, 20))
     s = SymRci(n, nev, ncv, which, tol, mxiter=mxiter, v0=v0, device=device)
     if isinstance(op, CSR):
@@ -285,9 +367,10 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
         while True:
             ido = s.aupd()
             if ido in (-1, 1):
-                x = s.slice(0)
-                y = op(x)
-                s.slice(1)[:] = y
+                if device:
+                    op(s.slice(0), s.slice(1))
+                else:
+                    s.slice(1)[:] = op(s.slice(0))
             elif ido == 99:
                 break
             else:
@@ -299,7 +382,7 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
     d, z, nconv = s.eupd(rvec=rvec)
     if rvec:
         if device:
-            z = z.view(s.nev, n)[:nconv].cpu().numpy().T
+            z = z.numpy().reshape(s.nev, n)[:nconv].T
         else:
             z = z.reshape(s.nev, n)[:nconv].T
     return d, (z if rvec else None), res

@@ -78,7 +78,8 @@ static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lw
 
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                      double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
-                     double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr) {
+                     double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr,
+                     int max_cycles = -1) {
     std::lock_guard<std::mutex> lk(g_mu);
     SymSolver* S = nullptr;
     if (*ido == 0) {
@@ -156,13 +157,20 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             if (r.ido == 1 && S->mode == 2) S->a.h2d_workd(r.x, n);
         }
     }
+    if (csr) S->pause_budget = max_cycles;
     for (;;) {
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
+            dev::prof_begin(dev::kProfSpmv, S->a.stream);
             dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
             continue;
+        }
+        if (r.ido == SymSolver::kPauseIdo) {  // cycle budget spent: park (no sync)
+            *ido = r.ido;
+            return;
         }
         // hand the request to the caller
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
@@ -219,6 +227,28 @@ void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, int* ido, char const* bmat, 
              lworkl, info, ahip_csr_view(A));
 }
 
+void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* ido,
+                                  char const* bmat, int n, char const* which, int nev, double* tol,
+                                  double* resid, int ncv, double* v, int ldv, int* iparam,
+                                  int* ipntr, double* workd, double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, ahip_csr_view(A), max_cycles);
+}
+
+void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }
+
+int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int nclass) {
+    dev::ProfStat st[dev::kProfClasses];
+    dev::prof_collect(st);
+    const int k = nclass < dev::kProfClasses ? nclass : dev::kProfClasses;
+    for (int c = 0; c < k; ++c) {
+        ms[c] = st[c].ms;
+        bytes[c] = st[c].bytes;
+        count[c] = st[c].count;
+    }
+    return dev::kProfClasses;
+}
+
 void sstats_c(void) { g_stats = Stats{}; }
 
 void stat_c(int* nopx, int* nbx, int* nrorth, int* nitref, int* nrstrt, float* tsaupd,
@@ -256,6 +286,22 @@ int arpack_hip_device_count(void) {
 }
 
 void arpack_hip_set_stream(void* stream) { g_stream = (hipStream_t)stream; }
+
+void* arpack_hip_malloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+    return p;
+}
+void arpack_hip_free(void* p) {
+    if (p) (void)hipFree(p);
+}
+int arpack_hip_memcpy(void* dst, const void* src, size_t bytes) {
+    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? 0 : -1;
+}
+int arpack_hip_memset(void* dst, int value, size_t bytes) {
+    return hipMemset(dst, value, bytes) == hipSuccess ? 0 : -1;
+}
+int arpack_hip_synchronize(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
 
 // ---- host kit exports (CPU-testable) ----
 int arpack_hip_kit_dstqrb(int n, double* d, double* e, double* z, double* work) {

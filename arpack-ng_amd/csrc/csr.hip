@@ -8,6 +8,8 @@
 //  laplace2d   5-pt 2-D Laplacian, m x m grid (EXAMPLES/SIMPLE/dssimp.f:484-538
 //              operator shape; `scale` = 1/h^2 = (m+1)^2 reproduces dssimp)
 //  laplace3d   7-pt 3-D Laplacian, m^3 (BASELINE config 4)
+//  anderson    Laplacian + W*u_i on the diagonal (SURVEY.md §8c G3 "3-D Anderson"):
+//              breaks the Laplacian's exact eigenvalue multiplicities
 //  banded_sym  the north-star symmetric CSR: pairs (i, i+d), 1 <= d < B, are
 //              present with probability per_row/4096 (~2*per_row nnz/row),
 //              off-diagonal values -k/4096 (k in 1..4096), diagonal
@@ -119,8 +121,9 @@ __global__ void k_lap_count(int64_t m, int dim, int64_t* __restrict__ cnt) {
     }
 }
 
-__global__ void k_lap_fill(int64_t m, int dim, double scale, const int64_t* __restrict__ rp,
-                           int32_t* __restrict__ col, double* __restrict__ val) {
+__global__ void k_lap_fill(int64_t m, int dim, double scale, double disorder, uint32_t seed,
+                           const int64_t* __restrict__ rp, int32_t* __restrict__ col,
+                           double* __restrict__ val) {
     const int64_t n = dim == 2 ? m * m : m * m * m;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const double off = -1.0 * scale, dg = (dim == 2 ? 4.0 : 6.0) * scale;
@@ -131,7 +134,11 @@ __global__ void k_lap_fill(int64_t m, int dim, double scale, const int64_t* __re
         if (dim == 3 && z > 0) put(i - m * m, off);
         if (y > 0) put(i - m, off);
         if (x > 0) put(i - 1, off);
-        put(i, dg);
+        // Anderson disorder: + W * u_i, u_i on a 2^-12 grid in [0,1) (exact sums)
+        const double u = disorder != 0.0
+                             ? (double)(mix32((uint32_t)i ^ mix32(seed ^ 0x2545f491u)) >> 20) * 0x1p-12
+                             : 0.0;
+        put(i, dg + disorder * u);
         if (x < m - 1) put(i + 1, off);
         if (y < m - 1) put(i + m, off);
         if (dim == 3 && z < m - 1) put(i + m * m, off);
@@ -234,7 +241,8 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale) {
+static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, double disorder = 0.0,
+                   uint32_t seed = 0) {
     const int64_t n = dim == 2 ? m * m : m * m * m;
     int64_t *cnt = nullptr, *rp = nullptr;
     if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
@@ -244,8 +252,8 @@ static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale) {
     int32_t* col = nullptr;
     double* val = nullptr;
     if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, scale, rp, col,
-                       val);
+    hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, scale, disorder,
+                       seed, rp, col, val);
     (void)hipDeviceSynchronize();
     *out = finish(n, n, nnz, rp, col, val);
     return 0;
@@ -253,6 +261,9 @@ static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale) {
 
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 2, scale); }
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 3, scale); }
+int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed) {
+    return gen_lap(A, m, dim, 1.0, disorder, seed);
+}
 
 int arpack_hip_gen_banded_sym(arpack_hip_csr** out, int64_t n, int64_t r0, int64_t r1, uint32_t seed,
                               int bandwidth, int per_row) {

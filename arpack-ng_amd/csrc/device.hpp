@@ -102,5 +102,31 @@ struct Csr {
     int group = 16;                   // lanes per row for the vector kernel
 };
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y);
+// algorithmic HBM bytes of one SpMV: 12*nnz + 8*(n+1) (int64 rowptr) + 8n (x) + 8n (y)
+double csr_bytes(const Csr& A);
+
+// ------------------------------------------------------- per-kernel profiler --
+// hipEvent pairs around launches (enabled by arpack_hip_profile(1)); gives the
+// live average duration and the algorithmic bytes of each kernel class over a
+// timed region (bench.py's roofline numbers).
+enum ProfClass : int {
+    kProfSpmv = 0,
+    kProfDots,
+    kProfUpdate,    // CGS update + fused DGKS dots, and the first DGKS sweep
+    kProfVq,        // dsapps V*Q
+    kProfPlace,
+    kProfFinalize,
+    kProfOther,     // rarely-open gated kernels (2nd refinement, zeroing), copies
+    kProfClasses
+};
+struct ProfStat {
+    double ms = 0.0, bytes = 0.0;
+    long long count = 0;
+};
+void prof_enable(bool on);
+bool prof_on();
+void prof_begin(ProfClass c, hipStream_t s);
+void prof_end(ProfClass c, hipStream_t s, double bytes);
+void prof_collect(ProfStat out[kProfClasses]);  // synchronises, returns and resets
 
 }  // namespace ahip::dev

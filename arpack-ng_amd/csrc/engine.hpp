@@ -82,6 +82,11 @@ public:
     // free-running mode (arpack_hip_dsaupd_csr): OP requests are served by
     // an on-device CSR operator without returning to the caller.
     bool free_run = false;
+    // cycle-granular pausing of the free-running driver (bench timing): at the
+    // top of each restart cycle, if pause_budget == 0 the solve parks with
+    // ido = kPauseIdo; -1 disables.
+    static constexpr int kPauseIdo = 98;
+    int pause_budget = -1;
     const dev::Csr* csr = nullptr;
 
     // workl offsets (0-based) of h, ritz, bounds, q, w

@@ -488,8 +488,19 @@ void ws_destroy(Workspace& ws) {
     ws = Workspace{};
 }
 
+namespace {
+struct ProfScope {  // event pair around one launch when profiling is on
+    ProfClass c;
+    hipStream_t s;
+    double bytes;
+    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_begin(c, s); }
+    ~ProfScope() { prof_end(c, s, bytes); }
+};
+}  // namespace
+
 void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double* copy1,
            double* sc, int j) {
+    ProfScope ps(kProfPlace, ws.stream, 8.0 * n * (2 + (copy1 != nullptr) + 2 * (sc != nullptr)));
     hipLaunchKernelGGL(k_place, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
                        sc, ws.st, j);
 }
@@ -504,6 +515,8 @@ static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const do
 
 void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
           const double* w, int gate) {
+    ProfScope ps(gate == 2 ? kProfOther : kProfDots, ws.stream,
+                 gate == 2 ? 0.0 : 8.0 * n * (j + 1 + (w != u)));
     if (j == 0) {
         launch_dots<1>(ws, n, 0, 0, V, ld, u, w, 1, 0, gate);
         return;
@@ -521,6 +534,8 @@ void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, 
             const double* rin, double* rout, bool spec, int gate) {
     const double* c = ws.coef + (size_t)which * ws.stride;
     const int sp = spec ? 1 : 0;
+    ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
+                 gate == 2 ? 0.0 : 8.0 * n * (j + 2));
     if (j <= 8) {
         hipLaunchKernelGGL(k_update_fused<8>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V, ld,
                            c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
@@ -538,17 +553,20 @@ void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, 
 }
 
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate) {
+    ProfScope ps(kProfFinalize, ws.stream, 8.0 * ws.nblk * m);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, ws.stride, m,
                        (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
 }
 
 void zero_if(const Workspace& ws, int64_t n, double* r) {
+    ProfScope ps(kProfOther, ws.stream, 0.0);
     hipLaunchKernelGGL(k_zero_if, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
 }
 
 void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp, int kev,
                double sigmak, double betak, double* r) {
     const int g = ws.nblk;
+    ProfScope ps(kProfVq, ws.stream, 8.0 * n * (kplusp + kev + (betak > 0.0) + 2));
     if (kplusp <= 16)
         hipLaunchKernelGGL(k_vq_update<16>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
                            ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
@@ -604,6 +622,10 @@ void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const
 void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
               int64_t ldz) {
     hipLaunchKernelGGL(k_ger_cols, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
+}
+
+double csr_bytes(const Csr& A) {
+    return 12.0 * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {

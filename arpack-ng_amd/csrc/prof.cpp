@@ -1,0 +1,86 @@
+// Per-kernel-class hipEvent profiler (see device.hpp).  Events are recorded on
+// the stream the kernel is launched on, so the measured duration is the
+// kernel's own device time inside the timed region, not host wall time.
+#include <mutex>
+#include <vector>
+
+#include "device.hpp"
+
+namespace ahip::dev {
+
+namespace {
+struct Pending {
+    ProfClass c;
+    hipEvent_t a, b;
+    double bytes;
+};
+std::mutex g_mu;
+bool g_on = false;
+std::vector<hipEvent_t> g_pool;
+std::vector<Pending> g_pending;
+hipEvent_t g_open[kProfClasses] = {};
+ProfStat g_acc[kProfClasses];
+
+hipEvent_t take() {
+    if (!g_pool.empty()) {
+        hipEvent_t e = g_pool.back();
+        g_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void drain_locked() {
+    for (auto& p : g_pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            g_acc[p.c].ms += ms;
+            g_acc[p.c].bytes += p.bytes;
+            g_acc[p.c].count += 1;
+        }
+        g_pool.push_back(p.a);
+        g_pool.push_back(p.b);
+    }
+    g_pending.clear();
+}
+}  // namespace
+
+void prof_enable(bool on) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_on = on;
+}
+
+bool prof_on() { return g_on; }
+
+void prof_begin(ProfClass c, hipStream_t s) {
+    if (!g_on) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_pending.size() > 4096) drain_locked();  // bound the number of live events
+    hipEvent_t e = take();
+    (void)hipEventRecord(e, s);
+    g_open[c] = e;
+}
+
+void prof_end(ProfClass c, hipStream_t s, double bytes) {
+    if (!g_on) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_open[c]) return;
+    hipEvent_t e = take();
+    (void)hipEventRecord(e, s);
+    g_pending.push_back(Pending{c, g_open[c], e, bytes});
+    g_open[c] = nullptr;
+}
+
+void prof_collect(ProfStat out[kProfClasses]) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    drain_locked();
+    for (int c = 0; c < kProfClasses; ++c) {
+        out[c] = g_acc[c];
+        g_acc[c] = ProfStat{};
+    }
+}
+
+}  // namespace ahip::dev

@@ -374,6 +374,8 @@ Task SymSolver::run() {
     }
 
     for (;;) {  // MAIN LANCZOS ITERATION LOOP (SRC/dsaup2.f:400-821)
+        if (pause_budget == 0) co_await rci(kPauseIdo, -1, -1);
+        if (pause_budget > 0) --pause_budget;
         ++iter;
         co_await saitr(nev, np, sinfo);
         if (sinfo > 0) {

@@ -23,6 +23,7 @@
 #ifndef ARPACK_HIP_H
 #define ARPACK_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifndef a_int
@@ -80,6 +81,13 @@ int arpack_hip_device_count(void);
 /* Share a HIP stream (hipStream_t) with the engine; NULL = engine-owned stream. */
 void arpack_hip_set_stream(void* stream);
 
+/* Device memory helpers (so callers need no other GPU runtime binding). */
+void* arpack_hip_malloc(size_t bytes);
+void arpack_hip_free(void* p);
+int arpack_hip_memcpy(void* dst, const void* src, size_t bytes); /* any direction */
+int arpack_hip_memset(void* dst, int value, size_t bytes);
+int arpack_hip_synchronize(void);
+
 /* Register a CSR matrix (rowptr int64[n+1], col int32[nnz], val f64[nnz]).
  * Pointers may be host or device; host data is copied to HBM. */
 int arpack_hip_csr_create(arpack_hip_csr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
@@ -100,6 +108,7 @@ void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, a_int* ido, char const* bmat
  * DESIGN.md §5).  Each allocates device CSR arrays owned by *A. */
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale);
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale);
+int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed);
 int arpack_hip_gen_banded_sym(arpack_hip_csr** A, int64_t n, int64_t row_begin,
                               int64_t row_end, uint32_t seed, int bandwidth, int per_row);
 /* Copy a registered CSR back to host buffers (sizes from arpack_hip_csr_info). */

@@ -79,7 +79,7 @@ def banded_sym(n, seed=1234, B=4096, per_row=25, r0=0, r1=None):
     return rowptr, c.astype(np.int32), v
 
 
-def laplace(m, dim=2, scale=1.0):
+def laplace(m, dim=2, scale=1.0, disorder=0.0, seed=0):
     n = m ** dim
     i = np.arange(n, dtype=np.int64)
     x = i % m
@@ -90,13 +90,19 @@ def laplace(m, dim=2, scale=1.0):
     dg = (4.0 if dim == 2 else 6.0) * scale
     if dim == 3:
         entries.append((z > 0, i - m * m, off))
-    entries += [(y > 0, i - m, off), (x > 0, i - 1, off), (np.ones(n, bool), i, dg),
+    dgv = np.full(n, dg)
+    if disorder != 0.0:
+        s2 = _mix32(np.uint64(seed) ^ np.uint64(0x2545F491))
+        u = (_mix32(i.astype(np.uint64) ^ s2) >> np.uint64(20)).astype(np.float64) * 2.0 ** -12
+        dgv = dg + disorder * u
+    entries += [(y > 0, i - m, off), (x > 0, i - 1, off), (np.ones(n, bool), i, dgv),
                 (x < m - 1, i + 1, off), (y < m - 1, i + m, off)]
     if dim == 3:
         entries.append((z < m - 1, i + m * m, off))
     r = np.concatenate([i[ok] for ok, _, _ in entries])
     c = np.concatenate([j[ok] for ok, j, _ in entries])
-    v = np.concatenate([np.full(int(ok.sum()), val) for ok, _, val in entries])
+    v = np.concatenate([np.asarray(val)[ok] if np.ndim(val) else np.full(int(ok.sum()), val)
+                        for ok, _, val in entries])
     order = np.lexsort((c, r))
     r, c, v = r[order], c[order], v[order]
     rowptr = np.zeros(n + 1, np.int64)
@@ -110,6 +116,10 @@ def laplace2d(m, scale=1.0):
 
 def laplace3d(m, scale=1.0):
     return laplace(m, 3, scale)
+
+
+def anderson(m, dim=3, disorder=16.0, seed=1234):
+    return laplace(m, dim, 1.0, disorder, seed)
 
 
 def diag(n):

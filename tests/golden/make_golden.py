@@ -84,13 +84,17 @@ if __name__ == "__main__":
     print("g1 fresh-process info=0 run identical to info=1 + dlarnv stream")
     run_sym("g2_icb_ds", M.diag(1000), ["diag", 1000], 9, 19, "LM", 1e-6, keep_z=True,
             mxiter=10000)
-    run_sym("g3_lap3d", M.laplace3d(20), ["laplace3d", 20, 1.0], 10, 30, "LA", 1e-10,
-            keep_z=True)
+    run_sym("g3_anderson3d", M.anderson(20, 3, 16.0, 1234), ["anderson", 20, 3, 16.0, 1234], 10,
+            30, "LA", 1e-10, keep_z=True)
+    run_sym("g9_lap3d_degenerate", M.laplace3d(20), ["laplace3d", 20, 1.0], 10, 30, "LA", 1e-10,
+            keep_z=False, degenerate=1)
     run_sym("g4_banded", M.banded_sym(20000, 1234, 512, 25), ["banded_sym", 20000, 1234, 512, 25],
             10, 30, "LA", 1e-8, keep_z=False)
-    run_sym("g5_lap2d_sa", M.laplace2d(30), ["laplace2d", 30, 1.0], 6, 20, "SA", 1e-7,
-            keep_z=False, mxiter=3000)
-    run_sym("g6_lap2d_be", M.laplace2d(30), ["laplace2d", 30, 1.0], 6, 20, "BE", 1e-7,
-            keep_z=False, mxiter=3000)
+    run_sym("g5_anderson2d_sa", M.anderson(40, 2, 4.0, 7), ["anderson", 40, 2, 4.0, 7], 6, 20,
+            "SA", 1e-9, keep_z=False, mxiter=3000)
+    run_sym("g6_anderson2d_be", M.anderson(40, 2, 4.0, 7), ["anderson", 40, 2, 4.0, 7], 6, 20,
+            "BE", 1e-9, keep_z=False, mxiter=3000)
+    run_sym("g10_anderson2d_sm", M.anderson(40, 2, 4.0, 7), ["anderson", 40, 2, 4.0, 7], 5, 24,
+            "SM", 1e-8, keep_z=False, mxiter=3000)
     run_sym("g8_banded_capped", M.banded_sym(20000, 1234, 512, 25),
             ["banded_sym", 20000, 1234, 512, 25], 10, 30, "LA", 1e-14, mxiter=5)
