@@ -92,6 +92,12 @@ def _declare(L):
     L.dsaupd_.argtypes = [_PI, C.c_char_p, _PI, C.c_char_p, _PI, C.POINTER(C.c_double), _PD, _PI,
                           _PD, _PI, _PI, _PI, _PD, _PD, _PI, _PI, C.c_size_t, C.c_size_t]
     L.stat_c.argtypes = [_PI] * 5 + [C.POINTER(C.c_float)] * 26
+    L.arpack_hip_dsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p, _I,
+                                               C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI,
+                                               _PD, _PD, _I, _PI]
+    L.arpack_hip_profile.argtypes = [_I]
+    L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
+    L.arpack_hip_synchronize.restype = C.c_int
     L.arpack_hip_kit_dstqrb.argtypes = [_I, _PD, _PD, _PD, _PD]
     L.arpack_hip_kit_dsteqr.argtypes = [_I, _PD, _PD, _PD, _I, _PD]
     L.arpack_hip_kit_dlartg.argtypes = [C.c_double, C.c_double] + [C.POINTER(C.c_double)] * 3
@@ -169,6 +175,29 @@ def _ptr(a):
 
 def _ip(a):
     return a.ctypes.data_as(_PI)
+
+
+PROF_CLASSES = ["spmv", "cgs_dots", "update", "vq", "place", "finalize", "other"]
+
+
+def profile(enable: bool = True):
+    """Turn the engine's per-kernel hipEvent timing on/off."""
+    lib().arpack_hip_profile(1 if enable else 0)
+
+
+def profile_read():
+    """{class: (total_ms, algorithmic_bytes, launches)} since the last read."""
+    k = len(PROF_CLASSES)
+    ms = np.zeros(k)
+    by = np.zeros(k)
+    cnt = np.zeros(k, np.int64)
+    lib().arpack_hip_profile_read(ms.ctypes.data, by.ctypes.data, cnt.ctypes.data, k)
+    return {c: (float(ms[i]), float(by[i]), int(cnt[i])) for i, c in enumerate(PROF_CLASSES)}
+
+
+def synchronize():
+    if lib().arpack_hip_synchronize() != 0:
+        raise RuntimeError("hipDeviceSynchronize failed")
 
 
 def stats():
@@ -321,6 +350,18 @@ class SymRci:
                                     self.lworkl, _ip(self.info))
         if self.tol <= 0.0:  # the solve used eps (SRC/dsaupd.f:550); keep it for dseupd
             self.tol = float(np.finfo(np.float64).eps / 2)
+        return int(self.ido[0])
+
+    def aupd_cycles(self, A: CSR, max_cycles: int):
+        """Free-running solve that parks (ido=98) after `max_cycles` more restart
+        cycles (arpack_hip_dsaupd_csr_cycles); returns ido (98 parked, 99 done)."""
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_dsaupd_csr_cycles(A.h, int(max_cycles), _ip(self.ido), self.bmat.encode(),
+                                           self.n, self.which.encode(), self.nev, C.byref(tol),
+                                           _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                           _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
         return int(self.ido[0])
 
     def slice(self, k):

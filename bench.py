@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json `metric`): implicit-restart (Arnoldi)
+iterations per second of the MI355X engine's dsaupd on the north-star operator
+
+    NS: symmetric CSR, n = 10,000,000 rows, ~50 nnz/row (banded hash pattern,
+        bandwidth 4096), diagonally dominant Anderson-like, which='LA',
+        nev = 10, ncv = 30, fp64, generated directly in HBM (synthetic data).
+
+A "step" is ONE implicit-restart cycle = one increment of iparam(3): np = 20
+Lanczos steps (CSR SpMV + classical Gram-Schmidt + DGKS against V) followed by
+the host shift selection and the on-device V*Q update (dsapps).  The whole loop
+runs on the GPU through arpack_hip_dsaupd_csr_cycles (the engine parks every K
+cycles so exactly K cycles sit inside the timed region).
+
+Also reported: Lanczos steps/s (OP*x/s), time-to-converge at tol=1e-6, the
+roofline of the dominant kernel (SpMV) from live hipEvent timing, and the
+reference CPU path (oracle/_ref: arpack-ng Fortran + OpenBLAS, OpenMP SpMV)
+timed on a bounded sample on the host cores.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+Multi-GPU: launched by torch.distributed.run, one rank per GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def load_pkg():
+    import importlib.util
+    if "arpack_ng_amd" in sys.modules:
+        return sys.modules["arpack_ng_amd"]
+    d = os.path.join(ROOT, "arpack-ng_amd")
+    spec = importlib.util.spec_from_file_location("arpack_ng_amd", os.path.join(d, "__init__.py"),
+                                                  submodule_search_locations=[d])
+    m = importlib.util.module_from_spec(spec)
+    sys.modules["arpack_ng_amd"] = m
+    spec.loader.exec_module(m)
+    return m
+
+
+def cpu_baseline(args):
+    """The reference on the host cores (rank 0, N=1 only), bounded sample."""
+    threads = min(16, len(os.sched_getaffinity(0)))
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--seed",
+           str(args.seed), "--bandwidth", str(args.bandwidth), "--per-row", str(args.per_row),
+           "--threads", str(threads)]
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        cb = json.loads(line)
+        return dict(value=cb["iters_per_s"], unit="iters/s", cores=threads, kind="reference",
+                    sample=cb["sample"], lanczos_steps_per_s=cb["lanczos_steps_per_s"],
+                    cycle_s=cb["cycle_s"])
+    except Exception as e:  # report, never fake
+        return dict(value=None, unit="iters/s", cores=threads, kind="reference",
+                    sample="failed: %s" % (str(e)[:200]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--per-row", type=int, default=25)
+    ap.add_argument("--bandwidth", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--nev", type=int, default=10)
+    ap.add_argument("--ncv", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ttc", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (gloo); data path is RCCL
+        dist.init_process_group("gloo")
+
+    pkg = load_pkg()
+    n, nev, ncv = args.n, args.nev, args.ncv
+    t = time.time()
+    A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row)
+    gen_s = time.time() - t
+    nnz = A.nnz
+
+    # ---- restart-cycle throughput: W untimed cycles, then exactly K timed ones
+    mx = args.warmup + args.steps + 5
+    s = pkg.SymRci(n, nev, ncv, "LA", 0.0, mxiter=mx, device=True)
+    assert s.aupd_cycles(A, 0) == 98            # getv0 + initial nev-step factorization
+    s.aupd_cycles(A, args.warmup)                # warmup cycles
+    pkg.synchronize()
+    if dist:
+        dist.barrier()
+    it0 = pkg.stats()["nopx"]
+    pkg.profile(True)
+    pkg.profile_read()
+    t0 = time.perf_counter()
+    ido = s.aupd_cycles(A, args.steps)
+    pkg.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    prof = pkg.profile_read()
+    pkg.profile(False)
+    nopx = pkg.stats()["nopx"] - it0
+    elapsed = t1 - t0
+    if dist:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    cycles = args.steps if ido == 98 else None
+    if cycles is None:  # converged inside the timed region: count what ran
+        cycles = int(s.iparam[2]) - args.warmup
+    iters_per_s = cycles / elapsed
+    del s
+
+    # ---- time to converge (tol = 1e-6), full solve incl. start vector
+    ttc = None
+    if not args.no_ttc:
+        s2 = pkg.SymRci(n, nev, ncv, "LA", 1e-6, mxiter=300, device=True)
+        pkg.synchronize()
+        t = time.perf_counter()
+        s2.aupd_csr(A)
+        pkg.synchronize()
+        ttc = dict(seconds=time.perf_counter() - t, iters=int(s2.iparam[2]),
+                   nconv=int(s2.iparam[4]), nopx=int(s2.iparam[8]), info=int(s2.info[0]))
+        del s2
+
+    ms, by, cnt = prof["spmv"]
+    spmv_avg_ms = ms / max(cnt, 1)
+    spmv_bytes = by / max(cnt, 1)
+    achieved = spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9 if cnt else None
+    kernels = {k: dict(ms=v[0], launches=v[2],
+                       gbs=(v[1] / (v[0] * 1e-3) / 1e9) if v[0] > 0 and v[1] > 0 else None)
+               for k, v in prof.items()}
+    orth_ms = sum(prof[k][0] for k in ("cgs_dots", "update", "finalize", "place"))
+    orth_bytes = sum(prof[k][1] for k in ("cgs_dots", "update", "place"))
+    step_ms = ms + orth_ms
+    step_gbs = (by + orth_bytes) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
+
+    out = {
+        "metric": "Arnoldi iters/sec + time-to-converge (nev=10), n=10M CSR; %HBM roofline",
+        "value": iters_per_s * (world if False else 1),
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / cycles,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (NS operator generated in HBM from a counter hash; no files)",
+        "config": {"workload": "dsaupd LA on NS symmetric CSR (BASELINE north star)",
+                   "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
+                   "which": "LA", "tol": "eps (cycles never converge in the timed window)",
+                   "parallelism": "single GPU" if world == 1 else "replicas"},
+        "lanczos_steps_per_s": nopx / elapsed,
+        "time_to_converge": ttc,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "kernel": "csr_spmv (k_csr_vector)",
+                     "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
+                     "spmv_plus_orth_gbs": step_gbs,
+                     "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
+        "kernels": kernels,
+        "gen_s": gen_s,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del A
+        out["cpu_baseline"] = cpu_baseline(args)
+        if out["cpu_baseline"].get("value"):
+            out["speedup_vs_cpu"] = iters_per_s / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,22 @@ void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, a_int* ido, char const* bmat
                            double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
                            double* workl, a_int lworkl, a_int* info);
 
+/* Same, but parks after at most `max_cycles` further restart cycles with
+ * ido = 98 (tol by reference, as dsaupd_).  Call again with ido = 98 to
+ * continue; ido = 99 when the solve is complete.  Used to time exactly K
+ * restart cycles (bench.py); max_cycles < 0 never parks. */
+void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_int* ido,
+                                  char const* bmat, a_int n, char const* which, a_int nev,
+                                  double* tol, double* resid, a_int ncv, double* v, a_int ldv,
+                                  a_int* iparam, a_int* ipntr, double* workd, double* workl,
+                                  a_int lworkl, a_int* info);
+
+/* Per-kernel-class device timing with hipEvents on the launch stream.
+ * Classes: 0 SpMV, 1 CGS dots, 2 update(+fused DGKS dots), 3 V*Q, 4 place,
+ * 5 finalize, 6 other.  read() synchronises and resets; returns #classes. */
+void arpack_hip_profile(int enable);
+int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int nclass);
+
 /* Synthetic operators generated directly in HBM (bench/test workloads, see
  * DESIGN.md §5).  Each allocates device CSR arrays owned by *A. */
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale);
