@@ -75,6 +75,9 @@ def _declare(L):
                                         C.c_void_p, C.c_void_p]
     L.arpack_hip_csr_destroy.argtypes = [C.c_void_p]
     L.arpack_hip_csr_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_csr_set_kernel.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.arpack_hip_csr_time.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    L.arpack_hip_csr_time.restype = C.c_double
     L.arpack_hip_csr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.arpack_hip_csr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_gen_laplace2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
@@ -276,6 +279,17 @@ class CSR:
         val = np.empty(self.nnz, np.float64)
         lib().arpack_hip_csr_download(self.h, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data)
         return rowptr, col, val
+
+    def set_kernel(self, kernel: int, tile: int = 4096):
+        """0 vector, 1 CSR-stream, 2 CSR-stream non-temporal."""
+        if lib().arpack_hip_csr_set_kernel(self.h, kernel, tile) != 0:
+            raise RuntimeError("kernel not applicable to this matrix")
+
+    def time_spmv(self, reps=20):
+        x = DeviceBuffer(self.n)
+        x.write(np.linspace(-1, 1, self.n))
+        y = DeviceBuffer(self.n)
+        return lib().arpack_hip_csr_time(self.h, x.ptr, y.ptr, reps)
 
     def matvec_device(self, x, y):
         """y = A x for device addresses (ints) or DeviceBuffers."""

@@ -34,6 +34,7 @@ struct arpack_hip_csr {
     double* val = nullptr;
     int64_t row_begin = 0;  // global index of local row 0 (sharded generators)
     int64_t ncols = 0;
+    int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
 };
 
 namespace ahip::gen {
@@ -191,6 +192,7 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.col = col;
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
+    if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
     return A;
 }
 
@@ -220,6 +222,7 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     (void)hipFree(A->rowptr);
     (void)hipFree(A->col);
     (void)hipFree(A->val);
+    if (A->rblk) (void)hipFree(A->rblk);
     delete A;
 }
 
@@ -239,6 +242,38 @@ int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* c
 int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
     ahip::dev::csr_spmv(nullptr, A->A, x, y);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
+    if (kernel == ahip::dev::kCsrVector) {
+        A->A.kernel = kernel;
+        return 0;
+    }
+    if (tile != 2048 && tile != 4096) return -1;
+    if (A->A.tile != tile || !A->rblk) {
+        if (A->rblk) (void)hipFree(A->rblk);
+        A->rblk = nullptr;
+        A->A.rblk = nullptr;
+        if (ahip::dev::csr_analyse(A->A, tile, &A->rblk) != 0) return -1;
+    }
+    A->A.kernel = kernel;
+    return 0;
+}
+
+double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    ahip::dev::csr_spmv(nullptr, A->A, x, y);  // warm
+    (void)hipEventRecord(a, nullptr);
+    for (int r = 0; r < reps; ++r) ahip::dev::csr_spmv(nullptr, A->A, x, y);
+    (void)hipEventRecord(b, nullptr);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return (double)ms / reps;
 }
 
 static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, double disorder = 0.0,

@@ -100,7 +100,18 @@ struct Csr {
     const int32_t* col = nullptr;     // nnz
     const double* val = nullptr;      // nnz
     int group = 16;                   // lanes per row for the vector kernel
+    // CSR-stream row blocks: block b owns rows [rblk[b], rblk[b+1]) whose
+    // nonzeros (<= tile) are streamed by one workgroup
+    const int64_t* rblk = nullptr;
+    int64_t nrblk = 0;
+    int tile = 0;
+    int kernel = 0;                   // kCsrVector / kCsrStream / kCsrStreamNT
 };
+enum CsrKernel : int { kCsrVector = 0, kCsrStream = 1, kCsrStreamNT = 2 };
+// Build the CSR-stream row blocks (host-side greedy pass over rowptr, once per
+// matrix, like a sparse-library "analysis" step).  Returns 0, or -1 if a row
+// is longer than the tile (the matrix then keeps the vector kernel).
+int csr_analyse(Csr& A, int tile, int64_t** rblk_dev);
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y);
 // algorithmic HBM bytes of one SpMV: 12*nnz + 8*(n+1) (int64 rowptr) + 8n (x) + 8n (y)
 double csr_bytes(const Csr& A);

@@ -105,63 +105,63 @@ __global__ __launch_bounds__(kBlock) void k_place(int64_t n, const double* __res
 }
 
 // ------------------------------------------------------------------- dots ---
-template <int CH>
-__global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, int jc,
-                                                 const double* __restrict__ V, int64_t ld,
-                                                 const double* __restrict__ u,
-                                                 const double* __restrict__ w, int same,
-                                                 int with_w, double* __restrict__ part,
-                                                 int pstride, int wslot,
+// Exact compile-time column count J (branch-free unrolled loads: all J column
+// loads of a row are in flight together).  WM: 0 no w'u, 1 w == u, 2 w != u.
+template <int J, int WM>
+__global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double* __restrict__ V,
+                                                 int64_t ld, const double* __restrict__ u,
+                                                 const double* __restrict__ w,
+                                                 double* __restrict__ part, int pstride, int wslot,
                                                  const LzState* __restrict__ st, int gate) {
     if (gate_closed(st, gate)) return;
-    double acc[CH];
+    double acc[J > 0 ? J : 1];
 #pragma unroll
-    for (int k = 0; k < CH; ++k) acc[k] = 0.0;
+    for (int k = 0; k < J; ++k) acc[k] = 0.0;
     double aw = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const double* Vb = V + (int64_t)j0 * ld;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         const double ui = u[i];
-        if (with_w) aw += (same ? ui : w[i]) * ui;
+        if constexpr (WM == 1) aw += ui * ui;
+        if constexpr (WM == 2) aw += w[i] * ui;
 #pragma unroll
-        for (int k = 0; k < CH; ++k)
-            if (k < jc) acc[k] += Vb[i + (int64_t)k * ld] * ui;
+        for (int k = 0; k < J; ++k) acc[k] += Vb[i + (int64_t)k * ld] * ui;
     }
-    block_partials<CH>(acc, jc, aw, with_w != 0, part + (int64_t)blockIdx.x * pstride + j0,
-                       wslot - j0);
+    constexpr int JJ = J > 0 ? J : 1;
+    block_partials<JJ>(acc, J, aw, WM != 0, part + (int64_t)blockIdx.x * pstride + j0,
+                                  wslot - j0);
 }
 
 // ----------------------------------------------------------------- update ---
-// rout = rin - V(:,0:j) c ; spec: partials of [V' rout ; rout' rout]
-template <int CH>
+// rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
+// same pass (the V row stays in registers: one HBM read of V serves both).
+template <int J, bool SPEC>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
-    int64_t n, int j, const double* __restrict__ V, int64_t ld, const double* __restrict__ c,
-    const double* rin, double* rout, int spec, double* __restrict__ part, int pstride,
+    int64_t n, const double* __restrict__ V, int64_t ld, const double* __restrict__ c,
+    const double* rin, double* rout, double* __restrict__ part, int pstride,
     const LzState* __restrict__ st, int gate) {
     if (gate_closed(st, gate)) return;
-    double acc[CH];
+    double acc[J];
 #pragma unroll
-    for (int k = 0; k < CH; ++k) acc[k] = 0.0;
+    for (int k = 0; k < J; ++k) acc[k] = 0.0;
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        double vrow[CH];
+        double vrow[J];
+#pragma unroll
+        for (int k = 0; k < J; ++k) vrow[k] = V[i + (int64_t)k * ld];
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            vrow[k] = (k < j) ? V[i + (int64_t)k * ld] : 0.0;
-            if (k < j) s += vrow[k] * c[k];
-        }
+        for (int k = 0; k < J; ++k) s += vrow[k] * c[k];
         const double r = rin[i] - s;
         rout[i] = r;
-        if (spec) {
+        if constexpr (SPEC) {
             rr += r * r;
 #pragma unroll
-            for (int k = 0; k < CH; ++k)
-                if (k < j) acc[k] += vrow[k] * r;
+            for (int k = 0; k < J; ++k) acc[k] += vrow[k] * r;
         }
     }
-    if (spec) block_partials<CH>(acc, j, rr, true, part + (int64_t)blockIdx.x * pstride, j);
+    if constexpr (SPEC) block_partials<J>(acc, J, rr, true, part + (int64_t)blockIdx.x * pstride, J);
 }
 
 // generic (any j): no fused dots
@@ -407,28 +407,7 @@ __global__ void k_axpby(int64_t n, double alpha, double* y, double beta, const d
         y[i] = alpha * y[i] + beta * x[i];
 }
 
-// ---------------------------------------------------------------- CSR SpMV ---
-// Vector kernel: G lanes per row (G | 64); lane k walks entries k, k+G, ...
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_csr_vector(int64_t n, const int64_t* __restrict__ rp,
-                                                       const int32_t* __restrict__ col,
-                                                       const double* __restrict__ val,
-                                                       const double* __restrict__ x,
-                                                       double* __restrict__ y) {
-    const int lane = threadIdx.x % G;
-    const int64_t rows_per_block = kBlock / G;
-    const int64_t stride = (int64_t)gridDim.x * rows_per_block;
-    for (int64_t row = (int64_t)blockIdx.x * rows_per_block + threadIdx.x / G; row < n;
-         row += stride) {
-        const int64_t b = rp[row], e = rp[row + 1];
-        double s = 0.0;
-        for (int64_t k = b + lane; k < e; k += G) s += val[k] * x[col[k]];
-#pragma unroll
-        for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, G);
-        if (lane == 0) y[row] = s;
-    }
-}
-
+// Z(:,l) += x * w[l]  (dseupd purification, SRC/dseupd.f:840-857)
 __global__ void k_ger_cols(int64_t n, int k, const double* __restrict__ x,
                            const double* __restrict__ w, double* Z, int64_t ldz) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -505,12 +484,28 @@ void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double
                        sc, ws.st, j);
 }
 
-template <int CH>
+#define AHIP_CASES_1_32(M) \
+    M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16) \
+    M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
+
+template <int WM>
 static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const double* V,
-                        int64_t ld, const double* u, const double* w, int with_w, int wslot,
-                        int gate) {
-    hipLaunchKernelGGL(k_dots<CH>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j0, jc, V, ld, u,
-                       w, (int)(w == u), with_w, ws.part, ws.stride, wslot, ws.st, gate);
+                        int64_t ld, const double* u, const double* w, int wslot, int gate) {
+    const dim3 g(ws.nblk), b(kBlock);
+    switch (jc) {
+        case 0:
+            hipLaunchKernelGGL((k_dots<0, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,
+                               ws.stride, wslot, ws.st, gate);
+            break;
+#define AHIP_DOTS_CASE(J)                                                                          \
+    case J:                                                                                        \
+        hipLaunchKernelGGL((k_dots<J, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,       \
+                           ws.stride, wslot, ws.st, gate);                                         \
+        break;
+        AHIP_CASES_1_32(AHIP_DOTS_CASE)
+#undef AHIP_DOTS_CASE
+        default: break;
+    }
 }
 
 void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
@@ -518,36 +513,42 @@ void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, co
     ProfScope ps(gate == 2 ? kProfOther : kProfDots, ws.stream,
                  gate == 2 ? 0.0 : 8.0 * n * (j + 1 + (w != u)));
     if (j == 0) {
-        launch_dots<1>(ws, n, 0, 0, V, ld, u, w, 1, 0, gate);
+        if (w == u) launch_dots<1>(ws, n, 0, 0, V, ld, u, w, 0, gate);
+        else launch_dots<2>(ws, n, 0, 0, V, ld, u, w, 0, gate);
         return;
     }
     for (int j0 = 0; j0 < j; j0 += 32) {
         const int jc = (j - j0 < 32) ? j - j0 : 32;
-        const int ww = (j0 == 0) ? 1 : 0;
-        if (jc <= 8) launch_dots<8>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
-        else if (jc <= 16) launch_dots<16>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
-        else launch_dots<32>(ws, n, j0, jc, V, ld, u, w, ww, j, gate);
+        if (j0 > 0) launch_dots<0>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else if (w == u) launch_dots<1>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else launch_dots<2>(ws, n, j0, jc, V, ld, u, w, j, gate);
     }
 }
 
 void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
             const double* rin, double* rout, bool spec, int gate) {
     const double* c = ws.coef + (size_t)which * ws.stride;
-    const int sp = spec ? 1 : 0;
     ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
                  gate == 2 ? 0.0 : 8.0 * n * (j + 2));
-    if (j <= 8) {
-        hipLaunchKernelGGL(k_update_fused<8>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V, ld,
-                           c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
-    } else if (j <= 16) {
-        hipLaunchKernelGGL(k_update_fused<16>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V,
-                           ld, c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
-    } else if (j <= 32) {
-        hipLaunchKernelGGL(k_update_fused<32>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V,
-                           ld, c, rin, rout, sp, ws.part, ws.stride, ws.st, gate);
+    const dim3 g(ws.nblk), b(kBlock);
+    if (j >= 1 && j <= 32) {
+        switch (j) {
+#define AHIP_UPD_CASE(J)                                                                           \
+    case J:                                                                                        \
+        if (spec)                                                                                  \
+            hipLaunchKernelGGL((k_update_fused<J, true>), g, b, 0, ws.stream, n, V, ld, c, rin,    \
+                               rout, ws.part, ws.stride, ws.st, gate);                             \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_update_fused<J, false>), g, b, 0, ws.stream, n, V, ld, c, rin,   \
+                               rout, ws.part, ws.stride, ws.st, gate);                             \
+        break;
+            AHIP_CASES_1_32(AHIP_UPD_CASE)
+#undef AHIP_UPD_CASE
+            default: break;
+        }
     } else {
-        hipLaunchKernelGGL(k_update_generic, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, j, V, ld,
-                           c, rin, rout, ws.st, gate);
+        hipLaunchKernelGGL(k_update_generic, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
+                           gate);
         if (spec) dots(ws, n, j, V, ld, rout, rout, gate);
     }
 }
@@ -622,25 +623,6 @@ void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const
 void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
               int64_t ldz) {
     hipLaunchKernelGGL(k_ger_cols, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
-}
-
-double csr_bytes(const Csr& A) {
-    return 12.0 * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
-}
-
-void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
-    const int G = A.group;
-    const int rows_per_block = kBlock / G;
-    int64_t g = (A.n + rows_per_block - 1) / rows_per_block;
-    if (g > 65536) g = 65536;
-    if (g < 1) g = 1;
-    switch (G) {
-        case 4: hipLaunchKernelGGL(k_csr_vector<4>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 8: hipLaunchKernelGGL(k_csr_vector<8>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 16: hipLaunchKernelGGL(k_csr_vector<16>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 32: hipLaunchKernelGGL(k_csr_vector<32>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        default: hipLaunchKernelGGL(k_csr_vector<64>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-    }
 }
 
 }  // namespace ahip::dev

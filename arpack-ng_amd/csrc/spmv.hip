@@ -1,0 +1,175 @@
+// CSR SpMV y = A x — the user OP of the `ido = +-1` requests, served on device.
+//
+// HBM-bound (0.17 flop/byte): the job is to stream val (8 B/nnz) and col
+// (4 B/nnz) once at full bandwidth while x is re-read from L2 (for banded
+// operators every x window is shared by ~50 neighbouring rows).
+//
+//  k_csr_stream  (default) CSR-stream: one 256-thread workgroup owns a row
+//                block whose nonzeros (<= TILE) it streams with fully
+//                coalesced loads, every lane issuing all TILE/256 val/col loads
+//                before the first x gather (deep memory-level parallelism);
+//                products go to LDS and each row is reduced by a power-of-two
+//                lane group with wave shuffles.  NT=true marks val/col as
+//                non-temporal so they do not evict x from L2.
+//  k_csr_vector  G lanes per row (fallback for rows longer than TILE).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "device.hpp"
+
+namespace ahip::dev {
+
+namespace {
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_csr_vector(int64_t n, const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const double* __restrict__ x,
+                                                       double* __restrict__ y) {
+    const int lane = threadIdx.x % G;
+    const int64_t rows_per_block = kBlock / G;
+    const int64_t stride = (int64_t)gridDim.x * rows_per_block;
+    for (int64_t row = (int64_t)blockIdx.x * rows_per_block + threadIdx.x / G; row < n;
+         row += stride) {
+        const int64_t b = rp[row], e = rp[row + 1];
+        double s = 0.0;
+        for (int64_t k = b + lane; k < e; k += G) s += val[k] * x[col[k]];
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, G);
+        if (lane == 0) y[row] = s;
+    }
+}
+
+template <class T, bool NT>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int TILE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_csr_stream(const int64_t* __restrict__ rblk,
+                                                       const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const double* __restrict__ x,
+                                                       double* __restrict__ y) {
+    constexpr int PER = TILE / kBlock;
+    __shared__ double prod[TILE];
+    const int t = threadIdx.x;
+    const int64_t r0 = rblk[blockIdx.x], r1 = rblk[blockIdx.x + 1];
+    const int64_t k0 = rp[r0];
+    const int cnt = (int)(rp[r1] - k0);
+    const int last = cnt > 0 ? cnt - 1 : 0;
+    // 1) issue every val/col load of this lane first (clamped, branch-free)
+    double v[PER];
+    int c[PER];
+    if (cnt > 0) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = min(t + u * kBlock, last);
+            v[u] = ld<double, NT>(val + k0 + k);
+            c[u] = ld<int32_t, NT>(col + k0 + k);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) { v[u] = 0.0; c[u] = 0; }
+    }
+    // 2) gather x and park the products in LDS
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int k = t + u * kBlock;
+        const double p = v[u] * x[c[u]];
+        if (k < cnt) prod[k] = p;
+    }
+    __syncthreads();
+    // 3) per-row reduction: L lanes per row (power of two, same wave)
+    const int nrows = (int)(r1 - r0);
+    if (nrows <= kBlock) {
+        int L = 1;
+        while (L * 2 * nrows <= kBlock && L < 64) L *= 2;
+        const int row = t / L, sub = t % L;
+        double s = 0.0;
+        int b = 0, e = 0;
+        if (row < nrows) {
+            b = (int)(rp[r0 + row] - k0);
+            e = (int)(rp[r0 + row + 1] - k0);
+            for (int k = b + sub; k < e; k += L) s += prod[k];
+        }
+        for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        if (row < nrows && sub == 0) y[r0 + row] = s;
+    } else {
+        for (int row = t; row < nrows; row += kBlock) {
+            const int b = (int)(rp[r0 + row] - k0), e = (int)(rp[r0 + row + 1] - k0);
+            double s = 0.0;
+            for (int k = b; k < e; ++k) s += prod[k];
+            y[r0 + row] = s;
+        }
+    }
+}
+
+}  // namespace
+
+int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
+    std::vector<int64_t> rp(A.n + 1);
+    if (hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -2;
+    std::vector<int64_t> blk;
+    blk.reserve(A.nnz / (tile / 2) + 16);
+    blk.push_back(0);
+    int64_t start = 0;
+    for (int64_t i = 0; i < A.n; ++i) {
+        const int64_t len = rp[i + 1] - rp[i];
+        if (len > tile) return -1;
+        // close the block before row i if adding it would exceed the tile
+        if (rp[i + 1] - rp[start] > tile) {
+            blk.push_back(i);
+            start = i;
+        }
+    }
+    blk.push_back(A.n);
+    int64_t* d = nullptr;
+    if (hipMalloc(&d, sizeof(int64_t) * blk.size()) != hipSuccess) return -2;
+    (void)hipMemcpy(d, blk.data(), sizeof(int64_t) * blk.size(), hipMemcpyHostToDevice);
+    *rblk_dev = d;
+    A.rblk = d;
+    A.nrblk = (int64_t)blk.size() - 1;
+    A.tile = tile;
+    return 0;
+}
+
+double csr_bytes(const Csr& A) {
+    return 12.0 * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
+}
+
+void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if (A.kernel != kCsrVector && A.rblk) {
+        const dim3 g((unsigned)A.nrblk), b(kBlock);
+        const bool nt = A.kernel == kCsrStreamNT;
+        if (A.tile == 2048) {
+            if (nt) hipLaunchKernelGGL((k_csr_stream<2048, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            else hipLaunchKernelGGL((k_csr_stream<2048, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+        } else {
+            if (nt) hipLaunchKernelGGL((k_csr_stream<4096, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            else hipLaunchKernelGGL((k_csr_stream<4096, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+        }
+        return;
+    }
+    const int G = A.group;
+    const int rows_per_block = kBlock / G;
+    int64_t g = (A.n + rows_per_block - 1) / rows_per_block;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    switch (G) {
+        case 4: hipLaunchKernelGGL(k_csr_vector<4>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 8: hipLaunchKernelGGL(k_csr_vector<8>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 16: hipLaunchKernelGGL(k_csr_vector<16>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 32: hipLaunchKernelGGL(k_csr_vector<32>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        default: hipLaunchKernelGGL(k_csr_vector<64>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+    }
+}
+
+}  // namespace ahip::dev

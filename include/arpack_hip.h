@@ -93,6 +93,11 @@ int arpack_hip_synchronize(void);
 int arpack_hip_csr_create(arpack_hip_csr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
                           const int32_t* col, const double* val);
 void arpack_hip_csr_destroy(arpack_hip_csr* A);
+/* SpMV kernel choice: 0 vector (G lanes/row), 1 CSR-stream, 2 CSR-stream with
+ * non-temporal val/col loads; tile = nonzeros per workgroup (2048 or 4096). */
+int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
+/* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
+double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
 /* y = A x on device (x, y device pointers). */
 int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y);
 

@@ -1,0 +1,18 @@
+"""Time the SpMV kernel variants on the bench operator (hipEvents, back-to-back)."""
+import json
+import sys
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import load_pkg  # noqa: E402
+
+pkg = load_pkg()
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+A = pkg.CSR.banded_sym(n, 1234, 4096, 25)
+by = 12.0 * A.nnz + 8.0 * (A.n + 1) + 16.0 * A.n
+out = {}
+for name, k, tile in [("vector", 0, 4096), ("stream2048", 1, 2048), ("stream4096", 1, 4096),
+                      ("stream2048_nt", 2, 2048), ("stream4096_nt", 2, 4096)]:
+    A.set_kernel(k, tile)
+    ms = min(A.time_spmv(10) for _ in range(3))
+    out[name] = dict(ms=ms, gbs=by / (ms * 1e-3) / 1e9)
+print(json.dumps(out))
