@@ -35,6 +35,7 @@ struct arpack_hip_csr {
     int64_t row_begin = 0;  // global index of local row 0 (sharded generators)
     int64_t ncols = 0;
     int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
+    void* win = nullptr;      // LDS-window superblock tables (owned)
 };
 
 namespace ahip::gen {
@@ -193,6 +194,7 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
     if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWindow;
     return A;
 }
 
@@ -223,6 +225,7 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     (void)hipFree(A->col);
     (void)hipFree(A->val);
     if (A->rblk) (void)hipFree(A->rblk);
+    if (A->win) (void)hipFree(A->win);
     delete A;
 }
 
@@ -246,6 +249,11 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
 
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
     if (kernel == ahip::dev::kCsrVector) {
+        A->A.kernel = kernel;
+        return 0;
+    }
+    if (kernel == ahip::dev::kCsrWindow || kernel == ahip::dev::kCsrWindowNT) {
+        if (!A->win) return -1;
         A->A.kernel = kernel;
         return 0;
     }

@@ -105,9 +105,25 @@ struct Csr {
     const int64_t* rblk = nullptr;
     int64_t nrblk = 0;
     int tile = 0;
-    int kernel = 0;                   // kCsrVector / kCsrStream / kCsrStreamNT
+    int kernel = 0;                   // CsrKernel
+    // LDS x-window superblocks (csr_analyse_window)
+    const int64_t* w_tiles = nullptr;     // tile row bounds (all superblocks)
+    const int64_t* w_sb_tile0 = nullptr;  // first tile of each superblock (+ end)
+    const int64_t* w_sb_c0 = nullptr;     // first column of each superblock window
+    const int32_t* w_sb_span = nullptr;   // window length
+    int64_t w_nsb = 0;
 };
-enum CsrKernel : int { kCsrVector = 0, kCsrStream = 1, kCsrStreamNT = 2 };
+enum CsrKernel : int {
+    kCsrVector = 0,
+    kCsrStream = 1,
+    kCsrStreamNT = 2,
+    kCsrWindow = 3,
+    kCsrWindowNT = 4,
+};
+// Superblock analysis for the LDS x-window kernel; -1 if some row's column
+// span exceeds the window (then the stream kernel is used).  *owned receives
+// the single device allocation holding the tables.
+int csr_analyse_window(Csr& A, int64_t ncols, void** owned);
 // Build the CSR-stream row blocks (host-side greedy pass over rowptr, once per
 // matrix, like a sparse-library "analysis" step).  Returns 0, or -1 if a row
 // is longer than the tile (the matrix then keeps the vector kernel).

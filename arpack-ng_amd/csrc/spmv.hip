@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <vector>
 
 #include "device.hpp"
@@ -110,7 +112,178 @@ __global__ __launch_bounds__(kBlock) void k_csr_stream(const int64_t* __restrict
     }
 }
 
+// Window kernel: one 1024-thread workgroup owns a SUPERBLOCK of rows whose
+// column span fits the LDS x-window.  It loads x[c0, c0+span) into LDS once
+// (coalesced), then streams the superblock's nonzeros tile by tile: val/col of
+// tile t+1 are issued before the rows of tile t are reduced, x is gathered from
+// LDS (no L2 gather traffic: for banded operators the per-nonzero gathers, not
+// the val/col stream, otherwise saturate the L2).
+constexpr int kWinThreads = 1024;
+constexpr int kWinTile = 8192;   // nonzeros per tile (8 per lane)
+constexpr int kWinX = 10240;     // doubles of x per window (80 KB)
+
+template <bool NT>
+__global__ __launch_bounds__(kWinThreads) void k_csr_window(
+    const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
+    const int64_t* __restrict__ sb_c0, const int32_t* __restrict__ sb_span,
+    const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ y) {
+    constexpr int PER = kWinTile / kWinThreads;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xw = lds;             // kWinX
+    double* prod = lds + kWinX;   // kWinTile
+    const int t = threadIdx.x;
+    const int64_t c0 = sb_c0[blockIdx.x];
+    const int span = sb_span[blockIdx.x];
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    const int64_t tb = sb_tile0[blockIdx.x], te = sb_tile0[blockIdx.x + 1];
+    double v[PER];
+    int c[PER];
+    auto issue = [&](int64_t tile) {
+        const int64_t k0 = rp[tiles[tile]];
+        const int cnt = (int)(rp[tiles[tile + 1]] - k0);
+        if (cnt == 0) {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) { v[u] = 0.0; c[u] = (int)c0; }
+            return cnt;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = min(t + u * kWinThreads, cnt - 1);
+            v[u] = ld<double, NT>(val + k0 + k);
+            c[u] = ld<int32_t, NT>(col + k0 + k);
+        }
+        return cnt;
+    };
+    int cnt = issue(tb);
+    __syncthreads();  // x window ready
+    for (int64_t tile = tb; tile < te; ++tile) {
+        const int64_t r0 = tiles[tile], r1 = tiles[tile + 1];
+        const int64_t k0 = rp[r0];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = t + u * kWinThreads;
+            const double p = v[u] * xw[c[u] - c0];
+            if (k < cnt) prod[k] = p;
+        }
+        int next_cnt = 0;
+        if (tile + 1 < te) next_cnt = issue(tile + 1);  // overlap with the reduction below
+        __syncthreads();
+        const int nrows = (int)(r1 - r0);
+        if (nrows <= kWinThreads) {
+            int L = 1;
+            while (L * 2 * nrows <= kWinThreads && L < 64) L *= 2;
+            const int row = t / L, sub = t % L;
+            double s = 0.0;
+            if (row < nrows) {
+                const int b = (int)(rp[r0 + row] - k0), e = (int)(rp[r0 + row + 1] - k0);
+                for (int k = b + sub; k < e; k += L) s += prod[k];
+            }
+            for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+            if (row < nrows && sub == 0) y[r0 + row] = s;
+        } else {
+            for (int row = t; row < nrows; row += kWinThreads) {
+                const int b = (int)(rp[r0 + row] - k0), e = (int)(rp[r0 + row + 1] - k0);
+                double s = 0.0;
+                for (int k = b; k < e; ++k) s += prod[k];
+                y[r0 + row] = s;
+            }
+        }
+        __syncthreads();  // prod reused by the next tile
+        cnt = next_cnt;
+    }
+}
+
+// per-row [min col, max col] (rows may be unsorted); empty rows -> [INT_MAX, -1]
+__global__ void k_row_span(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                           int32_t* __restrict__ mn, int32_t* __restrict__ mx) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int32_t a = 0x7fffffff, b = -1;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            a = min(a, col[k]);
+            b = max(b, col[k]);
+        }
+        mn[i] = a;
+        mx[i] = b;
+    }
+}
+
 }  // namespace
+
+int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
+    const int64_t n = A.n;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> mn(n), mx(n);
+    int32_t *dmn = nullptr, *dmx = nullptr;
+    if (hipMalloc(&dmn, sizeof(int32_t) * n) || hipMalloc(&dmx, sizeof(int32_t) * n)) return -2;
+    int64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(k_row_span, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dmn, dmx);
+    (void)hipMemcpy(mn.data(), dmn, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(mx.data(), dmx, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
+    (void)hipFree(dmn);
+    (void)hipFree(dmx);
+    // greedy superblocks (column span <= kWinX) split into tiles (<= kWinTile nnz)
+    std::vector<int64_t> tiles{0}, sb_tile0{0}, sb_c0;
+    std::vector<int32_t> sb_span;
+    int64_t sb_start = 0, tile_start = 0;
+    int64_t lo = INT64_MAX, hi = -1;
+    auto close_sb = [&](int64_t end_row) {
+        if (lo > hi) { lo = 0; hi = 0; }
+        sb_c0.push_back(lo);
+        sb_span.push_back((int32_t)(hi - lo + 1));
+        sb_tile0.push_back((int64_t)tiles.size() - 1);
+        (void)end_row;
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = rp[i + 1] - rp[i];
+        if (len > kWinTile) return -1;
+        int64_t nlo = lo, nhi = hi;
+        if (mx[i] >= 0) {
+            nlo = std::min<int64_t>(lo, mn[i]);
+            nhi = std::max<int64_t>(hi, mx[i]);
+            if (mx[i] - mn[i] + 1 > kWinX) return -1;
+        }
+        if (i > sb_start && nhi >= nlo && nhi - nlo + 1 > kWinX) {
+            // close tile and superblock before row i
+            tiles.push_back(i);
+            close_sb(i);
+            sb_start = tile_start = i;
+            lo = INT64_MAX;
+            hi = -1;
+            if (mx[i] >= 0) { lo = mn[i]; hi = mx[i]; }
+            continue;
+        }
+        lo = nlo;
+        hi = nhi;
+        if (i > tile_start && rp[i + 1] - rp[tile_start] > kWinTile) {
+            tiles.push_back(i);
+            tile_start = i;
+        }
+    }
+    tiles.push_back(n);
+    close_sb(n);
+    const int64_t nsb = (int64_t)sb_c0.size();
+    // one device allocation holding all four arrays
+    const size_t b_tiles = sizeof(int64_t) * tiles.size(), b_t0 = sizeof(int64_t) * sb_tile0.size(),
+                 b_c0 = sizeof(int64_t) * nsb, b_sp = sizeof(int32_t) * nsb;
+    char* d = nullptr;
+    if (hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_sp)) return -2;
+    (void)hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d + b_tiles + b_t0 + b_c0, sb_span.data(), b_sp, hipMemcpyHostToDevice);
+    A.w_tiles = (const int64_t*)d;
+    A.w_sb_tile0 = (const int64_t*)(d + b_tiles);
+    A.w_sb_c0 = (const int64_t*)(d + b_tiles + b_t0);
+    A.w_sb_span = (const int32_t*)(d + b_tiles + b_t0 + b_c0);
+    A.w_nsb = nsb;
+    *owned = d;
+    (void)ncols;
+    return 0;
+}
 
 int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
     std::vector<int64_t> rp(A.n + 1);
@@ -146,6 +319,24 @@ double csr_bytes(const Csr& A) {
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if ((A.kernel == kCsrWindow || A.kernel == kCsrWindowNT) && A.w_nsb > 0) {
+        const size_t lds = sizeof(double) * (kWinX + kWinTile);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_csr_window<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            (void)hipFuncSetAttribute((const void*)k_csr_window<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        if (A.kernel == kCsrWindowNT)
+            hipLaunchKernelGGL((k_csr_window<true>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+                               A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.val, x, y);
+        else
+            hipLaunchKernelGGL((k_csr_window<false>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+                               A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.val, x, y);
+        return;
+    }
     if (A.kernel != kCsrVector && A.rblk) {
         const dim3 g((unsigned)A.nrblk), b(kBlock);
         const bool nt = A.kernel == kCsrStreamNT;
