@@ -441,3 +441,83 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
         else:
             z = z.reshape(s.nev, n)[:nconv].T
     return d, (z if rvec else None), res
+
+
+# ----------------------------------------------------------- multi-GPU (RCCL)
+def _declare_dist(L):
+    L.arpack_hip_comm_unique_id.argtypes = [C.c_char_p]
+    L.arpack_hip_comm_init.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_int]
+    L.arpack_hip_comm_allreduce.argtypes = [C.c_void_p, C.c_int]
+    L.arpack_hip_dist_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_int64, C.c_int64]
+    L.arpack_hip_dist_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_dist_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int64)] * 4
+    L.arpack_hip_pdsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p,
+                                                _I, C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI,
+                                                _PI, _PD, _PD, _I, _PI]
+
+
+def comm_unique_id() -> bytes:
+    L = lib()
+    _declare_dist(L)
+    buf = C.create_string_buffer(128)
+    if L.arpack_hip_comm_unique_id(buf) != 0:
+        raise RuntimeError("ncclGetUniqueId failed")
+    return buf.raw
+
+
+def comm_init(nranks: int, rank: int, uid: bytes, device: int = 0):
+    """Create the engine's RCCL communicator (one process per GPU)."""
+    L = lib()
+    _declare_dist(L)
+    if L.arpack_hip_comm_init(nranks, rank, C.c_char_p(bytes(uid)), device) != 0:
+        raise RuntimeError("ncclCommInitRank failed")
+
+
+def comm_destroy():
+    lib().arpack_hip_comm_destroy()
+
+
+def partition_rows(n: int, nranks: int, rank: int):
+    """Contiguous balanced row blocks (PARPACK/TESTS/MPI/icb_parpack_c.c:60-77)."""
+    base, rem = divmod(n, nranks)
+    r0 = rank * base + min(rank, rem)
+    return r0, r0 + base + (1 if rank < rem else 0)
+
+
+class DistOp:
+    """This rank's rows of a row-block distributed operator (collective setup)."""
+
+    def __init__(self, A: CSR, n_global: int, row0: int):
+        L = lib()
+        _declare_dist(L)
+        h = C.c_void_p()
+        rc = L.arpack_hip_dist_create(C.byref(h), A.h, n_global, row0)
+        if rc != 0:
+            raise RuntimeError(f"arpack_hip_dist_create failed ({rc})")
+        self.h = h
+        self.A = A  # keeps the local CSR alive
+        self.n_global, self.row0, self.nloc = n_global, row0, A.n
+
+    def info(self):
+        v = [C.c_int64() for _ in range(4)]
+        lib().arpack_hip_dist_info(self.h, *[C.byref(x) for x in v])
+        return dict(zip(["halo_lo", "halo_hi", "send_lo", "send_hi"], [x.value for x in v]))
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_dist_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def pdsaupd_cycles(s: "SymRci", D: DistOp, max_cycles: int) -> int:
+    """Distributed free-running dsaupd on this rank's slice (s.n = local rows)."""
+    tol = C.c_double(s.tol)
+    lib().arpack_hip_pdsaupd_csr_cycles(D.h, int(max_cycles), _ip(s.ido), s.bmat.encode(), s.n,
+                                        s.which.encode(), s.nev, C.byref(tol), _ptr(s.resid),
+                                        s.ncv, _ptr(s.v), s.ldv, _ip(s.iparam), _ip(s.ipntr),
+                                        _ptr(s.workd), s.workl.ctypes.data, s.lworkl, _ip(s.info))
+    s.tol = tol.value
+    return int(s.ido[0])

@@ -15,6 +15,7 @@
 #include "engine.hpp"
 
 const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A);
+const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
 
 namespace ahip {
 
@@ -79,7 +80,8 @@ static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lw
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                      double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
                      double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr,
-                     int max_cycles = -1) {
+                     int max_cycles = -1, const DistOp* dist = nullptr) {
+    if (dist) csr = dist->A;
     std::lock_guard<std::mutex> lk(g_mu);
     SymSolver* S = nullptr;
     if (*ido == 0) {
@@ -89,6 +91,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
         int ierr = sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
         if (csr && (mode != 1 || bmat[0] != 'I' || csr->n != n)) ierr = (ierr ? ierr : -11);
+        if (dist && dist->nloc != n) ierr = (ierr ? ierr : -1);
         if (ierr != 0) {
             *info = ierr;
             *ido = 99;
@@ -131,6 +134,10 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             S->free_run = true;
             S->csr = csr;
         }
+        if (dist) {
+            S->dist = dist;
+            S->row0 = dist->row0;
+        }
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
@@ -164,7 +171,8 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const RciReq r = S->ctx.req;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             dev::prof_begin(dev::kProfSpmv, S->a.stream);
-            dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
+            else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
             dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
             continue;
         }
@@ -233,6 +241,18 @@ void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* 
                                   int* ipntr, double* workd, double* workl, int lworkl, int* info) {
     sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
              info, ahip_csr_view(A), max_cycles);
+}
+
+// Row-block distributed solve (PARPACK's pdsaupd decomposition, n = LOCAL rows):
+// each rank calls this with its slice of resid/V/workd; see dist.hpp.
+void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,
+                                   char const* bmat, int n, char const* which, int nev,
+                                   double* tol, double* resid, int ncv, double* v, int ldv,
+                                   int* iparam, int* ipntr, double* workd, double* workl,
+                                   int lworkl, int* info) {
+    const DistOp* d = ahip_dist_view(D);
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, d->A, max_cycles, d);
 }
 
 void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }

@@ -27,16 +27,7 @@
 #include "device.hpp"
 #include "../../include/arpack_hip.h"
 
-struct arpack_hip_csr {
-    ahip::dev::Csr A;
-    int64_t* rowptr = nullptr;
-    int32_t* col = nullptr;
-    double* val = nullptr;
-    int64_t row_begin = 0;  // global index of local row 0 (sharded generators)
-    int64_t ncols = 0;
-    int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
-    void* win = nullptr;      // LDS-window superblock tables (owned)
-};
+#include "csr_internal.hpp"
 
 namespace ahip::gen {
 
@@ -194,7 +185,7 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
     if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWindow;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVec;
     return A;
 }
 
@@ -252,7 +243,7 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
         A->A.kernel = kernel;
         return 0;
     }
-    if (kernel == ahip::dev::kCsrWindow || kernel == ahip::dev::kCsrWindowNT) {
+    if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVec8) {
         if (!A->win) return -1;
         A->A.kernel = kernel;
         return 0;
@@ -332,3 +323,51 @@ int arpack_hip_gen_banded_sym(arpack_hip_csr** out, int64_t n, int64_t r0, int64
 }  // extern "C"
 
 const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A) { return &A->A; }
+
+// ------------------------------------------------------------ remap helpers --
+namespace {
+__global__ void k_shift_cols(int64_t nnz, int32_t* col, int64_t shift) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += stride)
+        col[k] = (int32_t)((int64_t)col[k] - shift);
+}
+__global__ void k_col_span(int64_t nnz, const int32_t* col, int* mn, int* mx) {
+    int a = 0x7fffffff, b = -1;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += stride) {
+        a = min(a, col[k]);
+        b = max(b, col[k]);
+    }
+    atomicMin(mn, a);
+    atomicMax(mx, b);
+}
+}  // namespace
+
+int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax) {
+    int* d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(int))) return -1;
+    const int init[2] = {0x7fffffff, -1};
+    (void)hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice);
+    if (A->A.nnz > 0)
+        hipLaunchKernelGGL(k_col_span, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz, A->col, d,
+                           d + 1);
+    int h[2];
+    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    *cmin = h[0];
+    *cmax = h[1];
+    return 0;
+}
+
+int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
+    if (A->A.nnz > 0 && shift != 0)
+        hipLaunchKernelGGL(k_shift_cols, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz, A->col, shift);
+    (void)hipDeviceSynchronize();
+    A->ncols = ncols;
+    if (A->win) (void)hipFree(A->win);
+    A->win = nullptr;
+    A->A.w_nsb = 0;
+    A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVec;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

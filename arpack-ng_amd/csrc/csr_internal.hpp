@@ -1,0 +1,22 @@
+// Definition of the opaque arpack_hip_csr handle (shared by csr.hip / dist.hip).
+#pragma once
+#include <cstdint>
+
+#include "device.hpp"
+
+struct arpack_hip_csr {
+    ahip::dev::Csr A;
+    int64_t* rowptr = nullptr;
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    int64_t row_begin = 0;  // global index of local row 0 (sharded generators)
+    int64_t ncols = 0;
+    int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
+    void* win = nullptr;      // LDS-window superblock tables (owned)
+};
+
+// remap every column index c -> c - shift (int32) and rebuild the SpMV
+// analysis for an x vector of length ncols; 0 on success
+int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols);
+// per-matrix [min col, max col] over all rows (device reduction)
+int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax);

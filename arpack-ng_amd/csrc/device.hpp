@@ -75,7 +75,9 @@ void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, co
 void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
             const double* rin, double* rout, bool spec, int gate);
 // single-block fixed-order finalize of m = j+1 sums and the phase logic
-void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate);
+// from_sums: the m sums are already in ws.sums (reduced across ranks).
+void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
+              bool from_sums = false);
 // resid = 0 if st.zero
 void zero_if(const Workspace& ws, int64_t n, double* r);
 // V(:,0:kev) = V(:,0:kplusp) * Q(:,0:kev) in place (row-local) and
@@ -86,7 +88,8 @@ void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp
 void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k, int nz,
              double* Z, int64_t ldz);
 // dlarnv(idist=2) continuation: x[m] = 2*(seed*a^(m+1) mod 2^48)/2^48 - 1
-void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x);
+// offset: global index of x[0] in the stream (row-block sharding)
+void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x, int64_t offset = 0);
 void copy(hipStream_t s, int64_t n, const double* src, double* dst);
 void scal(hipStream_t s, int64_t n, double a, double* x);
 void fill(hipStream_t s, int64_t n, double a, double* x);
@@ -119,6 +122,9 @@ enum CsrKernel : int {
     kCsrStreamNT = 2,
     kCsrWindow = 3,
     kCsrWindowNT = 4,
+    kCsrWVec = 5,
+    kCsrWVecNT = 6,
+    kCsrWVec8 = 7,
 };
 // Superblock analysis for the LDS x-window kernel; -1 if some row's column
 // span exceeds the window (then the stream kernel is used).  *owned receives

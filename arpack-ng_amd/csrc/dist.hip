@@ -1,0 +1,103 @@
+// Distributed operator setup (halo plan) and the distributed SpMV.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/arpack_hip.h"
+#include "csr_internal.hpp"
+#include "dist.hpp"
+
+namespace ahip {
+void comm_halo(const Comm* c, const DistOp& D, hipStream_t s);
+
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
+    if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
+    comm_halo(D.comm, D, s);
+    dev::csr_spmv(s, *D.A, D.x_ext, y);
+}
+}  // namespace ahip
+
+struct arpack_hip_dist {
+    ahip::DistOp D;
+};
+
+extern "C" {
+
+int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_global,
+                           int64_t row0) {
+    using namespace ahip;
+    const Comm* c = comm_get();
+    const int P = comm_size(c), r = comm_rank(c);
+    const int64_t nloc = A->A.n;
+    int64_t cmin = 0, cmax = -1;
+    if (ahip_csr_col_span(A, &cmin, &cmax) != 0) return -1;
+    if (cmax < 0) cmin = cmax = row0;  // empty operator block
+    // share [row0, nloc, cmin, cmax] of every rank (allreduce of a one-hot table)
+    std::vector<double> tab(4 * (size_t)P, 0.0);
+    tab[4 * r + 0] = (double)row0;
+    tab[4 * r + 1] = (double)nloc;
+    tab[4 * r + 2] = (double)cmin;
+    tab[4 * r + 3] = (double)cmax;
+    double* d = nullptr;
+    if (hipMalloc(&d, sizeof(double) * tab.size())) return -1;
+    (void)hipMemcpy(d, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice);
+    comm_allreduce_sum(c, d, (int)tab.size(), nullptr);
+    (void)hipMemcpy(tab.data(), d, sizeof(double) * tab.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    auto R0 = [&](int q) { return (int64_t)tab[4 * q]; };
+    auto NL = [&](int q) { return (int64_t)tab[4 * q + 1]; };
+    auto HLO = [&](int q) { return std::max<int64_t>(0, R0(q) - (int64_t)tab[4 * q + 2]); };
+    auto HHI = [&](int q) {
+        return std::max<int64_t>(0, (int64_t)tab[4 * q + 3] - (R0(q) + NL(q) - 1));
+    };
+    for (int q = 0; q < P; ++q) {  // contiguous blocks, halos only from the neighbours
+        if (q > 0 && R0(q) != R0(q - 1) + NL(q - 1)) return -3;
+        if (q > 0 && HLO(q) > NL(q - 1)) return -4;
+        if (q < P - 1 && HHI(q) > NL(q + 1)) return -4;
+        if ((q == 0 && HLO(q) > 0) || (q == P - 1 && HHI(q) > 0)) return -4;
+    }
+    auto* D = new arpack_hip_dist;
+    DistOp& o = D->D;
+    o.n_global = n_global;
+    o.row0 = row0;
+    o.nloc = nloc;
+    o.halo_lo = HLO(r);
+    o.halo_hi = HHI(r);
+    o.send_lo = r > 0 ? HHI(r - 1) : 0;
+    o.send_hi = r < P - 1 ? HLO(r + 1) : 0;
+    o.comm = c;
+    const int64_t next = o.halo_lo + nloc + o.halo_hi;
+    if (hipMalloc(&o.x_ext, sizeof(double) * (next > 0 ? next : 1))) {
+        delete D;
+        return -1;
+    }
+    (void)hipMemset(o.x_ext, 0, sizeof(double) * (next > 0 ? next : 1));
+    // local column indices relative to x_ext
+    if (ahip_csr_remap_cols(A, row0 - o.halo_lo, next) != 0) {
+        (void)hipFree(o.x_ext);
+        delete D;
+        return -1;
+    }
+    o.A = &A->A;
+    *out = D;
+    return 0;
+}
+
+void arpack_hip_dist_destroy(arpack_hip_dist* D) {
+    if (!D) return;
+    (void)hipFree(D->D.x_ext);
+    delete D;
+}
+
+int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
+                         int64_t* send_lo, int64_t* send_hi) {
+    *halo_lo = D->D.halo_lo;
+    *halo_hi = D->D.halo_hi;
+    *send_lo = D->D.send_lo;
+    *send_hi = D->D.send_hi;
+    return 0;
+}
+
+}  // extern "C"
+
+const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D) { return &D->D; }

@@ -1,0 +1,41 @@
+// Row-block distribution over GPUs (PARPACK's decomposition,
+// PARPACK/SRC/MPI/pdsaitr.f): one process per GPU, rank r owns rows
+// [row0, row0 + nloc) of V, resid, workd and of the operator.  Every inner
+// product is a local partial + one RCCL allreduce of <= ncv+1 doubles (fused:
+// [V'w ; w'w] in one collective where PARPACK issues 2-3 MPI_ALLREDUCEs); V*Q
+// is row-local (pdsapps.f has no communication).  The SpMV needs the x entries
+// of the neighbouring ranks inside its column span: a halo exchanged with
+// ncclSend/ncclRecv into an extended x buffer [halo_lo | local | halo_hi].
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device.hpp"
+
+namespace ahip {
+
+struct Comm;  // RCCL communicator (comm.cpp)
+Comm* comm_get();
+int comm_rank(const Comm*);
+int comm_size(const Comm*);
+// in-place SUM allreduce of `count` doubles on `stream`
+void comm_allreduce_sum(const Comm*, double* dev, int count, hipStream_t stream);
+
+// Distributed operator: the local CSR (columns relative to the start of x_ext)
+// plus the halo plan.
+struct DistOp {
+    int64_t n_global = 0, row0 = 0, nloc = 0;
+    int64_t halo_lo = 0, halo_hi = 0;   // x_ext = [halo_lo | nloc | halo_hi]
+    int64_t send_lo = 0, send_hi = 0;   // my first rows -> rank-1, my last rows -> rank+1
+    double* x_ext = nullptr;            // device, halo_lo + nloc + halo_hi
+    const dev::Csr* A = nullptr;        // local rows, local (x_ext) column indices
+    const Comm* comm = nullptr;
+    double* x_mid() const { return x_ext + halo_lo; }
+};
+
+// y = A_loc * x for the distributed operator: copy x into x_ext (skipped when
+// the engine already placed it there), halo exchange, local SpMV.
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y);
+
+}  // namespace ahip

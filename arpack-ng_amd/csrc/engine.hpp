@@ -9,6 +9,7 @@
 
 #include "dense.hpp"
 #include "device.hpp"
+#include "dist.hpp"
 #include "rci.hpp"
 
 namespace ahip {
@@ -87,6 +88,10 @@ public:
     // ido = kPauseIdo; -1 disables.
     static constexpr int kPauseIdo = 98;
     int pause_budget = -1;
+    // multi-GPU row-block distribution (nullptr: single GPU): n is then the
+    // LOCAL row count and row0 the global index of local row 0
+    const DistOp* dist = nullptr;
+    int64_t row0 = 0;
     const dev::Csr* csr = nullptr;
 
     // workl offsets (0-based) of h, ritz, bounds, q, w
@@ -104,6 +109,7 @@ private:
     RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp);
     void read_state();
     void write_state();
+    void fin(int m, dev::FinPhase ph, int j, int rstart, int gate);
     double* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
 public:
     const double* op_x = nullptr;  // device pointers of the pending OP request

@@ -38,7 +38,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 // optional extra value) as this block's partial row.
 template <int CH>
 __device__ __forceinline__ void block_partials(double (&acc)[CH], int jc, double extra,
-                                               bool with_extra, double* prow, int extra_slot) {
+                                               bool with_extra, double* part, int col0,
+                                               int extra_slot) {
+    // k-major layout part[slot * nblk + block]: the finalize reads each slot
+    // as one contiguous (coalesced) run
     __shared__ double red[kBlock / 64][CH + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -58,13 +61,13 @@ __device__ __forceinline__ void block_partials(double (&acc)[CH], int jc, double
         double s = 0.0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += red[w][t];
-        prow[t] = s;
+        part[(size_t)(col0 + t) * gridDim.x + blockIdx.x] = s;
     }
     if (with_extra && t == kBlock - 1) {
         double s = 0.0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += red[w][CH];
-        prow[extra_slot] = s;
+        part[(size_t)extra_slot * gridDim.x + blockIdx.x] = s;
     }
 }
 
@@ -128,8 +131,7 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double
         for (int k = 0; k < J; ++k) acc[k] += Vb[i + (int64_t)k * ld] * ui;
     }
     constexpr int JJ = J > 0 ? J : 1;
-    block_partials<JJ>(acc, J, aw, WM != 0, part + (int64_t)blockIdx.x * pstride + j0,
-                                  wslot - j0);
+    block_partials<JJ>(acc, J, aw, WM != 0, part, j0, wslot);
 }
 
 // ----------------------------------------------------------------- update ---
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
             for (int k = 0; k < J; ++k) acc[k] += vrow[k] * r;
         }
     }
-    if constexpr (SPEC) block_partials<J>(acc, J, rr, true, part + (int64_t)blockIdx.x * pstride, J);
+    if constexpr (SPEC) block_partials<J>(acc, J, rr, true, part, 0, J);
 }
 
 // generic (any j): no fused dots
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_update_generic(int64_t n, int j,
 
 // --------------------------------------------------------------- finalize ---
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
-                                                   int pstride, int m, int phase, int j,
+                                                   int from_sums, int m, int phase, int j,
                                                    int rstart, int gate, double* __restrict__ sums,
                                                    double* __restrict__ coef, int cstride,
                                                    double* __restrict__ rec,
@@ -193,7 +195,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int k = wave; k < m; k += 16) {
         double s = 0.0;
-        for (int b = lane; b < nblk; b += 64) s += part[(int64_t)b * pstride + k];
+        if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
+            s = lane == 0 ? sums[k] : 0.0;
+        } else {
+            for (int b = lane; b < nblk; b += 64) s += part[(int64_t)k * nblk + b];
+        }
         s = wave_sum(s);
         if (lane == 0) s_sum[k] = s;
     }
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, double* V, int6
         rr += ri * ri;
     }
     double acc[1] = {0.0};
-    block_partials<1>(acc, 0, rr, true, part + (int64_t)blockIdx.x * pstride, 0);
+    block_partials<1>(acc, 0, rr, true, part, 0, 0);
 }
 
 __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
         rr += ri * ri;
     }
     double acc[1] = {0.0};
-    block_partials<1>(acc, 0, rr, true, part + (int64_t)blockIdx.x * pstride, 0);
+    block_partials<1>(acc, 0, rr, true, part, 0, 0);
 }
 
 // Z = V(:,0:k) * M(k x nz) ; row-local, so Z may alias V (rows held in registers)
@@ -373,11 +379,11 @@ constexpr uint64_t kMask48 = (1ull << 48) - 1;
 
 __device__ __forceinline__ uint64_t mulmod48(uint64_t a, uint64_t b) { return (a * b) & kMask48; }
 
-__global__ void k_larnv(int64_t n, uint64_t seed, double* __restrict__ x) {
+__global__ void k_larnv(int64_t n, uint64_t seed, int64_t offset, double* __restrict__ x) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         // a^(i+1) by square-and-multiply
-        uint64_t e = (uint64_t)i + 1, base = kLcgA, p = 1;
+        uint64_t e = (uint64_t)(i + offset) + 1, base = kLcgA, p = 1;
         while (e) {
             if (e & 1) p = mulmod48(p, base);
             base = mulmod48(base, base);
@@ -553,9 +559,9 @@ void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, 
     }
 }
 
-void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate) {
-    ProfScope ps(kProfFinalize, ws.stream, 8.0 * ws.nblk * m);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, ws.stride, m,
+void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums) {
+    ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * m);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, (int)from_sums, m,
                        (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
 }
 
@@ -603,8 +609,8 @@ void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k,
                            ldz);
 }
 
-void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x) {
-    hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, x);
+void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x, int64_t offset) {
+    hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x);
 }
 
 void copy(hipStream_t s, int64_t n, const double* src, double* dst) {

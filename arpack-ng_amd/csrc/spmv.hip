@@ -135,50 +135,57 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_window(
     const int t = threadIdx.x;
     const int64_t c0 = sb_c0[blockIdx.x];
     const int span = sb_span[blockIdx.x];
-    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
     const int64_t tb = sb_tile0[blockIdx.x], te = sb_tile0[blockIdx.x + 1];
-    double v[PER];
-    int c[PER];
-    auto issue = [&](int64_t tile) {
-        const int64_t k0 = rp[tiles[tile]];
-        const int cnt = (int)(rp[tiles[tile + 1]] - k0);
-        if (cnt == 0) {
-#pragma unroll
-            for (int u = 0; u < PER; ++u) { v[u] = 0.0; c[u] = (int)c0; }
-            return cnt;
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int k = min(t + u * kWinThreads, cnt - 1);
-            v[u] = ld<double, NT>(val + k0 + k);
-            c[u] = ld<int32_t, NT>(col + k0 + k);
-        }
-        return cnt;
+
+    // One tile in registers: its val/col slice and this lane's reduction row.
+    struct Buf {
+        double v[PER];
+        int c[PER];
+        int cnt, nrows, L, rb, re;
+        int64_t r0, k0;
     };
-    int cnt = issue(tb);
-    __syncthreads();  // x window ready
-    for (int64_t tile = tb; tile < te; ++tile) {
-        const int64_t r0 = tiles[tile], r1 = tiles[tile + 1];
-        const int64_t k0 = rp[r0];
+    auto issue = [&](int64_t tile, Buf& B) {
+        B.r0 = tiles[tile];
+        const int64_t r1 = tiles[tile + 1];
+        B.k0 = rp[B.r0];
+        B.cnt = (int)(rp[r1] - B.k0);
+        B.nrows = (int)(r1 - B.r0);
+        if (B.cnt == 0) {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) { B.v[u] = 0.0; B.c[u] = (int)c0; }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int k = min(t + u * kWinThreads, B.cnt - 1);
+                B.v[u] = ld<double, NT>(val + B.k0 + k);
+                B.c[u] = ld<int32_t, NT>(col + B.k0 + k);
+            }
+        }
+        int L = 1;
+        while (L * 2 * B.nrows <= kWinThreads && L < 64) L *= 2;
+        B.L = L;
+        const int row = t / L;
+        B.rb = B.re = 0;
+        if (B.nrows <= kWinThreads && row < B.nrows) {  // prefetch the row bounds
+            B.rb = (int)(rp[B.r0 + row] - B.k0);
+            B.re = (int)(rp[B.r0 + row + 1] - B.k0);
+        }
+    };
+    auto step = [&](int64_t tile, Buf& B) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int k = t + u * kWinThreads;
-            const double p = v[u] * xw[c[u] - c0];
-            if (k < cnt) prod[k] = p;
+            const double p = B.v[u] * xw[B.c[u] - c0];
+            if (k < B.cnt) prod[k] = p;
         }
-        int next_cnt = 0;
-        if (tile + 1 < te) next_cnt = issue(tile + 1);  // overlap with the reduction below
+        const int nrows = B.nrows, L = B.L, rb = B.rb, re = B.re;
+        const int64_t r0 = B.r0, k0 = B.k0;
+        if (tile + 2 < te) issue(tile + 2, B);  // two tiles stay in flight
         __syncthreads();
-        const int nrows = (int)(r1 - r0);
         if (nrows <= kWinThreads) {
-            int L = 1;
-            while (L * 2 * nrows <= kWinThreads && L < 64) L *= 2;
             const int row = t / L, sub = t % L;
             double s = 0.0;
-            if (row < nrows) {
-                const int b = (int)(rp[r0 + row] - k0), e = (int)(rp[r0 + row + 1] - k0);
-                for (int k = b + sub; k < e; k += L) s += prod[k];
-            }
+            for (int k = rb + sub; k < re; k += L) s += prod[k];
             for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
             if (row < nrows && sub == 0) y[r0 + row] = s;
         } else {
@@ -189,8 +196,97 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_window(
                 y[r0 + row] = s;
             }
         }
-        __syncthreads();  // prod reused by the next tile
-        cnt = next_cnt;
+        __syncthreads();  // prod is reused by the next tile
+    };
+    Buf A, B;
+    issue(tb, A);
+    if (tb + 1 < te) issue(tb + 1, B);
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    __syncthreads();  // x window ready
+    for (int64_t tile = tb; tile < te; tile += 2) {
+        step(tile, A);
+        if (tile + 1 < te) step(tile + 1, B);
+    }
+}
+
+// Window-vector kernel: same LDS x-window superblocks, but rows are reduced
+// straight from registers — L lanes per row, each lane holding U of the row's
+// nonzeros — so there is no product buffer and no barrier after the window
+// load (LDS = the window only: two workgroups per CU).  Rows of the next pass
+// are loaded before the current pass is reduced (two passes in flight).
+template <int L, int U, bool NT>
+__global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
+    const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
+    const int64_t* __restrict__ sb_c0, const int32_t* __restrict__ sb_span,
+    const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xw = lds;
+    constexpr int RPP = kWinThreads / L;  // rows per pass
+    const int t = threadIdx.x, sub = t % L;
+    const int64_t c0 = sb_c0[blockIdx.x];
+    const int span = sb_span[blockIdx.x];
+    const int64_t R0 = tiles[sb_tile0[blockIdx.x]], R1 = tiles[sb_tile0[blockIdx.x + 1]];
+    const int64_t npass = (R1 - R0 + RPP - 1) / RPP;
+    // Pipeline: row bounds are loaded two passes ahead of the val/col loads,
+    // which run two passes ahead of the reduction.
+    struct Bounds {
+        int64_t b, e;
+    };
+    struct Buf {
+        double v[U];
+        int c[U];
+        int64_t row, b, e;
+    };
+    auto bounds = [&](int64_t pass) {
+        Bounds r{0, 0};
+        const int64_t row = R0 + pass * RPP + t / L;
+        if (pass < npass && row < R1) {
+            r.b = rp[row];
+            r.e = rp[row + 1];
+        }
+        return r;
+    };
+    auto issue = [&](int64_t pass, const Bounds& bd, Buf& B) {
+        B.row = R0 + pass * RPP + t / L;
+        B.b = bd.b;
+        B.e = bd.e;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = B.b + sub + u * L;
+            const bool in = k < B.e;
+            B.v[u] = in ? ld<double, NT>(val + k) : 0.0;
+            B.c[u] = in ? ld<int32_t, NT>(col + k) : (int)c0;
+        }
+    };
+    auto finish = [&](Buf& B) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += B.v[u] * xw[B.c[u] - c0];
+        for (int64_t k = B.b + sub + U * L; k < B.e; k += L) s += val[k] * xw[col[k] - c0];
+#pragma unroll
+        for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        if (B.row < R1 && sub == 0) y[B.row] = s;
+    };
+    Buf A, B;
+    issue(0, bounds(0), A);
+    issue(1, bounds(1), B);
+    Bounds nA = bounds(2), nB = bounds(3);
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    __syncthreads();
+    for (int64_t p = 0; p < npass; p += 2) {
+        finish(A);
+        if (p + 2 < npass) {
+            issue(p + 2, nA, A);
+            nA = bounds(p + 4);
+        }
+        if (p + 1 < npass) {
+            finish(B);
+            if (p + 3 < npass) {
+                issue(p + 3, nB, B);
+                nB = bounds(p + 5);
+            }
+        }
     }
 }
 
@@ -318,7 +414,46 @@ double csr_bytes(const Csr& A) {
     return 12.0 * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
 }
 
+template <int L, int U>
+static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y, bool nt) {
+    const size_t lds = sizeof(double) * kWinX;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    const dim3 g((unsigned)A.w_nsb), b(kWinThreads);
+    if (nt)
+        hipLaunchKernelGGL((k_csr_wvec<L, U, true>), g, b, lds, s, A.w_sb_tile0, A.w_tiles, A.w_sb_c0,
+                           A.w_sb_span, A.rowptr, A.col, A.val, x, y);
+    else
+        hipLaunchKernelGGL((k_csr_wvec<L, U, false>), g, b, lds, s, A.w_sb_tile0, A.w_tiles, A.w_sb_c0,
+                           A.w_sb_span, A.rowptr, A.col, A.val, x, y);
+}
+
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if ((A.kernel == kCsrWVec || A.kernel == kCsrWVecNT) && A.w_nsb > 0) {
+        const bool nt = A.kernel == kCsrWVecNT;
+        const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;
+        if (avg <= 6) launch_wvec<4, 2>(s, A, x, y, nt);
+        else if (avg <= 12) launch_wvec<8, 2>(s, A, x, y, nt);
+        else if (avg <= 28) launch_wvec<8, 4>(s, A, x, y, nt);
+        else if (avg <= 60) launch_wvec<16, 4>(s, A, x, y, nt);
+        else if (avg <= 120) launch_wvec<32, 4>(s, A, x, y, nt);
+        else launch_wvec<64, 4>(s, A, x, y, nt);
+        return;
+    }
+    if (A.kernel == kCsrWVec8 && A.w_nsb > 0) {  // fewer lanes per row, more loads per lane
+        const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;
+        if (avg <= 12) launch_wvec<4, 4>(s, A, x, y, false);
+        else if (avg <= 28) launch_wvec<4, 8>(s, A, x, y, false);
+        else if (avg <= 60) launch_wvec<8, 8>(s, A, x, y, false);
+        else launch_wvec<16, 8>(s, A, x, y, false);
+        return;
+    }
     if ((A.kernel == kCsrWindow || A.kernel == kCsrWindowNT) && A.w_nsb > 0) {
         const size_t lds = sizeof(double) * (kWinX + kWinTile);
         static bool attr = false;
@@ -364,3 +499,56 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
 }
 
 }  // namespace ahip::dev
+
+// ------------------------------------------------------------ HBM probe ---
+// Read-only streaming probe (sum of a large buffer) at 8- or 16-byte loads per
+// lane: the achievable HBM read rate that the SpMV/Gram-Schmidt kernels are
+// compared against.
+namespace ahip::dev {
+namespace {
+template <int W>
+__global__ __launch_bounds__(256) void k_probe(int64_t n8, const double* __restrict__ a,
+                                               double* __restrict__ out) {
+    double s = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    if constexpr (W == 16) {
+        const double2* a2 = reinterpret_cast<const double2*>(a);
+        const int64_t n16 = n8 / 2;
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
+            const double2 v = a2[i];
+            s += v.x + v.y;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) s += a[i];
+    }
+    if (s == 12345.678) out[0] = s;  // keep the loads alive
+}
+}  // namespace
+}  // namespace ahip::dev
+
+extern "C" double arpack_hip_stream_probe(int64_t nbytes, int width, int grid, int reps) {
+    double* a = nullptr;
+    double* o = nullptr;
+    if (hipMalloc(&a, nbytes) || hipMalloc(&o, 8)) return -1.0;
+    (void)hipMemset(a, 0, nbytes);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const int64_t n8 = nbytes / 8;
+    auto launch = [&]() {
+        if (width == 16)
+            hipLaunchKernelGGL(ahip::dev::k_probe<16>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
+        else
+            hipLaunchKernelGGL(ahip::dev::k_probe<8>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
+    };
+    launch();
+    (void)hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; ++r) launch();
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipFree(a);
+    (void)hipFree(o);
+    return (double)nbytes * reps / (ms * 1e-3) / 1e9;
+}

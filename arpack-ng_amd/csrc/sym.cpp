@@ -121,6 +121,18 @@ RciAwait SymSolver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* 
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
+// Finalize of a reduction; with a multi-GPU distribution the local sums are
+// allreduced across ranks (one RCCL collective) before the phase logic runs.
+void SymSolver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
+    if (dist && comm_size(dist->comm) > 1) {
+        dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate);
+        comm_allreduce_sum(dist->comm, ws.sums, m, a.stream);
+        if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true);
+    } else {
+        dev::finalize(ws, m, ph, j, rstart, gate);
+    }
+}
+
 void SymSolver::read_state() {
     ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
@@ -138,8 +150,8 @@ Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
     double* wd = a.d_workd;
     ierr = 0;
     if (!initv) {  // dlarnv(idist=2, iseed, n, resid) — SRC/dgetv0.f:234-237
-        dev::larnv_uniform(ws, nn, g_dseed, a.d_resid);
-        g_dseed = lcg_advance(g_dseed, (uint64_t)nn);
+        dev::larnv_uniform(ws, nn, g_dseed, a.d_resid, row0);
+        g_dseed = lcg_advance(g_dseed, (uint64_t)(dist ? dist->n_global : nn));
     }
     if (itry == 1) {  // force into the range of OP (SRC/dgetv0.f:245-251)
         g_stats.nopx += 1;
@@ -160,7 +172,7 @@ Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
     ws.st_host->abort = 0;
     write_state();
     dev::dots(ws, nn, 0, a.d_v, a.d_ld, wd, a.d_resid, -1);
-    dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+    fin(1, dev::kFinNorm, 0, 0, -1);
     read_state();
     double rnorm0 = ws.st_host->rnorm;
     rnorm = rnorm0;
@@ -169,17 +181,17 @@ Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
     // iterative classical Gram-Schmidt against V(:,1:j-1) (SRC/dgetv0.f:326-397)
     for (int iter = 0;;) {
         dev::dots(ws, nn, j - 1, a.d_v, a.d_ld, wd, a.d_resid, -1);
-        dev::finalize(ws, j, dev::kFinCoef, 0, 0, -1);
+        fin(j, dev::kFinCoef, 0, 0, -1);
         dev::update(ws, nn, j - 1, a.d_v, a.d_ld, 0, a.d_resid, a.d_resid, bmat != 'G', -1);
         if (bmat == 'G') {
             g_stats.nbx += 1;
             dev::copy(a.stream, nn, a.d_resid, wd + nn);
             co_await rci(2, nn, 0);
             dev::dots(ws, nn, 0, a.d_v, a.d_ld, wd, a.d_resid, -1);
-            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+            fin(1, dev::kFinNorm, 0, 0, -1);
         } else {
             dev::copy(a.stream, nn, a.d_resid, wd);
-            dev::finalize(ws, j, dev::kFinNorm, 0, 0, -1);
+            fin(j, dev::kFinNorm, 0, 0, -1);
         }
         read_state();
         rnorm = ws.st_host->rnorm;
@@ -232,11 +244,12 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
                 write_state();
             }
             // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
-            dev::place(ws, nn, a.d_resid, vcol(j), free_run ? nullptr : wd + ivj,
+            double* xop = dist ? dist->x_mid() : (free_run ? vcol(j) : wd + ivj);
+            dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
                        bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
             g_stats.nopx += 1;
-            co_await op(1, ivj, irj, ipj, free_run ? vcol(j) : wd + ivj, wd + irj);
+            co_await op(1, ivj, irj, ipj, xop, wd + irj);
             // STEP 4: B*OP*v_j (skipped in mode 2: WORKD(IVJ) holds A*v_j)
             const double* u;
             if (mode == 2) {
@@ -250,17 +263,17 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
             }
             // wnorm and the CGS coefficients h = V_j' B r (SRC/dsaitr.f:538-594)
             dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
-            dev::finalize(ws, j + 1, dev::kFinCgs, j, rstart, -1);
+            fin(j + 1, dev::kFinCgs, j, rstart, -1);
             // r_j = OP*v_j - V_j h; for bmat='I' the same pass also produces the
             // DGKS coefficients V_j' r_j and r_j' r_j (SRC/dsaitr.f:582-639)
             dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1);
             if (bI) {
-                dev::finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+                fin(j + 1, dev::kFinPostCgs, j, rstart, -1);
                 // refinement sweeps, each gated on the device-side decision
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1);
-                dev::finalize(ws, j + 1, dev::kFinDgks1, j, rstart, 1);
+                fin(j + 1, dev::kFinDgks1, j, rstart, 1);
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 2, a.d_resid, a.d_resid, true, 2);
-                dev::finalize(ws, j + 1, dev::kFinDgks2, j, rstart, 2);
+                fin(j + 1, dev::kFinDgks2, j, rstart, 2);
                 dev::zero_if(ws, nn, a.d_resid);
             } else {
                 // generalized problem: every B*r is a reverse-communication request,
@@ -269,7 +282,7 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
                 dev::copy(a.stream, nn, a.d_resid, wd + irj);
                 co_await rci(2, irj, ipj);
                 dev::dots(ws, nn, j, a.d_v, a.d_ld, wd + ipj, a.d_resid, -1);
-                dev::finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+                fin(j + 1, dev::kFinPostCgs, j, rstart, -1);
                 read_state();
                 for (int sweep = 1; sweep <= 2 && ws.st_host->dgks == sweep; ++sweep) {
                     dev::update(ws, nn, j, a.d_v, a.d_ld, sweep, a.d_resid, a.d_resid, false, sweep);
@@ -277,7 +290,7 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
                     dev::copy(a.stream, nn, a.d_resid, wd + irj);
                     co_await rci(2, irj, ipj);
                     dev::dots(ws, nn, j, a.d_v, a.d_ld, wd + ipj, a.d_resid, -1);
-                    dev::finalize(ws, j + 1, sweep == 1 ? dev::kFinDgks1 : dev::kFinDgks2, j, rstart, sweep);
+                    fin(j + 1, sweep == 1 ? dev::kFinDgks1 : dev::kFinDgks2, j, rstart, sweep);
                     read_state();
                 }
                 dev::zero_if(ws, nn, a.d_resid);
@@ -458,9 +471,9 @@ Task SymSolver::run() {
             dev::copy(a.stream, n, a.d_resid, a.d_workd + n);
             co_await rci(2, n, 0);
             dev::dots(ws, n, 0, a.d_v, a.d_ld, a.d_workd, a.d_resid, -1);
-            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+            fin(1, dev::kFinNorm, 0, 0, -1);
         } else {
-            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
+            fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
         read_state();
         rnorm = ws.st_host->rnorm;

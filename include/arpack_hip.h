@@ -119,6 +119,35 @@ void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_i
                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
                                   a_int lworkl, a_int* info);
 
+/* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
+ * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
+ * rows) and PARPACK/SRC/MPI/pdsaitr.f.  One process per GPU; the communicator
+ * is RCCL (NCCL_UNIQUE_ID_BYTES = 128-byte id created by rank 0 and broadcast
+ * by the launcher). */
+int arpack_hip_comm_unique_id(char* id128);
+int arpack_hip_comm_init(int nranks, int rank, const char* id128, int device);
+void arpack_hip_comm_destroy(void);
+int arpack_hip_comm_rank(void);
+int arpack_hip_comm_size(void);
+int arpack_hip_comm_allreduce(double* dev, int count); /* in-place SUM (test hook) */
+
+typedef struct arpack_hip_dist arpack_hip_dist;
+/* Distributed operator from this rank's CSR rows [row0, row0 + A.n) with GLOBAL
+ * column indices: computes the halo plan with the other ranks (collective) and
+ * remaps A's columns to the local extended-x layout.  Returns 0; -3/-4 if the
+ * row blocks are not contiguous or a halo reaches beyond the neighbours. */
+int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_global, int64_t row0);
+void arpack_hip_dist_destroy(arpack_hip_dist* D);
+int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
+                         int64_t* send_lo, int64_t* send_hi);
+/* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
+ * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
+void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
+                                   char const* bmat, a_int n, char const* which, a_int nev,
+                                   double* tol, double* resid, a_int ncv, double* v, a_int ldv,
+                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
+                                   a_int lworkl, a_int* info);
+
 /* Per-kernel-class device timing with hipEvents on the launch stream.
  * Classes: 0 SpMV, 1 CGS dots, 2 update(+fused DGKS dots), 3 V*Q, 4 place,
  * 5 finalize, 6 other.  read() synchronises and resets; returns #classes. */

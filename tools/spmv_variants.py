@@ -12,7 +12,8 @@ by = 12.0 * A.nnz + 8.0 * (A.n + 1) + 16.0 * A.n
 out = {}
 for name, k, tile in [("vector", 0, 4096), ("stream2048", 1, 2048), ("stream4096", 1, 4096),
                       ("stream2048_nt", 2, 2048), ("stream4096_nt", 2, 4096),
-                      ("window", 3, 4096), ("window_nt", 4, 4096)]:
+                      ("window", 3, 4096), ("window_nt", 4, 4096), ("wvec", 5, 4096),
+                      ("wvec_nt", 6, 4096), ("wvec8", 7, 4096)]:
     A.set_kernel(k, tile)
     ms = min(A.time_spmv(10) for _ in range(3))
     out[name] = dict(ms=ms, gbs=by / (ms * 1e-3) / 1e9)
