@@ -217,6 +217,8 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     (void)hipFree(A->val);
     if (A->rblk) (void)hipFree(A->rblk);
     if (A->win) (void)hipFree(A->win);
+    if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
+    A->A.w_colw = nullptr;
     delete A;
 }
 
@@ -365,6 +367,8 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     (void)hipDeviceSynchronize();
     A->ncols = ncols;
     if (A->win) (void)hipFree(A->win);
+    if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
+    A->A.w_colw = nullptr;
     A->win = nullptr;
     A->A.w_nsb = 0;
     A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;

@@ -115,6 +115,7 @@ struct Csr {
     const int64_t* w_sb_c0 = nullptr;     // first column of each superblock window
     const int32_t* w_sb_span = nullptr;   // window length
     int64_t w_nsb = 0;
+    const uint16_t* w_colw = nullptr;     // col - c0(superblock), 16 bit (owned separately)
 };
 enum CsrKernel : int {
     kCsrVector = 0,

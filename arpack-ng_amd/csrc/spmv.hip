@@ -214,12 +214,16 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_window(
 // nonzeros — so there is no product buffer and no barrier after the window
 // load (LDS = the window only: two workgroups per CU).  Rows of the next pass
 // are loaded before the current pass is reduced (two passes in flight).
-template <int L, int U, bool NT>
+// CW: read the 16-bit window-relative column indices (colw = col - c0 of the
+// superblock, built by the analysis) instead of int32 col: 10 instead of 12
+// bytes per nonzero.
+template <int L, int U, bool NT, bool CW>
 __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
     const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
     const int64_t* __restrict__ sb_c0, const int32_t* __restrict__ sb_span,
     const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-    const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ y) {
+    const uint16_t* __restrict__ colw, const double* __restrict__ val,
+    const double* __restrict__ x, double* __restrict__ y) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* xw = lds;
     constexpr int RPP = kWinThreads / L;  // rows per pass
@@ -256,13 +260,14 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
             const int64_t k = B.b + sub + u * L;
             const bool in = k < B.e;
             B.v[u] = in ? ld<double, NT>(val + k) : 0.0;
-            B.c[u] = in ? ld<int32_t, NT>(col + k) : (int)c0;
+            if constexpr (CW) B.c[u] = in ? (int)ld<uint16_t, NT>(colw + k) : 0;
+            else B.c[u] = in ? ld<int32_t, NT>(col + k) - (int)c0 : 0;
         }
     };
     auto finish = [&](Buf& B) {
         double s = 0.0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) s += B.v[u] * xw[B.c[u] - c0];
+        for (int u = 0; u < U; ++u) s += B.v[u] * xw[B.c[u]];
         for (int64_t k = B.b + sub + U * L; k < B.e; k += L) s += val[k] * xw[col[k] - c0];
 #pragma unroll
         for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
@@ -288,6 +293,14 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
             }
         }
     }
+}
+
+__global__ void k_colw(const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
+                       const int64_t* __restrict__ sb_c0, const int64_t* __restrict__ rp,
+                       const int32_t* __restrict__ col, uint16_t* __restrict__ colw) {
+    const int64_t c0 = sb_c0[blockIdx.x];
+    const int64_t k0 = rp[tiles[sb_tile0[blockIdx.x]]], k1 = rp[tiles[sb_tile0[blockIdx.x + 1]]];
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) colw[k] = (uint16_t)(col[k] - c0);
 }
 
 // per-row [min col, max col] (rows may be unsorted); empty rows -> [INT_MAX, -1]
@@ -376,6 +389,14 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     A.w_sb_c0 = (const int64_t*)(d + b_tiles + b_t0);
     A.w_sb_span = (const int32_t*)(d + b_tiles + b_t0 + b_c0);
     A.w_nsb = nsb;
+    // 16-bit window-relative column indices (one per nonzero)
+    uint16_t* cw = nullptr;
+    if (A.nnz > 0 && hipMalloc(&cw, sizeof(uint16_t) * A.nnz) == hipSuccess) {
+        hipLaunchKernelGGL(k_colw, dim3((unsigned)nsb), dim3(256), 0, nullptr, A.w_sb_tile0, A.w_tiles,
+                           A.w_sb_c0, A.rowptr, A.col, cw);
+        (void)hipDeviceSynchronize();
+        A.w_colw = cw;
+    }
     *owned = d;
     (void)ncols;
     return 0;
@@ -411,27 +432,31 @@ int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
 }
 
 double csr_bytes(const Csr& A) {
-    return 12.0 * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
+    // bytes the selected kernel must move: val + column index (+ rowptr, x, y)
+    const bool cw = A.w_colw != nullptr && (A.kernel == kCsrWVec || A.kernel == kCsrWVec8);
+    return (cw ? 10.0 : 12.0) * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
+}
+
+template <int L, int U, bool NT, bool CW>
+static void launch_wvec1(hipStream_t s, const Csr& A, const double* x, double* y) {
+    const size_t lds = sizeof(double) * kWinX;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, NT, CW>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_csr_wvec<L, U, NT, CW>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+                       A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.w_colw,
+                       A.val, x, y);
 }
 
 template <int L, int U>
 static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y, bool nt) {
-    const size_t lds = sizeof(double) * kWinX;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
-    }
-    const dim3 g((unsigned)A.w_nsb), b(kWinThreads);
-    if (nt)
-        hipLaunchKernelGGL((k_csr_wvec<L, U, true>), g, b, lds, s, A.w_sb_tile0, A.w_tiles, A.w_sb_c0,
-                           A.w_sb_span, A.rowptr, A.col, A.val, x, y);
-    else
-        hipLaunchKernelGGL((k_csr_wvec<L, U, false>), g, b, lds, s, A.w_sb_tile0, A.w_tiles, A.w_sb_c0,
-                           A.w_sb_span, A.rowptr, A.col, A.val, x, y);
+    const bool cw = A.w_colw != nullptr && A.kernel != kCsrWVecNT;
+    if (cw) launch_wvec1<L, U, false, true>(s, A, x, y);
+    else if (nt) launch_wvec1<L, U, true, false>(s, A, x, y);
+    else launch_wvec1<L, U, false, false>(s, A, x, y);
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {

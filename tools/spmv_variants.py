@@ -14,6 +14,8 @@ for name, k, tile in [("vector", 0, 4096), ("stream2048", 1, 2048), ("stream4096
                       ("stream2048_nt", 2, 2048), ("stream4096_nt", 2, 4096),
                       ("window", 3, 4096), ("window_nt", 4, 4096), ("wvec", 5, 4096),
                       ("wvec_nt", 6, 4096), ("wvec8", 7, 4096)]:
+    if name.startswith("wvec"):
+        pass
     A.set_kernel(k, tile)
     ms = min(A.time_spmv(10) for _ in range(3))
     out[name] = dict(ms=ms, gbs=by / (ms * 1e-3) / 1e9)
