@@ -18,7 +18,7 @@
 namespace ahip::dev {
 
 constexpr int kBlock = 256;
-constexpr int kMaxRedBlocks = 1024;
+constexpr int kMaxRedBlocks = 2048;
 
 // Scalar state of the current step j (device memory).
 struct LzState {

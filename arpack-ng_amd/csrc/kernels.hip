@@ -184,6 +184,21 @@ __global__ __launch_bounds__(kBlock) void k_update_generic(int64_t n, int j,
 }
 
 // --------------------------------------------------------------- finalize ---
+// Fixed-order sum of one slot's nblk per-block partials -> sums[slot].
+__global__ __launch_bounds__(256) void k_reduce_slots(const double* __restrict__ part, int nblk,
+                                                      double* __restrict__ sums,
+                                                      const LzState* __restrict__ st, int gate) {
+    if (gate_closed(st, gate)) return;
+    __shared__ double red[4];
+    const double* p = part + (int64_t)blockIdx.x * nblk;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += 256) s += p[b];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
                                                    int from_sums, int m, int phase, int j,
                                                    int rstart, int gate, double* __restrict__ sums,
@@ -561,8 +576,14 @@ void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, 
 
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums) {
     ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * m);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, (int)from_sums, m,
-                       (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
+    if (!from_sums) {
+        // stage 2a: one workgroup per slot sums that slot's nblk partials (coalesced)
+        hipLaunchKernelGGL(k_reduce_slots, dim3(m), dim3(256), 0, ws.stream, ws.part, ws.nblk, ws.sums,
+                           ws.st, gate);
+    }
+    // stage 2b: the phase logic on the m sums (one small workgroup)
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, 1, m, (int)ph, j,
+                       rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
 }
 
 void zero_if(const Workspace& ws, int64_t n, double* r) {
