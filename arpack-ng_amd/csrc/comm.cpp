@@ -22,7 +22,7 @@ int comm_rank(const Comm* c) { return c ? c->rank : 0; }
 int comm_size(const Comm* c) { return c ? c->nranks : 1; }
 
 void comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream) {
-    if (!c || c->nranks == 1) return;
+    if (!c || !c->nccl) return;
     (void)ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, c->nccl, stream);
 }
 
@@ -43,7 +43,7 @@ int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
     c->rank = rank;
     c->nranks = nranks;
     c->device = device;
-    if (nranks > 1) {
+    {   // a 1-rank communicator is real too, so the distributed path runs on one GPU
         ncclUniqueId uid;
         std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
         if (ncclCommInitRank(&c->nccl, nranks, uid, rank) != ncclSuccess) {

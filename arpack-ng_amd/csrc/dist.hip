@@ -1,6 +1,7 @@
 // Distributed operator setup (halo plan) and the distributed SpMV.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/arpack_hip.h"
@@ -23,6 +24,32 @@ struct arpack_hip_dist {
 
 extern "C" {
 
+// Halo plan of rank r from every rank's [row0, nloc, min col, max col] (global
+// indices).  out = {halo_lo, halo_hi, send_lo, send_hi}: rank r receives
+// halo_lo rows from r-1 and halo_hi rows from r+1 and sends its first send_lo
+// rows to r-1 and its last send_hi rows to r+1 (the slab exchange of
+// PARPACK/EXAMPLES/MPI/pdsdrv1.f:429-480, generalised to any banded CSR).
+int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out) {
+    auto R0 = [&](int q) { return (int64_t)tab[4 * q]; };
+    auto NL = [&](int q) { return (int64_t)tab[4 * q + 1]; };
+    auto HLO = [&](int q) { return std::max<int64_t>(0, R0(q) - (int64_t)tab[4 * q + 2]); };
+    auto HHI = [&](int q) {
+        return std::max<int64_t>(0, (int64_t)tab[4 * q + 3] - (R0(q) + NL(q) - 1));
+    };
+    if (P < 1 || r < 0 || r >= P) return -1;
+    for (int q = 0; q < P; ++q) {  // contiguous blocks, halos only from the neighbours
+        if (q > 0 && R0(q) != R0(q - 1) + NL(q - 1)) return -3;
+        if (q > 0 && HLO(q) > NL(q - 1)) return -4;
+        if (q < P - 1 && HHI(q) > NL(q + 1)) return -4;
+        if ((q == 0 && HLO(q) > 0) || (q == P - 1 && HHI(q) > 0)) return -4;
+    }
+    out[0] = HLO(r);
+    out[1] = HHI(r);
+    out[2] = r > 0 ? HHI(r - 1) : 0;
+    out[3] = r < P - 1 ? HLO(r + 1) : 0;
+    return 0;
+}
+
 int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_global,
                            int64_t row0) {
     using namespace ahip;
@@ -44,27 +71,18 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     comm_allreduce_sum(c, d, (int)tab.size(), nullptr);
     (void)hipMemcpy(tab.data(), d, sizeof(double) * tab.size(), hipMemcpyDeviceToHost);
     (void)hipFree(d);
-    auto R0 = [&](int q) { return (int64_t)tab[4 * q]; };
-    auto NL = [&](int q) { return (int64_t)tab[4 * q + 1]; };
-    auto HLO = [&](int q) { return std::max<int64_t>(0, R0(q) - (int64_t)tab[4 * q + 2]); };
-    auto HHI = [&](int q) {
-        return std::max<int64_t>(0, (int64_t)tab[4 * q + 3] - (R0(q) + NL(q) - 1));
-    };
-    for (int q = 0; q < P; ++q) {  // contiguous blocks, halos only from the neighbours
-        if (q > 0 && R0(q) != R0(q - 1) + NL(q - 1)) return -3;
-        if (q > 0 && HLO(q) > NL(q - 1)) return -4;
-        if (q < P - 1 && HHI(q) > NL(q + 1)) return -4;
-        if ((q == 0 && HLO(q) > 0) || (q == P - 1 && HHI(q) > 0)) return -4;
-    }
+    int64_t plan[4];
+    const int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
+    if (rc != 0) return rc;
     auto* D = new arpack_hip_dist;
     DistOp& o = D->D;
     o.n_global = n_global;
     o.row0 = row0;
     o.nloc = nloc;
-    o.halo_lo = HLO(r);
-    o.halo_hi = HHI(r);
-    o.send_lo = r > 0 ? HHI(r - 1) : 0;
-    o.send_hi = r < P - 1 ? HLO(r + 1) : 0;
+    o.halo_lo = plan[0];
+    o.halo_hi = plan[1];
+    o.send_lo = plan[2];
+    o.send_hi = plan[3];
     o.comm = c;
     const int64_t next = o.halo_lo + nloc + o.halo_hi;
     if (hipMalloc(&o.x_ext, sizeof(double) * (next > 0 ? next : 1))) {

@@ -124,7 +124,7 @@ RciAwait SymSolver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* 
 // Finalize of a reduction; with a multi-GPU distribution the local sums are
 // allreduced across ranks (one RCCL collective) before the phase logic runs.
 void SymSolver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
-    if (dist && comm_size(dist->comm) > 1) {
+    if (dist && dist->comm) {
         dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate);
         comm_allreduce_sum(dist->comm, ws.sums, m, a.stream);
         if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true);

@@ -46,6 +46,23 @@ def load_pkg():
     return m
 
 
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch of `kernel_substr` from the committed rocprofv3 PMC
+    summary (profiles/r*_pmc.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this same command, gfx950-corrected)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        ks = json.load(fh)["kernels"]
+    hits = [v for k, v in ks.items() if kernel_substr in k]
+    if not hits:
+        return None, None
+    v = max(hits, key=lambda e: e["launches"])
+    return v["traffic_bytes"], os.path.basename(files[-1])
+
+
 def cpu_baseline(args):
     """The reference on the host cores (rank 0, N=1 only), bounded sample."""
     threads = min(16, len(os.sched_getaffinity(0)))
@@ -176,6 +193,7 @@ def main():
     step_ms = ms + orth_ms
     step_gbs = (by + orth_bytes) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
 
+    traffic, traffic_src = pmc_traffic("k_csr_wvec")
     out = {
         "metric": "Arnoldi iters/sec + time-to-converge (nev=10), n=10M CSR; %HBM roofline",
         "value": iters_per_s,
@@ -197,8 +215,9 @@ def main():
         "lanczos_steps_per_s": nopx / elapsed,
         "time_to_converge": ttc,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                     "kernel": "csr_spmv (k_csr_vector)",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "kernel": "csr_spmv (k_csr_wvec: LDS x-window, 16-bit window-relative cols)",
                      "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},

@@ -140,6 +140,10 @@ int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_glo
 void arpack_hip_dist_destroy(arpack_hip_dist* D);
 int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
                          int64_t* send_lo, int64_t* send_hi);
+/* Halo plan (host only, CPU-testable): tab = [row0, nloc, min col, max col] per
+ * rank (4*P doubles, global indices); out = {halo_lo, halo_hi, send_lo, send_hi}
+ * of rank r.  Returns 0, -3 (blocks not contiguous) or -4 (halo too wide). */
+int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out);
 /* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
  * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
 void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
