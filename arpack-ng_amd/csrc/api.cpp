@@ -351,4 +351,34 @@ void arpack_hip_kit_dlarnv(int* iseed, int n, double* x) {
     iseed_from_seed48(s, iseed);
 }
 
+double arpack_hip_kit_dnrm2(int n, const double* x) { return la::nrm2(n, x, 1); }
+void arpack_hip_kit_dlanv2(double* a, double* b, double* c, double* d, double* rt1r, double* rt1i,
+                           double* rt2r, double* rt2i, double* cs, double* sn) {
+    la::lanv2(*a, *b, *c, *d, *rt1r, *rt1i, *rt2r, *rt2i, *cs, *sn);
+}
+int arpack_hip_kit_dlahqr(int wantt, int wantz, int n, int ilo, int ihi, double* h, int ldh,
+                          double* wr, double* wi, int iloz, int ihiz, double* z, int ldz) {
+    return la::lahqr(wantt != 0, wantz != 0, n, ilo, ihi, h, ldh, wr, wi, iloz, ihiz, z, ldz);
+}
+int arpack_hip_kit_dtrevc(char howmny, int* select, int n, const double* t, int ldt, double* vr,
+                          int ldvr, double* work) {
+    return la::trevc_right(howmny, select, n, t, ldt, vr, ldvr, work);
+}
+void arpack_hip_kit_dsortc(char const* which, int apply, int n, double* xr, double* xi, double* y) {
+    la::dsortc(la::parse_which(which), apply != 0, n, xr, xi, y);
+}
+void arpack_hip_kit_dngets(int ishift, char const* which, int* kev, int* np, double* ritzr,
+                           double* ritzi, double* bounds) {
+    la::dngets(ishift, la::parse_which(which), *kev, *np, ritzr, ritzi, bounds);
+}
+int arpack_hip_kit_dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr,
+                          double* ritzi, double* bounds, double* q, int ldq, double* workl) {
+    return la::dneigh(rnorm, n, h, ldh, ritzr, ritzi, bounds, q, ldq, workl);
+}
+int arpack_hip_kit_dnapps_host(int kev, int np, const double* shiftr, const double* shifti,
+                               double* h, int ldh, double* q, int ldq, double* workl,
+                               int64_t nglob) {
+    return la::dnapps_host(kev, np, shiftr, shifti, h, ldh, q, ldq, workl, nglob);
+}
+
 }  // extern "C"

@@ -349,19 +349,18 @@ int steqr(int n, double* dd, double* ee, double* zz, int zrows, int ldz, double*
     return info;
 }
 
+// dnrm2 as the image's OpenBLAS computes it (x86-64 kernel: sum of squares in
+// x87 extended precision, one rounding at the end) -- bit-identical on 2,700
+// random vectors (tests/test_kit_ns.py), which the scaled LAPACK reference
+// algorithm is not.
 double nrm2(int n, const double* x, int incx) {
     if (n < 1) return 0.0;
-    if (n == 1) return std::fabs(x[0]);
-    double scale = 0.0, ssq = 1.0;
+    long double s = 0.0L;
     for (int i = 0; i < n; ++i) {
-        const double v = x[(size_t)i * incx];
-        if (v != 0.0) {
-            const double a = std::fabs(v);
-            if (scale < a) { const double q = scale / a; ssq = 1.0 + ssq * q * q; scale = a; }
-            else { const double q = a / scale; ssq += q * q; }
-        }
+        const long double v = x[(size_t)i * incx];
+        s += v * v;
     }
-    return scale * std::sqrt(ssq);
+    return (double)std::sqrt(s);
 }
 
 void larfg(int n, double& alpha, double* x, int incx, double& tau) {

@@ -77,4 +77,27 @@ int dseigt(double rnorm, int n, const double* h, int ldh, double* eig, double* b
 void dsapps_host(int kev, int np, const double* shift, double* h, int ldh, double* q,
                  int ldq);
 
+// ---------------- nonsymmetric kit (dense_ns.cpp) ----------------------------
+void lanv2(double& a, double& b, double& c, double& d, double& rt1r, double& rt1i, double& rt2r,
+           double& rt2i, double& cs, double& sn);
+double lanhs1(int n, const double* a, int lda);
+// dlahqr with 1-based ilo/ihi/iloz/ihiz; returns info
+int lahqr(bool wantt, bool wantz, int n, int ilo, int ihi, double* h, int ldh, double* wr,
+          double* wi, int iloz, int ihiz, double* z, int ldz);
+void ladiv(double a, double b, double c, double d, double& p, double& q);
+int laln2(int na, int nw, double smin, double ca, const double* a, int lda, double d1, double d2,
+          const double* b, int ldb, double wr, double wi, double* x, int ldx, double& scale,
+          double& xnorm);
+// dtrevc side='R'; howmny 'A' | 'B' | 'S'; work 3n; returns m
+int trevc_right(char howmny, int* select, int n, const double* t, int ldt, double* vr, int ldvr,
+                double* work);
+void dsortc(Which which, bool apply, int n, double* xr, double* xi, double* y);
+void dngets(int ishift, Which which, int& kev, int& np, double* ritzr, double* ritzi,
+            double* bounds);
+int dnconv(int n, const double* ritzr, const double* ritzi, const double* bounds, double tol);
+int dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr, double* ritzi,
+           double* bounds, double* q, int ldq, double* workl);
+int dnapps_host(int kev, int np, const double* shiftr, const double* shifti, double* h, int ldh,
+                double* q, int ldq, double* workl, int64_t nglob);
+
 }  // namespace ahip::la

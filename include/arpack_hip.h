@@ -177,6 +177,24 @@ void arpack_hip_kit_dsortr(char const* which, int apply, int n, double* x1, doub
 void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h, int ldh,
                                 double* q, int ldq);
 void arpack_hip_kit_dlarnv(int* iseed, int n, double* x);
+/* nonsymmetric kit (restated LAPACK dlahqr/dtrevc/dlanv2/dnrm2 and ARPACK
+ * dsortc/dngets/dneigh/dnapps; compared against SRC/dsortc.f, dngets.f,
+ * dneigh.f, dnapps.f and the image's LAPACK in tests/test_kit_ns.py) */
+double arpack_hip_kit_dnrm2(int n, const double* x);
+void arpack_hip_kit_dlanv2(double* a, double* b, double* c, double* d, double* rt1r,
+                           double* rt1i, double* rt2r, double* rt2i, double* cs, double* sn);
+int arpack_hip_kit_dlahqr(int wantt, int wantz, int n, int ilo, int ihi, double* h, int ldh,
+                          double* wr, double* wi, int iloz, int ihiz, double* z, int ldz);
+int arpack_hip_kit_dtrevc(char howmny, int* select, int n, const double* t, int ldt, double* vr,
+                          int ldvr, double* work);
+void arpack_hip_kit_dsortc(char const* which, int apply, int n, double* xr, double* xi, double* y);
+void arpack_hip_kit_dngets(int ishift, char const* which, int* kev, int* np, double* ritzr,
+                           double* ritzi, double* bounds);
+int arpack_hip_kit_dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr,
+                          double* ritzi, double* bounds, double* q, int ldq, double* workl);
+int arpack_hip_kit_dnapps_host(int kev, int np, const double* shiftr, const double* shifti,
+                               double* h, int ldh, double* q, int ldq, double* workl,
+                               int64_t nglob);
 
 #ifdef __cplusplus
 }
