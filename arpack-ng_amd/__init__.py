@@ -98,6 +98,10 @@ def _declare(L):
     L.arpack_hip_dsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p, _I,
                                                C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI,
                                                _PD, _PD, _I, _PI]
+    L.dnaupd_c.argtypes = L.dsaupd_c.argtypes
+    L.dnaupd_.argtypes = L.dsaupd_.argtypes
+    L.arpack_hip_dnaupd_csr_cycles.argtypes = L.arpack_hip_dsaupd_csr_cycles.argtypes
+    L.arpack_hip_gen_convdiff2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
     L.arpack_hip_profile.argtypes = [_I]
     L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
     L.arpack_hip_synchronize.restype = C.c_int
@@ -249,6 +253,14 @@ class CSR:
         h = C.c_void_p()
         if lib().arpack_hip_gen_laplace2d(C.byref(h), m, scale) != 0:
             raise RuntimeError("laplace2d generation failed")
+        return cls(h.value)
+
+    @classmethod
+    def convdiff2d(cls, m, rho):
+        """-Lap u + rho du/dx (EXAMPLES/NONSYM/dndrv1.f:397-475), m x m grid."""
+        h = C.c_void_p()
+        if lib().arpack_hip_gen_convdiff2d(C.byref(h), m, rho) != 0:
+            raise RuntimeError("convdiff2d generation failed")
         return cls(h.value)
 
     @classmethod
@@ -406,6 +418,53 @@ class SymRci:
     def ritz(self):
         o = int(self.ipntr[5]) - 1
         return self.workl[o:o + self.ncv].copy()
+
+
+class NsRci(SymRci):
+    """dnaupd state (SRC/dnaupd.f:400-693): like SymRci, with ipntr(14) and
+    lworkl = 3*ncv^2 + 6*ncv; Ritz values are complex (ritzr/ritzi)."""
+
+    def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300,
+                 ishift=1, v0=None, device=False, icb=False):
+        super().__init__(n, nev, ncv, which, tol, bmat, mode, mxiter, ishift, v0, device, icb)
+        self.ipntr = np.zeros(14, np.int32)
+        self.lworkl = 3 * ncv * ncv + 6 * ncv
+        self.workl = np.zeros(self.lworkl)
+
+    def aupd(self):
+        if self.icb:
+            lib().dnaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(),
+                           self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
+                           self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        else:
+            tol = C.c_double(self.tol)
+            lib().dnaupd_(_ip(self.ido), self.bmat.encode(), C.byref(C.c_int(self.n)),
+                          self.which.encode(), C.byref(C.c_int(self.nev)), C.byref(tol),
+                          _ptr(self.resid), C.byref(C.c_int(self.ncv)), _ptr(self.v),
+                          C.byref(C.c_int(self.ldv)), _ip(self.iparam), _ip(self.ipntr),
+                          _ptr(self.workd), self.workl.ctypes.data, C.byref(C.c_int(self.lworkl)),
+                          _ip(self.info), 1, 2)
+            self.tol = tol.value
+        return int(self.ido[0])
+
+    def aupd_cycles(self, A: CSR, max_cycles: int):
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_dnaupd_csr_cycles(A.h, int(max_cycles), _ip(self.ido), self.bmat.encode(),
+                                           self.n, self.which.encode(), self.nev, C.byref(tol),
+                                           _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                           _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
+    def aupd_csr(self, A: CSR):
+        return self.aupd_cycles(A, -1)
+
+    @property
+    def ritz(self):
+        o, oi = int(self.ipntr[5]) - 1, int(self.ipntr[6]) - 1
+        return self.workl[o:o + self.ncv] + 1j * self.workl[oi:oi + self.ncv]
 
 
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,

@@ -3,7 +3,7 @@
 //
 // Argument checking, the workl layout and the iparam/info post-processing
 // follow SRC/dsaupd.f:473-690 exactly; everything between ido = 0 and ido = 99
-// is the SymSolver coroutine (sym.cpp).
+// is the Solver coroutine (sym.cpp).
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -24,7 +24,7 @@ uint64_t g_dseed = 0;
 static bool g_dseed_init = false;
 static hipStream_t g_stream = nullptr;
 static std::mutex g_mu;
-static std::unordered_map<const void*, std::unique_ptr<SymSolver>> g_sym;
+static std::unordered_map<const void*, std::unique_ptr<Solver>> g_sym;
 
 hipStream_t default_stream() { return g_stream; }
 
@@ -77,19 +77,42 @@ static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lw
     return ierr;
 }
 
+// dnaupd argument checks (SRC/dnaupd.f:436-466); returns ierr
+static int ns_check(char bmat, int n, la::Which which, int nev, int ncv, int lworkl, int mode,
+                    int ishift, int mxiter) {
+    int ierr = 0;
+    if (n <= 0) ierr = -1;
+    else if (nev <= 0) ierr = -2;
+    else if (ncv <= nev + 1 || ncv > n) ierr = -3;
+    else if (mxiter <= 0) ierr = -4;
+    else if (which != la::Which::LM && which != la::Which::SM && which != la::Which::LR &&
+             which != la::Which::SR && which != la::Which::LI && which != la::Which::SI)
+        ierr = -5;
+    else if (bmat != 'I' && bmat != 'G') ierr = -6;
+    else if (lworkl < 3 * ncv * ncv + 6 * ncv) ierr = -7;
+    else if (mode < 1 || mode > 4) ierr = -10;
+    else if (mode == 1 && bmat == 'G') ierr = -11;
+    else if (ishift < 0 || ishift > 1) ierr = -12;
+    return ierr;
+}
+
+// The *aupd driver shared by dsaupd (ns = false, SRC/dsaupd.f:408-690) and
+// dnaupd (ns = true, SRC/dnaupd.f:400-693): argument checks and workl layout
+// at ido = 0, then resume the solve coroutine until it needs the caller.
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                      double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
                      double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr,
-                     int max_cycles = -1, const DistOp* dist = nullptr) {
+                     int max_cycles = -1, const DistOp* dist = nullptr, bool ns = false) {
     if (dist) csr = dist->A;
     std::lock_guard<std::mutex> lk(g_mu);
-    SymSolver* S = nullptr;
+    Solver* S = nullptr;
     if (*ido == 0) {
         ensure_seed();
         g_stats = Stats{};  // dstats (SRC/dstats.f)
         const la::Which w = la::parse_which(which);
         const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
-        int ierr = sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
+        int ierr = ns ? ns_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter)
+                      : sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
         if (csr && (mode != 1 || bmat[0] != 'I' || csr->n != n)) ierr = (ierr ? ierr : -11);
         if (dist && dist->nloc != n) ierr = (ierr ? ierr : -1);
         if (ierr != 0) {
@@ -98,7 +121,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             return;
         }
         if (*tol <= 0.0) *tol = la::kEps;
-        auto up = std::make_unique<SymSolver>();
+        auto up = std::make_unique<Solver>();
         S = up.get();
         S->bmat = bmat[0];
         S->which = w;
@@ -111,19 +134,37 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->np = ncv - nev;
         S->lworkl = lworkl;
         S->info = *info;
-        // workl layout (SRC/dsaupd.f:566-595)
-        std::memset(workl, 0, sizeof(double) * (size_t)(ncv * ncv + 8 * ncv));
-        S->ih = 0;
-        S->iritz = S->ih + 2 * ncv;
-        S->ibounds = S->iritz + ncv;
-        S->iq = S->ibounds + ncv;
-        S->iw = S->iq + ncv * ncv;
-        const int next = S->iw + 3 * ncv;
-        ipntr[3] = next + 1;
-        ipntr[4] = S->ih + 1;
-        ipntr[5] = S->iritz + 1;
-        ipntr[6] = S->ibounds + 1;
-        ipntr[10] = S->iw + 1;
+        if (!ns) {  // workl layout (SRC/dsaupd.f:566-595)
+            std::memset(workl, 0, sizeof(double) * (size_t)(ncv * ncv + 8 * ncv));
+            S->ih = 0;
+            S->iritz = S->ih + 2 * ncv;
+            S->ibounds = S->iritz + ncv;
+            S->iq = S->ibounds + ncv;
+            S->iw = S->iq + ncv * ncv;
+            const int next = S->iw + 3 * ncv;
+            ipntr[3] = next + 1;
+            ipntr[4] = S->ih + 1;
+            ipntr[5] = S->iritz + 1;
+            ipntr[6] = S->ibounds + 1;
+            ipntr[10] = S->iw + 1;
+        } else {  // workl layout (SRC/dnaupd.f:494-520)
+            std::memset(workl, 0, sizeof(double) * (size_t)(3 * ncv * ncv + 6 * ncv));
+            S->arnoldi = true;
+            S->ih = 0;
+            S->iritz = S->ih + ncv * ncv;
+            S->iritzi = S->iritz + ncv;
+            S->ibounds = S->iritzi + ncv;
+            S->iq = S->ibounds + ncv;
+            S->iw = S->iq + ncv * ncv;
+            const int next = S->iw + ncv * ncv + 3 * ncv;
+            ipntr[3] = next + 1;
+            ipntr[4] = S->ih + 1;
+            ipntr[5] = S->iritz + 1;
+            ipntr[6] = S->iritzi + 1;
+            ipntr[7] = S->ibounds + 1;
+            ipntr[13] = S->iw + 1;
+        }
+        S->n_global = dist ? dist->n_global : n;
         if (S->a.attach(n, ncv, resid, v, ldv, workd) != 0 ||
             dev::ws_create(S->ws, n, ncv, S->a.stream) != hipSuccess) {
             *info = -9999;
@@ -142,7 +183,8 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->iparam = iparam;
         S->ipntr = ipntr;
         S->workl = workl;
-        S->root.emplace(S->run());
+        if (ns) S->ws.hld = ncv;
+        S->root.emplace(ns ? S->run_ns() : S->run());
         start_root(*S->root, S->ctx);
         g_sym[v] = std::move(up);
     } else {
@@ -161,7 +203,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const RciReq& r = S->ctx.req;
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
             S->a.h2d_workd(r.y, n);
-            if (r.ido == 1 && S->mode == 2) S->a.h2d_workd(r.x, n);
+            if (r.ido == 1 && S->mode == 2 && !S->arnoldi) S->a.h2d_workd(r.x, n);
         }
     }
     if (csr) S->pause_budget = max_cycles;
@@ -176,7 +218,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
             continue;
         }
-        if (r.ido == SymSolver::kPauseIdo) {  // cycle budget spent: park (no sync)
+        if (r.ido == Solver::kPauseIdo) {  // cycle budget spent: park (no sync)
             *ido = r.ido;
             return;
         }
@@ -218,6 +260,28 @@ void dsaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, dou
               double* workl, int lworkl, int* info) {
     sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
              lworkl, info, nullptr);
+}
+
+void dnaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, double tol,
+              double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr, double* workd,
+              double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr, -1, nullptr, true);
+}
+
+void dnaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, double* tol,
+             double* resid, int* ncv, double* v, int* ldv, int* iparam, int* ipntr, double* workd,
+             double* workl, int* lworkl, int* info, size_t, size_t) {
+    sym_aupd(ido, bmat, *n, which, *nev, tol, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl,
+             *lworkl, info, nullptr, -1, nullptr, true);
+}
+
+void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* ido,
+                                  char const* bmat, int n, char const* which, int nev, double* tol,
+                                  double* resid, int ncv, double* v, int ldv, int* iparam,
+                                  int* ipntr, double* workd, double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, ahip_csr_view(A), max_cycles, nullptr, true);
 }
 
 void dsaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, double* tol,

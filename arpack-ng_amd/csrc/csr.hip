@@ -138,6 +138,26 @@ __global__ void k_lap_fill(int64_t m, int dim, double scale, double disorder, ui
     }
 }
 
+// 2-D convection-diffusion -Lap u + rho du/dx on the unit square (the dndrv1 /
+// dnsimp operator, EXAMPLES/NONSYM/dndrv1.f:397-475): x-neighbours dl/du,
+// y-neighbours offy, diagonal dd (coefficients computed on the host).
+__global__ void k_cd_fill(int64_t m, double dd, double dl, double du, double offy,
+                          const int64_t* __restrict__ rp, int32_t* __restrict__ col,
+                          double* __restrict__ val) {
+    const int64_t n = m * m;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t x = i % m, y = i / m;
+        int64_t k = rp[i];
+        auto put = [&](int64_t j, double v) { col[k] = (int32_t)j; val[k] = v; ++k; };
+        if (y > 0) put(i - m, offy);
+        if (x > 0) put(i - 1, dl);
+        put(i, dd);
+        if (x < m - 1) put(i + 1, du);
+        if (y < m - 1) put(i + m, offy);
+    }
+}
+
 }  // namespace ahip::gen
 
 namespace {
@@ -296,6 +316,27 @@ static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, doubl
 }
 
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 2, scale); }
+
+int arpack_hip_gen_convdiff2d(arpack_hip_csr** out, int64_t m, double rho) {
+    const int64_t n = m * m;
+    // coefficients exactly as EXAMPLES/NONSYM/dndrv1.f:425,458-462 compute them
+    const double h = 1.0 / (double)(m + 1), h2 = h * h;
+    const double dd = 4.0 / h2, dl = -1.0 / h2 - 0.5 * rho / h, du = -1.0 / h2 + 0.5 * rho / h;
+    const double offy = -1.0 / (1.0 / (double)((m + 1) * (m + 1)));
+    int64_t *cnt = nullptr, *rp = nullptr;
+    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, 2, cnt);
+    const int64_t nnz = scan_counts(n, cnt, rp);
+    (void)hipFree(cnt);
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
+    hipLaunchKernelGGL(ahip::gen::k_cd_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dd, dl, du, offy,
+                       rp, col, val);
+    (void)hipDeviceSynchronize();
+    *out = finish(n, n, nnz, rp, col, val);
+    return 0;
+}
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 3, scale); }
 int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed) {
     return gen_lap(A, m, dim, 1.0, disorder, seed);

@@ -55,6 +55,10 @@ struct Workspace {
     double* coef = nullptr;   // 3 * stride : CGS, DGKS-1, DGKS-2 coefficient vectors
     double* rec = nullptr;    // 2 * (ncv+1): alpha_j, beta_j per step
     double* q = nullptr;      // ncv * ncv  (V*Q matrix for dsapps / eupd)
+    // Arnoldi (dnaitr): column j of H, h(1:j, j) = V_j' w + DGKS corrections,
+    // recorded by the finalize kernel; hld = ncv (0 for the Lanczos path).
+    double* hcol = nullptr;   // hld * ncv
+    int hld = 0;
     LzState* st = nullptr;
     LzState* st_host = nullptr;  // pinned mirror
     double* host_scratch = nullptr;  // pinned, >= 4*stride doubles

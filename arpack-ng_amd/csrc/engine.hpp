@@ -59,8 +59,11 @@ struct Arrays {
 bool is_device_pointer(const void* p);
 hipStream_t default_stream();  // set through arpack_hip_set_stream()
 
-// Symmetric implicitly restarted Lanczos (dsaupd family).
-class SymSolver {
+// One implicitly restarted Krylov solve: symmetric Lanczos (dsaupd family,
+// sym.cpp) or nonsymmetric Arnoldi (dnaupd family, ns.cpp).  The n-length
+// step machinery (getv0, the Lanczos/Arnoldi step with CGS + DGKS, V*Q) is
+// shared; only the ncv-sized host work differs.
+class Solver {
 public:
     // configuration fixed at ido == 0 (SRC/dsaupd.f:473-596)
     char bmat = 'I';
@@ -94,17 +97,22 @@ public:
     int64_t row0 = 0;
     const dev::Csr* csr = nullptr;
 
-    // workl offsets (0-based) of h, ritz, bounds, q, w
-    int ih = 0, iritz = 0, ibounds = 0, iq = 0, iw = 0;
+    // nonsymmetric Arnoldi (dnaupd): full upper-Hessenberg H (ld ncv)
+    bool arnoldi = false;
+    int64_t n_global = 0;  // problem dimension (enters dnaitr/dnapps' smlnum)
+    // workl offsets (0-based) of h, ritz (ritzr), ritzi, bounds, q, w
+    int ih = 0, iritz = 0, iritzi = 0, ibounds = 0, iq = 0, iw = 0;
     double rnorm = 0.0;  // host copy of dsaup2's rnorm
 
-    ~SymSolver();
-    Task run();
+    ~Solver();
+    Task run();     // dsaup2
+    Task run_ns();  // dnaup2
 
 private:
     Task getv0(bool initv, int j, int itry, int& ierr);
     Task saitr(int k, int npk, int& iinfo);
     void sapps(int kev, int npk);
+    void vq_device(int kev, int kplusp, double sigmak, double betak);
     RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
     RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp);
     void read_state();

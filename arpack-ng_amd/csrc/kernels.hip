@@ -204,7 +204,8 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    int rstart, int gate, double* __restrict__ sums,
                                                    double* __restrict__ coef, int cstride,
                                                    double* __restrict__ rec,
-                                                   LzState* __restrict__ st) {
+                                                   LzState* __restrict__ st,
+                                                   double* __restrict__ hcol, int hld) {
     if (gate_closed(st, gate)) return;
     __shared__ double s_sum[256];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -224,6 +225,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     const int jm = m - 1;  // index of the w'u / r'r slot
     if (phase == kFinCgs) {
         if (t < jm) coef[t] = s_sum[t];
+        if (hld && t < jm) hcol[(int64_t)(j - 1) * hld + t] = s_sum[t];  // h(1:j,j) (dnaitr.f:566)
         if (t == 0) {
             st->zero = 0;
             st->dgks = 0;
@@ -288,7 +290,10 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
     __syncthreads();
     const int take = s_take;
-    if (take && t < jm) coef[take * cstride + t] = s_sum[t];
+    if (take && t < jm) {
+        coef[take * cstride + t] = s_sum[t];
+        if (hld) hcol[(int64_t)(j - 1) * hld + t] += s_sum[t];  // daxpy into h(1:j,j) (dnaitr.f:681)
+    }
 }
 
 __global__ void k_zero_if(int64_t n, double* r, const LzState* st) {
@@ -466,6 +471,7 @@ hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipMalloc(&ws.coef, sizeof(double) * 3 * (size_t)ws.stride))) return e;
     if ((e = hipMalloc(&ws.rec, sizeof(double) * 2 * (size_t)(ncv + 1)))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * (size_t)ncv * ncv))) return e;
+    if ((e = hipMalloc(&ws.hcol, sizeof(double) * (size_t)ncv * ncv))) return e;
     if ((e = hipMalloc(&ws.st, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
@@ -482,6 +488,7 @@ void ws_destroy(Workspace& ws) {
     if (ws.coef) (void)hipFree(ws.coef);
     if (ws.rec) (void)hipFree(ws.rec);
     if (ws.q) (void)hipFree(ws.q);
+    if (ws.hcol) (void)hipFree(ws.hcol);
     if (ws.st) (void)hipFree(ws.st);
     if (ws.st_host) (void)hipHostFree(ws.st_host);
     if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
@@ -583,7 +590,7 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
     }
     // stage 2b: the phase logic on the m sums (one small workgroup)
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, 1, m, (int)ph, j,
-                       rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st);
+                       rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
 }
 
 void zero_if(const Workspace& ws, int64_t n, double* r) {

@@ -4,10 +4,10 @@
 // n-length data stays in HBM.
 //
 // Reference map:
-//   SymSolver::run    SRC/dsaupd.f:408-690 + SRC/dsaup2.f:179-851
-//   SymSolver::saitr  SRC/dsaitr.f:204-853   (Lanczos steps, CGS + DGKS)
-//   SymSolver::getv0  SRC/dgetv0.f:119-421   (start / restart vector)
-//   SymSolver::sapps  SRC/dsapps.f:131-518   (shifts on T host-side, V*Q on device)
+//   Solver::run    SRC/dsaupd.f:408-690 + SRC/dsaup2.f:179-851
+//   Solver::saitr  SRC/dsaitr.f:204-853   (Lanczos steps, CGS + DGKS)
+//   Solver::getv0  SRC/dgetv0.f:119-421   (start / restart vector)
+//   Solver::sapps  SRC/dsapps.f:131-518   (shifts on T host-side, V*Q on device)
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -101,21 +101,21 @@ void Arrays::download_all() {
 
 void Arrays::sync() { ck(hipStreamSynchronize(stream)); }
 
-// ------------------------------------------------------------- SymSolver ---
+// ------------------------------------------------------------- Solver ---
 
-SymSolver::~SymSolver() {
+Solver::~Solver() {
     root.reset();
     dev::ws_destroy(ws);
     a.release();
 }
 
-RciAwait SymSolver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
+RciAwait Solver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = nullptr;
     op_y = nullptr;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
-RciAwait SymSolver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp) {
+RciAwait Solver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp) {
     op_x = xp;
     op_y = yp;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
@@ -123,7 +123,7 @@ RciAwait SymSolver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* 
 
 // Finalize of a reduction; with a multi-GPU distribution the local sums are
 // allreduced across ranks (one RCCL collective) before the phase logic runs.
-void SymSolver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
+void Solver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
     if (dist && dist->comm) {
         dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate);
         comm_allreduce_sum(dist->comm, ws.sums, m, a.stream);
@@ -133,19 +133,19 @@ void SymSolver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
     }
 }
 
-void SymSolver::read_state() {
+void Solver::read_state() {
     ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
 
-void SymSolver::write_state() {
+void Solver::write_state() {
     ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
 }
 
 // dgetv0: generate (or take) a start vector, force it into range(OP), and for
 // j > 1 B-orthogonalise it against V(:,1:j-1) with <= 5 refinement sweeps.
 // On exit st.rnorm and this->rnorm hold its B-norm.
-Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
+Task Solver::getv0(bool initv, int j, int itry, int& ierr) {
     const int64_t nn = n;
     double* wd = a.d_workd;
     ierr = 0;
@@ -212,7 +212,7 @@ Task SymSolver::getv0(bool initv, int j, int itry, int& ierr) {
 }
 
 // dsaitr: extend a k-step Lanczos factorization to k+npk steps.
-Task SymSolver::saitr(int k, int npk, int& iinfo) {
+Task Solver::saitr(int k, int npk, int& iinfo) {
     const int64_t nn = n;
     double* wd = a.d_workd;
     const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
@@ -252,7 +252,7 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
             co_await op(1, ivj, irj, ipj, xop, wd + irj);
             // STEP 4: B*OP*v_j (skipped in mode 2: WORKD(IVJ) holds A*v_j)
             const double* u;
-            if (mode == 2) {
+            if (mode == 2 && !arnoldi) {  // dsaitr only; dnaitr has no mode-2 shortcut
                 u = wd + ivj;
             } else if (!bI) {
                 g_stats.nbx += 1;
@@ -319,40 +319,67 @@ Task SymSolver::saitr(int k, int npk, int& iinfo) {
     g_stats.nitref += ws.st_host->nitref;
     ws.st_host->nrorth = ws.st_host->nitref = 0;
     write_state();
-    // assemble h(k+1:k+np, 1:2) from the per-step device records
+    // assemble the new columns of H from the per-step device records
     double* rec = ws.host_scratch;
     ck(hipMemcpyAsync(rec, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost, a.stream));
-    a.sync();
     double* h = workl + ih;
-    for (int jj = k + 1; jj <= k + npk; ++jj) {
-        h[(jj - 1) + ncv] = rec[2 * (jj - 1)];
-        h[jj - 1] = rec[2 * (jj - 1) + 1];
+    if (!arnoldi) {  // T(ncv,2): h(:,1) subdiagonal, h(:,2) diagonal
+        a.sync();
+        for (int jj = k + 1; jj <= k + npk; ++jj) {
+            h[(jj - 1) + ncv] = rec[2 * (jj - 1)];
+            h[jj - 1] = rec[2 * (jj - 1) + 1];
+        }
+    } else {  // H(ncv,ncv): h(1:j,j) from the device, h(j,j-1) = beta_j (SRC/dnaitr.f:566-590)
+        std::vector<double> hc((size_t)ncv * npk);
+        ck(hipMemcpyAsync(hc.data(), ws.hcol + (size_t)k * ncv, sizeof(double) * hc.size(),
+                          hipMemcpyDeviceToHost, a.stream));
+        a.sync();
+        for (int jj = k + 1; jj <= k + npk; ++jj) {
+            double* col = h + (size_t)(jj - 1) * ncv;
+            std::memcpy(col, hc.data() + (size_t)(jj - 1 - k) * ncv, sizeof(double) * jj);
+            if (jj > 1) col[jj - 2] = rec[2 * (jj - 1) + 1];
+        }
+        // negligible subdiagonals of the new Hessenberg block (SRC/dnaitr.f:820-838)
+        const double ulp = 2.0 * la::kEps;
+        const double smlnum = la::kSafmin * ((double)n_global / ulp);
+        const int kp = k + npk;
+        for (int i = std::max(1, k); i <= kp - 1; ++i) {
+            double tst1 = std::fabs(h[(i - 1) + (size_t)(i - 1) * ncv]) + std::fabs(h[i + (size_t)i * ncv]);
+            if (tst1 == 0.0) tst1 = la::lanhs1(kp, h, ncv);
+            double& sub = h[i + (size_t)(i - 1) * ncv];
+            if (std::fabs(sub) <= std::max(ulp * tst1, smlnum)) sub = 0.0;
+        }
     }
     (void)rstart_j;
     co_return;
 }
 
 // dsapps: bulge chase on the host, V*Q and the residual update on the device.
-void SymSolver::sapps(int kev, int npk) {
+void Solver::sapps(int kev, int npk) {
     const int kplusp = kev + npk;
     double* h = workl + ih;
     double* q = workl + iq;
     la::dsapps_host(kev, npk, workl + iritz, h, ncv, q, ncv);
     if (npk == 0) return;
-    // compact Q(:, 1:kev+1) into the device workspace (ld = kplusp)
-    double* qs = ws.host_scratch;  // reuse pinned scratch if large enough
-    std::vector<double> qbuf((size_t)kplusp * (kev + 1));
-    for (int c = 0; c <= kev && c < kplusp; ++c)
-        for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
-    (void)qs;
-    ck(hipMemcpyAsync(ws.q, qbuf.data(), sizeof(double) * qbuf.size(), hipMemcpyHostToDevice, a.stream));
     const double sigmak = q[(kplusp - 1) + (size_t)(kev - 1) * ncv];
     const double betak = h[kev];  // h(kev+1,1)
+    vq_device(kev, kplusp, sigmak, betak);
+}
+
+// V(:,1:kev) = V(:,1:kplusp) * Q(:,1:kev); v_{kev+1} = V*Q(:,kev+1) if betak > 0;
+// resid = sigmak*resid + betak*v_{kev+1} (SRC/dsapps.f:450-493, dnapps.f:583-640).
+// Q is the host matrix at workl(iq) (ld ncv).
+void Solver::vq_device(int kev, int kplusp, double sigmak, double betak) {
+    const double* q = workl + iq;
+    std::vector<double> qbuf((size_t)kplusp * (kev + 1));  // compact, ld = kplusp
+    for (int c = 0; c <= kev && c < kplusp; ++c)
+        for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
+    ck(hipMemcpyAsync(ws.q, qbuf.data(), sizeof(double) * qbuf.size(), hipMemcpyHostToDevice, a.stream));
     dev::vq_update(ws, n, a.d_v, a.d_ld, kplusp, kev, sigmak, betak, a.d_resid);
     a.sync();  // qbuf lifetime
 }
 
-Task SymSolver::run() {
+Task Solver::run() {
     // ---- dsaup2 initialisation (SRC/dsaup2.f:258-317)
     const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
     int nev = nev0;

@@ -44,9 +44,19 @@ void dseupd_c(a_int rvec, char const* howmny, a_int const* select, double* d, do
               a_int* iparam, a_int* ipntr, double* workd, double* workl, a_int lworkl,
               a_int* info);
 
+/* dnaupd_c (ICB/arpack.h:18; SRC/icbadn.F90): same arguments as dsaupd_c, but
+ * ipntr has 14 entries and lworkl >= 3*ncv^2 + 6*ncv. */
+void dnaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
+              double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
+              a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info);
+
 /* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
  *      argument by reference + hidden trailing CHARACTER lengths ---------------- */
 void dsaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
+             double* tol, double* resid, a_int* ncv, double* v, a_int* ldv, a_int* iparam,
+             a_int* ipntr, double* workd, double* workl, a_int* lworkl, a_int* info,
+             size_t bmat_len, size_t which_len);
+void dnaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
              double* tol, double* resid, a_int* ncv, double* v, a_int* ldv, a_int* iparam,
              a_int* ipntr, double* workd, double* workl, a_int* lworkl, a_int* info,
              size_t bmat_len, size_t which_len);
@@ -119,6 +129,14 @@ void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_i
                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
                                   a_int lworkl, a_int* info);
 
+/* dnaupd with OP = A served on the GPU (mode 1), cycle-parked like
+ * arpack_hip_dsaupd_csr_cycles (SRC/dnaupd.f semantics, ipntr[14]). */
+void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_int* ido,
+                                  char const* bmat, a_int n, char const* which, a_int nev,
+                                  double* tol, double* resid, a_int ncv, double* v, a_int ldv,
+                                  a_int* iparam, a_int* ipntr, double* workd, double* workl,
+                                  a_int lworkl, a_int* info);
+
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
  * rows) and PARPACK/SRC/MPI/pdsaitr.f.  One process per GPU; the communicator
@@ -161,6 +179,9 @@ int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int ncl
 /* Synthetic operators generated directly in HBM (bench/test workloads, see
  * DESIGN.md §5).  Each allocates device CSR arrays owned by *A. */
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale);
+/* 2-D convection-diffusion -Lap u + rho du/dx, m x m interior grid
+ * (EXAMPLES/NONSYM/dndrv1.f:397-475; complex spectrum once rho*h/2 > 1). */
+int arpack_hip_gen_convdiff2d(arpack_hip_csr** A, int64_t m, double rho);
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale);
 int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed);
 int arpack_hip_gen_banded_sym(arpack_hip_csr** A, int64_t n, int64_t row_begin,

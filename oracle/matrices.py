@@ -110,6 +110,32 @@ def laplace(m, dim=2, scale=1.0, disorder=0.0, seed=0):
     return rowptr, c.astype(np.int32), v
 
 
+def convdiff2d(m, rho):
+    """-Lap u + rho du/dx on an m x m grid, coefficients as
+    EXAMPLES/NONSYM/dndrv1.f:425,458-462 compute them (device twin:
+    arpack_hip_gen_convdiff2d)."""
+    n = m * m
+    h = 1.0 / (m + 1)
+    h2 = h * h
+    dd = 4.0 / h2
+    dl = -1.0 / h2 - 0.5 * rho / h
+    du = -1.0 / h2 + 0.5 * rho / h
+    offy = -1.0 / (1.0 / float((m + 1) * (m + 1)))
+    i = np.arange(n, dtype=np.int64)
+    x = i % m
+    y = i // m
+    entries = [(y > 0, i - m, offy), (x > 0, i - 1, dl), (np.ones(n, bool), i, dd),
+               (x < m - 1, i + 1, du), (y < m - 1, i + m, offy)]
+    r = np.concatenate([i[ok] for ok, _, _ in entries])
+    c = np.concatenate([j[ok] for ok, j, _ in entries])
+    v = np.concatenate([np.full(int(ok.sum()), val) for ok, _, val in entries])
+    order = np.lexsort((c, r))
+    r, c, v = r[order], c[order], v[order]
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(r, minlength=n), out=rowptr[1:])
+    return rowptr, c.astype(np.int32), v
+
+
 def laplace2d(m, scale=1.0):
     return laplace(m, 2, scale)
 

@@ -50,6 +50,47 @@ def run_sym(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=F
     return r
 
 
+def run_ns(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, **extra):
+    """dnaupd/dneupd fixture (SRC/dnaupd.f, SRC/dneupd.f); workl layout
+    SRC/dnaupd.f:494-520 (ritzr at ih+ncv^2, ritzi, bounds)."""
+    rowptr, col, val = mat
+    n = len(rowptr) - 1
+    if v0 is None:
+        v0, _ = M.dlarnv_uniform(n)
+    r = ref.dnaupd_solve(csr_op(rowptr, col, val), n, nev, ncv, which, tol, v0=v0,
+                         mxiter=mxiter, return_state=True)
+    assert r["info"] >= 0, r
+    o = ncv * ncv
+    out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
+               mxiter=mxiter, v0=v0, info=r["info"], iparam=r["iparam"], dr=r["dr"], di=r["di"],
+               nopx=r["stats"]["nopx"], nrorth=r["stats"]["nrorth"],
+               nitref=r["stats"]["nitref"], ritzr=r["workl"][o:o + ncv],
+               ritzi=r["workl"][o + ncv:o + 2 * ncv], bounds=r["workl"][o + 2 * ncv:o + 3 * ncv],
+               eupd_info=r["eupd_info"])
+    if keep_z:
+        out["z"] = r["z"]
+    out.update(extra)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(name, "info", r["info"], "iparam", r["iparam"][[2, 4, 8, 10]], "dr", r["dr"][:3],
+          "di", r["di"][:3])
+    return r
+
+
+def nonsym_fixtures():
+    cd10 = M.convdiff2d(10, 100.0)
+    run_ns("n1_dnsimp", cd10, ["convdiff2d", 10, 100.0], 4, 20, "LM", 0.0, keep_z=True)
+    run_ns("n2_dnsimp_tol", cd10, ["convdiff2d", 10, 100.0], 4, 20, "LM", 1e-10, keep_z=True)
+    cd30 = M.convdiff2d(30, 100.0)
+    run_ns("n3_convdiff_lm", cd30, ["convdiff2d", 30, 100.0], 10, 40, "LM", 1e-10, keep_z=True)
+    run_ns("n4_convdiff_lr", cd10, ["convdiff2d", 10, 100.0], 4, 20, "LR", 1e-9, mxiter=3000)
+    run_ns("n5_convdiff_li", cd10, ["convdiff2d", 10, 100.0], 4, 20, "LI", 1e-9, mxiter=3000)
+    run_ns("n6_convdiff_sr", cd10, ["convdiff2d", 10, 100.0], 4, 20, "SR", 1e-9, mxiter=3000)
+    cd100 = M.convdiff2d(100, 10.0)
+    run_ns("n7_convdiff_real", cd100, ["convdiff2d", 100, 10.0], 10, 40, "LM", 1e-8,
+           mxiter=3000)
+    run_ns("n8_convdiff_capped", cd30, ["convdiff2d", 30, 100.0], 10, 40, "LM", 1e-14, mxiter=4)
+
+
 def g7_dlarnv():
     lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
                                  "scipy.libs", "libscipy_openblas*.so"))[0]
@@ -76,6 +117,9 @@ def g1_fresh_process_check():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["ns"]:
+        nonsym_fixtures()
+        sys.exit(0)
     g7_dlarnv()
     r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
                  keep_z=True)
@@ -98,3 +142,4 @@ if __name__ == "__main__":
             "SM", 1e-8, keep_z=False, mxiter=3000)
     run_sym("g8_banded_capped", M.banded_sym(20000, 1234, 512, 25),
             ["banded_sym", 20000, 1234, 512, 25], 10, 30, "LA", 1e-14, mxiter=5)
+    nonsym_fixtures()
