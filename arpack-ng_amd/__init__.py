@@ -99,6 +99,9 @@ def _declare(L):
                                                C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI,
                                                _PD, _PD, _I, _PI]
     L.dnaupd_c.argtypes = L.dsaupd_c.argtypes
+    L.dneupd_c.argtypes = [_I, C.c_char_p, _PI, _PD, _PD, _PD, _I, C.c_double, C.c_double, _PD,
+                           C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I, _PI, _PI,
+                           _PD, _PD, _I, _PI]
     L.dnaupd_.argtypes = L.dsaupd_.argtypes
     L.arpack_hip_dnaupd_csr_cycles.argtypes = L.arpack_hip_dsaupd_csr_cycles.argtypes
     L.arpack_hip_gen_convdiff2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
@@ -459,7 +462,31 @@ class NsRci(SymRci):
         return int(self.ido[0])
 
     def aupd_csr(self, A: CSR):
-        return self.aupd_cycles(A, -1)
+        r = self.aupd_cycles(A, -1)
+        if self.tol <= 0.0:
+            self.tol = float(np.finfo(np.float64).eps / 2)
+        return r
+
+    def eupd(self, rvec=True, howmny="A", sigmar=0.0, sigmai=0.0, z=None):
+        """dneupd_c: returns (dr, di, Z, nconv); Z has nev+1 columns (SRC/dneupd.f)."""
+        nconv = int(self.iparam[4])
+        dr, di = np.zeros(self.nev + 1), np.zeros(self.nev + 1)
+        if z is None:
+            m = (self.nev + 1) * self.n
+            z = DeviceBuffer(m) if self.device else np.zeros(m)
+        select = np.zeros(self.ncv, np.int32)
+        workev = np.zeros(3 * self.ncv)
+        info = np.zeros(1, np.int32)
+        lib().dneupd_c(1 if rvec else 0, howmny.encode(), _ip(select), dr.ctypes.data,
+                       di.ctypes.data, _ptr(z), self.n, sigmar, sigmai, workev.ctypes.data,
+                       self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol,
+                       _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam),
+                       _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data, self.lworkl,
+                       _ip(info))
+        if info[0] < 0:
+            raise ArpackError("dneupd", int(info[0]))
+        self.eupd_info = int(info[0])
+        return dr[:nconv], di[:nconv], z, nconv
 
     @property
     def ritz(self):

@@ -445,4 +445,10 @@ int arpack_hip_kit_dnapps_host(int kev, int np, const double* shiftr, const doub
     return la::dnapps_host(kev, np, shiftr, shifti, h, ldh, q, ldq, workl, nglob);
 }
 
+int arpack_hip_kit_dtrsen(const int* select, int n, double* t, int ldt, double* q, int ldq,
+                          double* wr, double* wi, int* m) {
+    std::vector<double> work(n > 0 ? n : 1);
+    return la::trsen(select, n, t, ldt, q, ldq, wr, wi, *m, work.data());
+}
+
 }  // extern "C"

@@ -99,5 +99,14 @@ int dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr, double*
            double* bounds, double* q, int ldq, double* workl);
 int dnapps_host(int kev, int np, const double* shiftr, const double* shifti, double* h, int ldh,
                 double* q, int ldq, double* workl, int64_t nglob);
+// Schur reordering for dneupd: dlasy2, dlaexc, dtrexc, dtrsen(job='N', compq='V')
+int lasy2(int isgn, int n1, int n2, const double* tl, int ldtl, const double* tr, int ldtr,
+          const double* b, int ldb, double& scale, double* x, int ldx, double& xnorm);
+int laexc(bool wantq, int n, double* t, int ldt, double* q, int ldq, int j1, int n1, int n2,
+          double* work);
+int trexc(bool wantq, int n, double* t, int ldt, double* q, int ldq, int& ifst, int& ilst,
+          double* work);
+int trsen(const int* select, int n, double* t, int ldt, double* q, int ldq, double* wr,
+          double* wi, int& m, double* work);
 
 }  // namespace ahip::la

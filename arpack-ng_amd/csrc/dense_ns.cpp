@@ -1157,4 +1157,501 @@ int dnapps_host(int kev, int np, const double* shiftr, const double* shifti, dou
 #undef Q
 }
 
+// ------------------------------------------------- Schur reordering (dneupd) --
+namespace {
+// dlarfx for an order-3 reflector (LAPACK's unrolled special case, scalar).
+void larfx3(char side, int m, int n, const double* v, double tau, double* c, int ldc) {
+    if (tau == 0.0) return;
+    const double v1 = v[0], v2 = v[1], v3 = v[2];
+    const double t1 = tau * v1, t2 = tau * v2, t3 = tau * v3;
+    if (side == 'L') {  // order m = 3
+        for (int j = 0; j < n; ++j) {
+            double* cj = c + (size_t)j * ldc;
+            const double sum = v1 * cj[0] + v2 * cj[1] + v3 * cj[2];
+            cj[0] -= sum * t1;
+            cj[1] -= sum * t2;
+            cj[2] -= sum * t3;
+        }
+    } else {  // order n = 3
+        for (int j = 0; j < m; ++j) {
+            double* c1 = c + j;
+            const double sum = v1 * c1[0] + v2 * c1[ldc] + v3 * c1[2 * (size_t)ldc];
+            c1[0] -= sum * t1;
+            c1[ldc] -= sum * t2;
+            c1[2 * (size_t)ldc] -= sum * t3;
+        }
+    }
+}
+// drot over n pairs (x, y) with strides (OpenBLAS arithmetic, see rot_x/rot_y)
+void drot(int n, double* x, int incx, double* y, int incy, double c, double s) {
+    for (int i = 0; i < n; ++i) {
+        const double a = x[(size_t)i * incx], b = y[(size_t)i * incy];
+        x[(size_t)i * incx] = rot_x(c, s, a, b);
+        y[(size_t)i * incy] = rot_y(c, s, a, b);
+    }
+}
+}  // namespace
+
+// dlasy2 (ltranl = ltranr = false): TL*X + isgn*X*TR = scale*B, n1,n2 in {1,2}.
+int lasy2(int isgn, int n1, int n2, const double* tl, int ldtl, const double* tr, int ldtr,
+          const double* b, int ldb, double& scale, double* x, int ldx, double& xnorm) {
+#define TL(i, j) tl[((i)-1) + (size_t)((j)-1) * ldtl]
+#define TR(i, j) tr[((i)-1) + (size_t)((j)-1) * ldtr]
+#define B(i, j) b[((i)-1) + (size_t)((j)-1) * ldb]
+#define X(i, j) x[((i)-1) + (size_t)((j)-1) * ldx]
+    static const int locu12[4] = {3, 4, 1, 2}, locl21[4] = {2, 1, 4, 3}, locu22[4] = {4, 3, 2, 1};
+    static const bool xswpiv[4] = {false, false, true, true}, bswpiv[4] = {false, true, false, true};
+    int info = 0;
+    if (n1 == 0 || n2 == 0) return 0;
+    const double eps = kUlp;
+    const double smlnum = kSafmin / eps;
+    const double sgn = isgn;
+    const int k = n1 + n1 + n2 - 2;
+    double tmp[4], btmp[4], x2[2];
+    if (k == 1) {
+        double tau1 = TL(1, 1) + sgn * TR(1, 1);
+        double bet = std::fabs(tau1);
+        if (bet <= smlnum) {
+            tau1 = smlnum;
+            bet = smlnum;
+            info = 1;
+        }
+        scale = 1.0;
+        const double gam = std::fabs(B(1, 1));
+        if (smlnum * gam > bet) scale = 1.0 / gam;
+        X(1, 1) = (B(1, 1) * scale) / tau1;
+        xnorm = std::fabs(X(1, 1));
+        return info;
+    }
+    if (k == 2 || k == 3) {
+        double smin;
+        if (k == 2) {  // 1 x 2
+            smin = std::max(eps * std::max({std::fabs(TL(1, 1)), std::fabs(TR(1, 1)), std::fabs(TR(1, 2)),
+                                            std::fabs(TR(2, 1)), std::fabs(TR(2, 2))}),
+                            smlnum);
+            tmp[0] = TL(1, 1) + sgn * TR(1, 1);
+            tmp[3] = TL(1, 1) + sgn * TR(2, 2);
+            tmp[1] = sgn * TR(1, 2);
+            tmp[2] = sgn * TR(2, 1);
+            btmp[0] = B(1, 1);
+            btmp[1] = B(1, 2);
+        } else {  // 2 x 1
+            smin = std::max(eps * std::max({std::fabs(TR(1, 1)), std::fabs(TL(1, 1)), std::fabs(TL(1, 2)),
+                                            std::fabs(TL(2, 1)), std::fabs(TL(2, 2))}),
+                            smlnum);
+            tmp[0] = TL(1, 1) + sgn * TR(1, 1);
+            tmp[3] = TL(2, 2) + sgn * TR(1, 1);
+            tmp[1] = TL(2, 1);
+            tmp[2] = TL(1, 2);
+            btmp[0] = B(1, 1);
+            btmp[1] = B(2, 1);
+        }
+        int ipiv = 0;
+        for (int q = 1; q < 4; ++q)
+            if (std::fabs(tmp[q]) > std::fabs(tmp[ipiv])) ipiv = q;
+        double u11 = tmp[ipiv];
+        if (std::fabs(u11) <= smin) {
+            info = 1;
+            u11 = smin;
+        }
+        const double u12 = tmp[locu12[ipiv] - 1];
+        const double l21 = tmp[locl21[ipiv] - 1] / u11;
+        double u22 = tmp[locu22[ipiv] - 1] - u12 * l21;
+        const bool xswap = xswpiv[ipiv], bswap = bswpiv[ipiv];
+        if (std::fabs(u22) <= smin) {
+            info = 1;
+            u22 = smin;
+        }
+        if (bswap) {
+            const double temp = btmp[1];
+            btmp[1] = btmp[0] - l21 * temp;
+            btmp[0] = temp;
+        } else {
+            btmp[1] = btmp[1] - l21 * btmp[0];
+        }
+        scale = 1.0;
+        if ((2.0 * smlnum) * std::fabs(btmp[1]) > std::fabs(u22) ||
+            (2.0 * smlnum) * std::fabs(btmp[0]) > std::fabs(u11)) {
+            scale = 0.5 / std::max(std::fabs(btmp[0]), std::fabs(btmp[1]));
+            btmp[0] *= scale;
+            btmp[1] *= scale;
+        }
+        x2[1] = btmp[1] / u22;
+        x2[0] = btmp[0] / u11 - (u12 / u11) * x2[1];
+        if (xswap) std::swap(x2[0], x2[1]);
+        X(1, 1) = x2[0];
+        if (n1 == 1) {
+            X(1, 2) = x2[1];
+            xnorm = std::fabs(X(1, 1)) + std::fabs(X(1, 2));
+        } else {
+            X(2, 1) = x2[1];
+            xnorm = std::max(std::fabs(X(1, 1)), std::fabs(X(2, 1)));
+        }
+        return info;
+    }
+    // 2 x 2: equivalent 4 x 4 system, complete pivoting
+    double smin = std::max({std::fabs(TR(1, 1)), std::fabs(TR(1, 2)), std::fabs(TR(2, 1)), std::fabs(TR(2, 2))});
+    smin = std::max({smin, std::fabs(TL(1, 1)), std::fabs(TL(1, 2)), std::fabs(TL(2, 1)), std::fabs(TL(2, 2))});
+    smin = std::max(eps * smin, smlnum);
+    double t16[4][4] = {};  // t16[col][row] (column-major like the reference)
+#define T16(i, j) t16[(j)-1][(i)-1]
+    T16(1, 1) = TL(1, 1) + sgn * TR(1, 1);
+    T16(2, 2) = TL(2, 2) + sgn * TR(1, 1);
+    T16(3, 3) = TL(1, 1) + sgn * TR(2, 2);
+    T16(4, 4) = TL(2, 2) + sgn * TR(2, 2);
+    T16(1, 2) = TL(1, 2);
+    T16(2, 1) = TL(2, 1);
+    T16(3, 4) = TL(1, 2);
+    T16(4, 3) = TL(2, 1);
+    T16(1, 3) = sgn * TR(2, 1);
+    T16(2, 4) = sgn * TR(2, 1);
+    T16(3, 1) = sgn * TR(1, 2);
+    T16(4, 2) = sgn * TR(1, 2);
+    btmp[0] = B(1, 1);
+    btmp[1] = B(2, 1);
+    btmp[2] = B(1, 2);
+    btmp[3] = B(2, 2);
+    int jpiv[4] = {0, 0, 0, 0};
+    for (int i = 1; i <= 3; ++i) {
+        double xmax = 0.0;
+        int ipsv = i, jpsv = i;
+        for (int ip = i; ip <= 4; ++ip)
+            for (int jp = i; jp <= 4; ++jp)
+                if (std::fabs(T16(ip, jp)) >= xmax) {
+                    xmax = std::fabs(T16(ip, jp));
+                    ipsv = ip;
+                    jpsv = jp;
+                }
+        if (ipsv != i) {
+            for (int c = 1; c <= 4; ++c) std::swap(T16(ipsv, c), T16(i, c));
+            std::swap(btmp[i - 1], btmp[ipsv - 1]);
+        }
+        if (jpsv != i)
+            for (int r = 1; r <= 4; ++r) std::swap(T16(r, jpsv), T16(r, i));
+        jpiv[i - 1] = jpsv;
+        if (std::fabs(T16(i, i)) < smin) {
+            info = 1;
+            T16(i, i) = smin;
+        }
+        for (int j = i + 1; j <= 4; ++j) {
+            T16(j, i) = T16(j, i) / T16(i, i);
+            btmp[j - 1] = btmp[j - 1] - T16(j, i) * btmp[i - 1];
+            for (int kk = i + 1; kk <= 4; ++kk) T16(j, kk) = T16(j, kk) - T16(j, i) * T16(i, kk);
+        }
+    }
+    if (std::fabs(T16(4, 4)) < smin) {
+        info = 1;
+        T16(4, 4) = smin;
+    }
+    scale = 1.0;
+    if ((8.0 * smlnum) * std::fabs(btmp[0]) > std::fabs(T16(1, 1)) ||
+        (8.0 * smlnum) * std::fabs(btmp[1]) > std::fabs(T16(2, 2)) ||
+        (8.0 * smlnum) * std::fabs(btmp[2]) > std::fabs(T16(3, 3)) ||
+        (8.0 * smlnum) * std::fabs(btmp[3]) > std::fabs(T16(4, 4))) {
+        scale = (1.0 / 8.0) / std::max({std::fabs(btmp[0]), std::fabs(btmp[1]), std::fabs(btmp[2]),
+                                         std::fabs(btmp[3])});
+        for (double& bb : btmp) bb *= scale;
+    }
+    for (int i = 1; i <= 4; ++i) {
+        const int kk = 5 - i;
+        const double temp = 1.0 / T16(kk, kk);
+        tmp[kk - 1] = btmp[kk - 1] * temp;
+        for (int j = kk + 1; j <= 4; ++j) tmp[kk - 1] = tmp[kk - 1] - (temp * T16(kk, j)) * tmp[j - 1];
+    }
+    for (int i = 1; i <= 3; ++i) {
+        const int kk = 4 - i;
+        if (jpiv[kk - 1] != kk) std::swap(tmp[kk - 1], tmp[jpiv[kk - 1] - 1]);
+    }
+    X(1, 1) = tmp[0];
+    X(2, 1) = tmp[1];
+    X(1, 2) = tmp[2];
+    X(2, 2) = tmp[3];
+    xnorm = std::max(std::fabs(tmp[0]) + std::fabs(tmp[2]), std::fabs(tmp[1]) + std::fabs(tmp[3]));
+    return info;
+#undef T16
+#undef TL
+#undef TR
+#undef B
+#undef X
+}
+
+// dlaexc: swap adjacent diagonal blocks T11 (n1) and T22 (n2) at row j1 (1-based).
+int laexc(bool wantq, int n, double* t, int ldt, double* q, int ldq, int j1, int n1, int n2,
+          double* work) {
+#define T(i, j) t[((i)-1) + (size_t)((j)-1) * ldt]
+#define Q(i, j) q[((i)-1) + (size_t)((j)-1) * ldq]
+    (void)work;
+    if (n == 0 || n1 == 0 || n2 == 0) return 0;
+    if (j1 + n1 > n) return 0;
+    const int j2 = j1 + 1, j3 = j1 + 2, j4 = j1 + 3;
+    if (n1 == 1 && n2 == 1) {
+        const double t11 = T(j1, j1), t22 = T(j2, j2);
+        double cs, sn, temp;
+        lartg(T(j1, j2), t22 - t11, cs, sn, temp);
+        if (j3 <= n) drot(n - j1 - 1, &T(j1, j3), ldt, &T(j2, j3), ldt, cs, sn);
+        drot(j1 - 1, &T(1, j1), 1, &T(1, j2), 1, cs, sn);
+        T(j1, j1) = t22;
+        T(j2, j2) = t11;
+        if (wantq) drot(n, &Q(1, j1), 1, &Q(1, j2), 1, cs, sn);
+        return 0;
+    }
+    const int nd = n1 + n2;
+    double d[16];  // D(4,4), ldd = 4
+#define D(i, j) d[((i)-1) + ((j)-1) * 4]
+    double dnorm = 0.0;
+    for (int j = 1; j <= nd; ++j)
+        for (int i = 1; i <= nd; ++i) {
+            D(i, j) = T(j1 + i - 1, j1 + j - 1);
+            const double a = std::fabs(D(i, j));
+            if (dnorm < a || std::isnan(a)) dnorm = a;
+        }
+    const double eps = kUlp;
+    const double smlnum = kSafmin / eps;
+    const double thresh = std::max(10.0 * eps * dnorm, smlnum);
+    double x[4], scale, xnorm;  // X(2,2), ldx = 2
+    lasy2(-1, n1, n2, d, 4, &D(n1 + 1, n1 + 1), 4, &D(1, n1 + 1), 4, scale, x, 2, xnorm);
+    const int k = n1 + n1 + n2 - 3;
+    if (k == 1) {  // n1 = 1, n2 = 2
+        double u[3] = {scale, x[0], x[2]};
+        double tau;
+        larfg(3, u[2], u, 1, tau);
+        u[2] = 1.0;
+        const double t11 = T(j1, j1);
+        larfx3('L', 3, 3, u, tau, d, 4);
+        larfx3('R', 3, 3, u, tau, d, 4);
+        if (std::max({std::fabs(D(3, 1)), std::fabs(D(3, 2)), std::fabs(D(3, 3) - t11)}) > thresh) return 1;
+        larfx3('L', 3, n - j1 + 1, u, tau, &T(j1, j1), ldt);
+        larfx3('R', j2, 3, u, tau, &T(1, j1), ldt);
+        T(j3, j1) = 0.0;
+        T(j3, j2) = 0.0;
+        T(j3, j3) = t11;
+        if (wantq) larfx3('R', n, 3, u, tau, &Q(1, j1), ldq);
+    } else if (k == 2) {  // n1 = 2, n2 = 1
+        double u[3] = {-x[0], -x[1], scale};
+        double tau;
+        larfg(3, u[0], u + 1, 1, tau);
+        u[0] = 1.0;
+        const double t33 = T(j3, j3);
+        larfx3('L', 3, 3, u, tau, d, 4);
+        larfx3('R', 3, 3, u, tau, d, 4);
+        if (std::max({std::fabs(D(2, 1)), std::fabs(D(3, 1)), std::fabs(D(1, 1) - t33)}) > thresh) return 1;
+        larfx3('R', j3, 3, u, tau, &T(1, j1), ldt);
+        larfx3('L', 3, n - j1, u, tau, &T(j1, j2), ldt);
+        T(j1, j1) = t33;
+        T(j2, j1) = 0.0;
+        T(j3, j1) = 0.0;
+        if (wantq) larfx3('R', n, 3, u, tau, &Q(1, j1), ldq);
+    } else {  // n1 = 2, n2 = 2
+        double u1[3] = {-x[0], -x[1], scale};
+        double tau1;
+        larfg(3, u1[0], u1 + 1, 1, tau1);
+        u1[0] = 1.0;
+        const double temp = -tau1 * (x[2] + u1[1] * x[3]);
+        double u2[3] = {-temp * u1[1] - x[3], -temp * u1[2], scale};
+        double tau2;
+        larfg(3, u2[0], u2 + 1, 1, tau2);
+        u2[0] = 1.0;
+        // order-3 reflectors on the 4 x 4 block D
+        larfx3('L', 3, 4, u1, tau1, d, 4);
+        larfx3('R', 4, 3, u1, tau1, d, 4);
+        larfx3('L', 3, 4, u2, tau2, &D(2, 1), 4);
+        larfx3('R', 4, 3, u2, tau2, &D(1, 2), 4);
+        if (std::max({std::fabs(D(3, 1)), std::fabs(D(3, 2)), std::fabs(D(4, 1)), std::fabs(D(4, 2))}) > thresh)
+            return 1;
+        larfx3('L', 3, n - j1 + 1, u1, tau1, &T(j1, j1), ldt);
+        larfx3('R', j4, 3, u1, tau1, &T(1, j1), ldt);
+        larfx3('L', 3, n - j1 + 1, u2, tau2, &T(j2, j1), ldt);
+        larfx3('R', j4, 3, u2, tau2, &T(1, j2), ldt);
+        T(j3, j1) = 0.0;
+        T(j3, j2) = 0.0;
+        T(j4, j1) = 0.0;
+        T(j4, j2) = 0.0;
+        if (wantq) {
+            larfx3('R', n, 3, u1, tau1, &Q(1, j1), ldq);
+            larfx3('R', n, 3, u2, tau2, &Q(1, j2), ldq);
+        }
+    }
+#undef D
+    double wr1, wi1, wr2, wi2, cs, sn;
+    if (n2 == 2) {  // standardise the new 2 x 2 block T11
+        lanv2(T(j1, j1), T(j1, j2), T(j2, j1), T(j2, j2), wr1, wi1, wr2, wi2, cs, sn);
+        drot(n - j1 - 1, &T(j1, j1 + 2), ldt, &T(j2, j1 + 2), ldt, cs, sn);
+        drot(j1 - 1, &T(1, j1), 1, &T(1, j2), 1, cs, sn);
+        if (wantq) drot(n, &Q(1, j1), 1, &Q(1, j2), 1, cs, sn);
+    }
+    if (n1 == 2) {  // standardise the new 2 x 2 block T22
+        const int k3 = j1 + n2, k4 = k3 + 1;
+        lanv2(T(k3, k3), T(k3, k4), T(k4, k3), T(k4, k4), wr1, wi1, wr2, wi2, cs, sn);
+        if (k3 + 2 <= n) drot(n - k3 - 1, &T(k3, k3 + 2), ldt, &T(k4, k3 + 2), ldt, cs, sn);
+        drot(k3 - 1, &T(1, k3), 1, &T(1, k4), 1, cs, sn);
+        if (wantq) drot(n, &Q(1, k3), 1, &Q(1, k4), 1, cs, sn);
+    }
+    return 0;
+#undef T
+#undef Q
+}
+
+// dtrexc: move the block at ifst to ilst (1-based, in/out).
+int trexc(bool wantq, int n, double* t, int ldt, double* q, int ldq, int& ifst, int& ilst,
+          double* work) {
+#define T(i, j) t[((i)-1) + (size_t)((j)-1) * ldt]
+    if (n <= 1) return 0;
+    if (ifst > 1 && T(ifst, ifst - 1) != 0.0) --ifst;
+    int nbf = 1;
+    if (ifst < n && T(ifst + 1, ifst) != 0.0) nbf = 2;
+    if (ilst > 1 && T(ilst, ilst - 1) != 0.0) --ilst;
+    int nbl = 1;
+    if (ilst < n && T(ilst + 1, ilst) != 0.0) nbl = 2;
+    if (ifst == ilst) return 0;
+    int here, info = 0;
+    if (ifst < ilst) {
+        if (nbf == 2 && nbl == 1) --ilst;
+        if (nbf == 1 && nbl == 2) ++ilst;
+        here = ifst;
+        do {
+            if (nbf == 1 || nbf == 2) {
+                int nbnext = 1;
+                if (here + nbf + 1 <= n && T(here + nbf + 1, here + nbf) != 0.0) nbnext = 2;
+                info = laexc(wantq, n, t, ldt, q, ldq, here, nbf, nbnext, work);
+                if (info != 0) {
+                    ilst = here;
+                    return info;
+                }
+                here += nbnext;
+                if (nbf == 2 && T(here + 1, here) == 0.0) nbf = 3;
+            } else {
+                int nbnext = 1;
+                if (here + 3 <= n && T(here + 3, here + 2) != 0.0) nbnext = 2;
+                info = laexc(wantq, n, t, ldt, q, ldq, here + 1, 1, nbnext, work);
+                if (info != 0) {
+                    ilst = here;
+                    return info;
+                }
+                if (nbnext == 1) {
+                    laexc(wantq, n, t, ldt, q, ldq, here, 1, nbnext, work);
+                    ++here;
+                } else {
+                    if (T(here + 2, here + 1) == 0.0) nbnext = 1;
+                    if (nbnext == 2) {
+                        info = laexc(wantq, n, t, ldt, q, ldq, here, 1, nbnext, work);
+                        if (info != 0) {
+                            ilst = here;
+                            return info;
+                        }
+                        here += 2;
+                    } else {
+                        laexc(wantq, n, t, ldt, q, ldq, here, 1, 1, work);
+                        laexc(wantq, n, t, ldt, q, ldq, here + 1, 1, 1, work);
+                        here += 2;
+                    }
+                }
+            }
+        } while (here < ilst);
+    } else {
+        here = ifst;
+        do {
+            if (nbf == 1 || nbf == 2) {
+                int nbnext = 1;
+                if (here >= 3 && T(here - 1, here - 2) != 0.0) nbnext = 2;
+                info = laexc(wantq, n, t, ldt, q, ldq, here - nbnext, nbnext, nbf, work);
+                if (info != 0) {
+                    ilst = here;
+                    return info;
+                }
+                here -= nbnext;
+                if (nbf == 2 && T(here + 1, here) == 0.0) nbf = 3;
+            } else {
+                int nbnext = 1;
+                if (here >= 3 && T(here - 1, here - 2) != 0.0) nbnext = 2;
+                info = laexc(wantq, n, t, ldt, q, ldq, here - nbnext, nbnext, 1, work);
+                if (info != 0) {
+                    ilst = here;
+                    return info;
+                }
+                if (nbnext == 1) {
+                    laexc(wantq, n, t, ldt, q, ldq, here, nbnext, 1, work);
+                    --here;
+                } else {
+                    if (T(here, here - 1) == 0.0) nbnext = 1;
+                    if (nbnext == 2) {
+                        info = laexc(wantq, n, t, ldt, q, ldq, here - 1, 2, 1, work);
+                        if (info != 0) {
+                            ilst = here;
+                            return info;
+                        }
+                        here -= 2;
+                    } else {
+                        laexc(wantq, n, t, ldt, q, ldq, here, 1, 1, work);
+                        laexc(wantq, n, t, ldt, q, ldq, here - 1, 1, 1, work);
+                        here -= 2;
+                    }
+                }
+            }
+        } while (here > ilst);
+    }
+    ilst = here;
+    return 0;
+#undef T
+}
+
+// dtrsen(job = 'N', compq = 'V'): move the selected eigenvalues to the leading
+// block; wr/wi recomputed from T; m = dimension of the selected subspace.
+int trsen(const int* select, int n, double* t, int ldt, double* q, int ldq, double* wr,
+          double* wi, int& m, double* work) {
+#define T(i, j) t[((i)-1) + (size_t)((j)-1) * ldt]
+    m = 0;
+    bool pair = false;
+    for (int k = 1; k <= n; ++k) {
+        if (pair) {
+            pair = false;
+        } else if (k < n) {
+            if (T(k + 1, k) == 0.0) {
+                if (select[k - 1]) ++m;
+            } else {
+                pair = true;
+                if (select[k - 1] || select[k]) m += 2;
+            }
+        } else if (select[n - 1]) {
+            ++m;
+        }
+    }
+    int info = 0;
+    if (!(m == n || m == 0)) {
+        int ks = 0;
+        pair = false;
+        for (int k = 1; k <= n; ++k) {
+            if (pair) {
+                pair = false;
+                continue;
+            }
+            bool swap = select[k - 1] != 0;
+            if (k < n && T(k + 1, k) != 0.0) {
+                pair = true;
+                swap = swap || select[k] != 0;
+            }
+            if (swap) {
+                ++ks;
+                int ierr = 0, kk = k;
+                if (k != ks) ierr = trexc(true, n, t, ldt, q, ldq, kk, ks, work);  // ks in/out
+                if (ierr == 1 || ierr == 2) {
+                    info = 1;
+                    break;
+                }
+                if (pair) ++ks;
+            }
+        }
+    }
+    for (int k = 1; k <= n; ++k) {
+        wr[k - 1] = T(k, k);
+        wi[k - 1] = 0.0;
+    }
+    for (int k = 1; k <= n - 1; ++k)
+        if (T(k + 1, k) != 0.0) {
+            wi[k - 1] = std::sqrt(std::fabs(T(k, k + 1))) * std::sqrt(std::fabs(T(k + 1, k)));
+            wi[k] = -wi[k - 1];
+        }
+    return info;
+#undef T
+}
+
 }  // namespace ahip::la

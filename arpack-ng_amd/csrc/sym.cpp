@@ -337,7 +337,7 @@ Task Solver::saitr(int k, int npk, int& iinfo) {
         for (int jj = k + 1; jj <= k + npk; ++jj) {
             double* col = h + (size_t)(jj - 1) * ncv;
             std::memcpy(col, hc.data() + (size_t)(jj - 1 - k) * ncv, sizeof(double) * jj);
-            if (jj > 1) col[jj - 2] = rec[2 * (jj - 1) + 1];
+            if (jj > 1) h[(jj - 1) + (size_t)(jj - 2) * ncv] = rec[2 * (jj - 1) + 1];  // h(jj,jj-1)
         }
         // negligible subdiagonals of the new Hessenberg block (SRC/dnaitr.f:820-838)
         const double ulp = 2.0 * la::kEps;

@@ -50,6 +50,14 @@ void dnaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int ne
               double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
               a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info);
 
+/* dneupd_c (ICB/arpack.h:19; SRC/icbadn.F90): dr/di (nev+1), z(ldz, nev+1),
+ * workev(3*ncv); sigmar/sigmai by value. */
+void dneupd_c(a_int rvec, char const* howmny, a_int const* select, double* dr, double* di,
+              double* z, a_int ldz, double sigmar, double sigmai, double* workev,
+              char const* bmat, a_int n, char const* which, a_int nev, double tol, double* resid,
+              a_int ncv, double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
+              double* workl, a_int lworkl, a_int* info);
+
 /* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
  *      argument by reference + hidden trailing CHARACTER lengths ---------------- */
 void dsaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
@@ -60,6 +68,11 @@ void dnaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* n
              double* tol, double* resid, a_int* ncv, double* v, a_int* ldv, a_int* iparam,
              a_int* ipntr, double* workd, double* workl, a_int* lworkl, a_int* info,
              size_t bmat_len, size_t which_len);
+void dneupd_(a_int* rvec, char const* howmny, a_int* select, double* dr, double* di, double* z,
+             a_int* ldz, double* sigmar, double* sigmai, double* workev, char const* bmat,
+             a_int* n, char const* which, a_int* nev, double* tol, double* resid, a_int* ncv,
+             double* v, a_int* ldv, a_int* iparam, a_int* ipntr, double* workd, double* workl,
+             a_int* lworkl, a_int* info, size_t howmny_len, size_t bmat_len, size_t which_len);
 void dseupd_(a_int* rvec, char const* howmny, a_int* select, double* d, double* z,
              a_int* ldz, double* sigma, char const* bmat, a_int* n, char const* which,
              a_int* nev, double* tol, double* resid, a_int* ncv, double* v, a_int* ldv,
@@ -213,6 +226,8 @@ void arpack_hip_kit_dngets(int ishift, char const* which, int* kev, int* np, dou
                            double* ritzi, double* bounds);
 int arpack_hip_kit_dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr,
                           double* ritzi, double* bounds, double* q, int ldq, double* workl);
+int arpack_hip_kit_dtrsen(const int* select, int n, double* t, int ldt, double* q, int ldq,
+                          double* wr, double* wi, int* m); /* job='N', compq='V' */
 int arpack_hip_kit_dnapps_host(int kev, int np, const double* shiftr, const double* shifti,
                                double* h, int ldh, double* q, int ldq, double* workl,
                                int64_t nglob);

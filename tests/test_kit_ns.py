@@ -211,3 +211,42 @@ def test_dnapps_host_matches_reference(pkg, kev, seed):
     # complex-pair steps run dlarf (dgemv + dger): a few ulps of drift allowed
     np.testing.assert_allclose(h1, h2, rtol=0, atol=1e-10 * np.abs(h1).max())
     np.testing.assert_allclose(q1, q2, rtol=0, atol=1e-10)
+
+
+@pytest.mark.parametrize("n,seed,pick", [(12, 0, "last"), (20, 1, "every3"), (30, 2, "last"),
+                                         (40, 3, "rand"), (40, 4, "rand")])
+def test_dtrsen_matches_lapack(pkg, n, seed, pick):
+    """Schur reordering used by dneupd (SRC/dneupd.f:659): dtrsen('N','V') with
+    dtrexc/dlaexc/dlasy2 underneath, bitwise against the image's LAPACK."""
+    B = _blas()
+    h = _hess(n, seed)
+    z = np.asfortranarray(np.eye(n))
+    wr, wi = np.zeros(n), np.zeros(n)
+    assert pkg.lib().arpack_hip_kit_dlahqr(1, 1, n, 1, n, pd(h), n, pd(wr), pd(wi), 1, n, pd(z),
+                                           n) == 0
+    sel = np.zeros(n, np.int32)
+    if pick == "last":
+        sel[-n // 3:] = 1
+    elif pick == "every3":
+        sel[::3] = 1
+    else:
+        sel[np.random.default_rng(seed).permutation(n)[:n // 2]] = 1
+    t1, q1 = h.copy(order="F"), z.copy(order="F")
+    wr1, wi1 = np.zeros(n), np.zeros(n)
+    m1, info1 = C.c_int(), C.c_int()
+    s_, sep = C.c_double(), C.c_double()
+    work = np.zeros(n)
+    iwork = np.zeros(1, np.int32)
+    B.scipy_dtrsen_(C.c_char_p(b"N"), C.c_char_p(b"V"), pi(sel), ri(n), pd(t1), ri(n), pd(q1),
+                    ri(n), pd(wr1), pd(wi1), C.byref(m1), C.byref(s_), C.byref(sep), pd(work),
+                    ri(n), pi(iwork), ri(1), C.byref(info1), C.c_size_t(1), C.c_size_t(1))
+    t2, q2 = h.copy(order="F"), z.copy(order="F")
+    wr2, wi2 = np.zeros(n), np.zeros(n)
+    m2 = C.c_int()
+    info2 = pkg.lib().arpack_hip_kit_dtrsen(pi(sel), n, pd(t2), n, pd(q2), n, pd(wr2), pd(wi2),
+                                            C.byref(m2))
+    assert (info1.value, m1.value) == (info2, m2.value)
+    np.testing.assert_array_equal(wr1, wr2)
+    np.testing.assert_array_equal(wi1, wi2)
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(q1, q2)
