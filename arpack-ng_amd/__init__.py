@@ -105,6 +105,18 @@ def _declare(L):
     L.dnaupd_.argtypes = L.dsaupd_.argtypes
     L.arpack_hip_dnaupd_csr_cycles.argtypes = L.arpack_hip_dsaupd_csr_cycles.argtypes
     L.arpack_hip_gen_convdiff2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
+    L.znaupd_c.argtypes = [_PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I,
+                           _PI, _PI, _PD, _PD, _I, _PD, _PI]
+    L.arpack_hip_znaupd_zcsr.argtypes = [C.c_void_p, _PI, C.c_char_p, _I, C.c_char_p, _I,
+                                         C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI, _PD,
+                                         _PD, _I, _PD, _PI]
+    L.arpack_hip_zcsr_create.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64, C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
+    L.arpack_hip_gen_zrandom.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int, C.c_uint32,
+                                         C.c_double]
+    L.arpack_hip_zcsr_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_zcsr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.arpack_hip_zcsr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_profile.argtypes = [_I]
     L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
     L.arpack_hip_synchronize.restype = C.c_int
@@ -492,6 +504,126 @@ class NsRci(SymRci):
     def ritz(self):
         o, oi = int(self.ipntr[5]) - 1, int(self.ipntr[6]) - 1
         return self.workl[o:o + self.ncv] + 1j * self.workl[oi:oi + self.ncv]
+
+
+class ZCSR:
+    """Complex CSR operator in HBM (arpack_hip_zcsr)."""
+
+    def __init__(self, handle):
+        self.h = handle
+        n, nnz = C.c_int64(), C.c_int64()
+        lib().arpack_hip_zcsr_info(self.h, C.byref(n), C.byref(nnz))
+        self.n, self.nnz = n.value, nnz.value
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_zcsr_destroy(self.h)
+        except Exception:
+            pass
+
+    @classmethod
+    def from_arrays(cls, rowptr, col, val):
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        cc = np.ascontiguousarray(col, np.int32)
+        vv = np.ascontiguousarray(val, np.complex128)
+        h = C.c_void_p()
+        if lib().arpack_hip_zcsr_create(C.byref(h), len(rp) - 1, len(cc), rp.ctypes.data,
+                                        cc.ctypes.data, vv.ctypes.data) != 0:
+            raise RuntimeError("zcsr_create failed")
+        return cls(h.value)
+
+    @classmethod
+    def random(cls, n, per_row=100, seed=5, dshift=100.0):
+        """BASELINE config 5 operator generated in HBM (oracle twin: matrices.zrandom)."""
+        h = C.c_void_p()
+        if lib().arpack_hip_gen_zrandom(C.byref(h), n, per_row, seed, dshift) != 0:
+            raise RuntimeError("gen_zrandom failed")
+        return cls(h.value)
+
+    def download(self):
+        rp = np.zeros(self.n + 1, np.int64)
+        col = np.zeros(self.nnz, np.int32)
+        val = np.zeros(self.nnz, np.complex128)
+        lib().arpack_hip_zcsr_download(self.h, rp.ctypes.data, col.ctypes.data, val.ctypes.data)
+        return rp, col, val
+
+
+class ZRci:
+    """znaupd/zneupd state (SRC/znaupd.f, SRC/zneupd.f): complex128 arrays,
+    ipntr(14), lworkl = 3*ncv^2 + 5*ncv, rwork(ncv).  Host arrays; the caller
+    applies OP on workd slices (ido = -1/1; B*x at ipntr(3) in mode 3)."""
+
+    def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300, ishift=1,
+                 v0=None):
+        self.n, self.nev, self.ncv = n, nev, ncv
+        self.which, self.bmat, self.tol, self.mode = which, bmat, float(tol), mode
+        self.ido = np.zeros(1, np.int32)
+        self.info = np.zeros(1, np.int32)
+        self.iparam = np.zeros(11, np.int32)
+        self.ipntr = np.zeros(14, np.int32)
+        self.iparam[0], self.iparam[2], self.iparam[6] = ishift, mxiter, mode
+        self.lworkl = 3 * ncv * ncv + 5 * ncv
+        self.workl = np.zeros(self.lworkl, np.complex128)
+        self.rwork = np.zeros(ncv)
+        self.resid = np.zeros(n, np.complex128) if v0 is None else np.array(v0, np.complex128)
+        self.v = np.zeros(ncv * n, np.complex128)
+        self.workd = np.zeros(3 * n, np.complex128)
+        self.info[0] = 0 if v0 is None else 1
+
+    def aupd(self):
+        """One znaupd_c call (tol by value, SRC/icbazn.F90); returns ido."""
+        lib().znaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev,
+                       self.tol, self.resid.ctypes.data, self.ncv, self.v.ctypes.data, self.n,
+                       _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
+                       self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data, _ip(self.info))
+        return int(self.ido[0])
+
+    def aupd_zcsr(self, A: "ZCSR"):
+        """Whole loop on the GPU with OP = A (mode 1)."""
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_znaupd_zcsr(A.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                     self.which.encode(), self.nev, C.byref(tol),
+                                     self.resid.ctypes.data, self.ncv, self.v.ctypes.data, self.n,
+                                     _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
+                                     self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data,
+                                     _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
+    def slice(self, k):
+        o = int(self.ipntr[k]) - 1
+        return self.workd[o:o + self.n]
+
+    def eupd(self, rvec=True, howmny="A", sigma=0j):
+        """zneupd_c: returns (d, Z (n x nconv), nconv)."""
+        nconv = int(self.iparam[4])
+        d = np.zeros(self.nev + 1, np.complex128)
+        z = np.zeros((self.nev + 1) * self.n, np.complex128)
+        select = np.zeros(self.ncv, np.int32)
+        workev = np.zeros(2 * self.ncv, np.complex128)
+        info = np.zeros(1, np.int32)
+        f = lib().zneupd_c
+        f.argtypes = [_I, C.c_char_p, _PI, _PD, _PD, _I, _CD, _PD, C.c_char_p, _I, C.c_char_p, _I,
+                      C.c_double, _PD, _I, _PD, _I, _PI, _PI, _PD, _PD, _I, _PD, _PI]
+        f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, z.ctypes.data, self.n,
+          _CD(sigma.real, sigma.imag), workev.ctypes.data, self.bmat.encode(), self.n,
+          self.which.encode(), self.nev, self.tol, self.resid.ctypes.data, self.ncv,
+          self.v.ctypes.data, self.n, _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
+          self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data, _ip(info))
+        if info[0] < 0:
+            raise ArpackError("zneupd", int(info[0]))
+        return d[:nconv], z.reshape(self.nev + 1, self.n)[:nconv].T, nconv
+
+    @property
+    def ritz(self):
+        o = int(self.ipntr[5]) - 1
+        return self.workl[o:o + self.ncv].copy()
+
+
+class _CD(C.Structure):
+    """C99 double _Complex passed by value (two doubles in SSE registers)."""
+    _fields_ = [("re", C.c_double), ("im", C.c_double)]
 
 
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,

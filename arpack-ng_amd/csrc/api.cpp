@@ -57,6 +57,8 @@ static void ensure_seed() {
     }
 }
 
+void ahip_ensure_seed() { ensure_seed(); }
+
 // dsaupd argument checks (SRC/dsaupd.f:501-543); returns ierr
 static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lworkl, int mode,
                      int ishift, int mxiter) {

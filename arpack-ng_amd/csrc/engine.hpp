@@ -27,6 +27,7 @@ extern uint64_t g_dseed;
 uint64_t seed48_from_iseed(const int iseed[4]);
 void iseed_from_seed48(uint64_t s, int iseed[4]);
 uint64_t lcg_advance(uint64_t seed, uint64_t steps);  // seed * a^steps mod 2^48
+void ahip_ensure_seed();  // iseed = (1,3,5,7) once per process
 
 // Caller-visible arrays in one place. `dev_*` are what the kernels use: the
 // caller's own buffers in device-pointer mode, engine-owned mirrors in

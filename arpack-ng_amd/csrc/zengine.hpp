@@ -1,0 +1,93 @@
+// Complex (znaupd family) engine: device workspace, complex CSR operator and
+// the ZSolver coroutine (zsolver.cpp).  The complex path keeps the shared
+// Arrays mirror (n complex = 2n doubles) and drives its step decisions from
+// the host: config 5 is shift-invert, where the caller's solve dominates.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <complex>
+#include <cstdint>
+#include <optional>
+#include <vector>
+
+#include "engine.hpp"
+#include "zdense.hpp"
+
+namespace ahip {
+
+namespace zdev {
+struct Ws {
+    hipStream_t stream = nullptr;
+    int nblk = 0;
+    double* part = nullptr;  // 2*(ncv+2) slots x nblk
+    double* sums = nullptr;
+    double* coef = nullptr;  // complex coefficients (h) staged for the update
+    double* q = nullptr;     // complex ncv x ncv (V*Q, eupd)
+    double* host = nullptr;  // pinned
+};
+struct ZCsr {
+    int64_t n = 0, nnz = 0;
+    const int64_t* rowptr = nullptr;
+    const int32_t* col = nullptr;
+    const double* val = nullptr;  // interleaved complex
+    bool owned = false;
+};
+hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s);
+void ws_destroy(Ws& ws);
+// out[c] = V(:,c)^H u for c < j; out[j] = w^H u if w
+void dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
+          const double* w, std::complex<double>* out);
+// rout = rin - V(:,0:j) h
+void update(const Ws& ws, int64_t n, int j, const double* V, int64_t ld,
+            const std::complex<double>* h, const double* rin, double* rout);
+// Z(:,0:nz) = V(:,0:k) M (k x nz); Z may alias V
+void gemm(const Ws& ws, int64_t n, const double* V, int64_t ld, int k, int nz,
+          const std::complex<double>* M, double* Z, int64_t ldz);
+// y = a*y + b*x (x may be null)
+void axpby(const Ws& ws, int64_t n, std::complex<double> a, double* y, std::complex<double> b,
+           const double* x);
+// Z(:,c) += x * w[c]
+void ger(const Ws& ws, int64_t n, int k, const double* x, const std::complex<double>* w,
+         double* Z, int64_t ldz);
+void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
+int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift);
+}  // namespace zdev
+
+class ZSolver {
+public:
+    using cd = std::complex<double>;
+    char bmat = 'I';
+    la::Which which = la::Which::LM;
+    int n = 0, ncv = 0, mode = 1, ishift = 1, mxiter = 0, nev0 = 0, np = 0, lworkl = 0;
+    double tol = 0.0;
+    int* iparam = nullptr;
+    int* ipntr = nullptr;
+    cd* workl = nullptr;
+    double* rwork = nullptr;
+    int info = 0;
+    int ih = 0, iritz = 0, ibounds = 0, iq = 0, iw = 0;
+    double rnorm = 0.0;
+
+    Arrays a;  // n complex = 2n doubles; offsets below are in complex units
+    zdev::Ws ws;
+    RciCtx ctx;
+    std::optional<Task> root;
+    const zdev::ZCsr* csr = nullptr;  // free-running OP (mode 1)
+    const double* op_x = nullptr;
+    double* op_y = nullptr;
+
+    ~ZSolver();
+    Task run();  // znaup2
+
+private:
+    Task getv0(bool initv, int j, int itry, int& ierr);
+    Task naitr(int k, int npk, int& iinfo);
+    RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
+    RciAwait op(int ido, int64_t x, int64_t y, int64_t bx);
+    double* col(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based, doubles
+    double* wd(int64_t off) { return a.d_workd + 2 * off; }           // complex offset
+    int64_t ldc() const { return a.d_ld / 2; }                         // ld in complex units
+    double cnorm(const double* x);                                     // dznrm2 on device
+};
+
+}  // namespace ahip

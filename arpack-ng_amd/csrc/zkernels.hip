@@ -1,0 +1,388 @@
+// Complex (complex128) n-length kernels of the znaupd engine and the complex
+// CSR operator.  Vectors are interleaved (re, im) doubles, i.e. the layout of
+// Fortran COMPLEX*16 / C double _Complex.  All HBM-bound:
+//   zdots   partial sums of V(:,c0:c0+8)^H u, 8 columns per pass over u
+//   zupdate r = w - V h
+//   zgemm   Z = V(:,0:k) M (row-local, alias-safe): znapps V*Q, zneupd
+//   zcsr    y = A x, one wavefront per row
+// Reductions are two-stage and fixed-order (bitwise reproducible).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/arpack_hip.h"
+#include "zengine.hpp"
+
+namespace ahip::zdev {
+
+namespace {
+constexpr int kB = 256;
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {  // conj(a) * b
+    return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
+}
+
+// part layout: part[slot * nblk + block]; slot 2c = Re, 2c+1 = Im of column c0+c
+template <int C>
+__global__ __launch_bounds__(kB) void k_zdots(int64_t n, int c0, int cnt, const double2* __restrict__ V,
+                                              int64_t ld, const double2* __restrict__ u,
+                                              double* __restrict__ part, int nblk) {
+    double2 acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = make_double2(0.0, 0.0);
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        const double2 ui = u[i];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (c < cnt) {
+                const double2 p = cmulc(V[i + (int64_t)(c0 + c) * ld], ui);
+                acc[c].x += p.x;
+                acc[c].y += p.y;
+            }
+    }
+    __shared__ double red[4][2 * C];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        if (c < cnt) {
+            const double re = wsum(acc[c].x), im = wsum(acc[c].y);
+            if (lane == 0) {
+                red[wave][2 * c] = re;
+                red[wave][2 * c + 1] = im;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * cnt) {
+        const int s = threadIdx.x;
+        const double v = (red[0][s] + red[1][s]) + (red[2][s] + red[3][s]);
+        part[(int64_t)(2 * c0 + s) * nblk + blockIdx.x] = v;
+    }
+}
+
+__global__ __launch_bounds__(kB) void k_sum_slots(const double* __restrict__ part, int nblk,
+                                                  double* __restrict__ sums) {
+    __shared__ double red[4];
+    const double* p = part + (int64_t)blockIdx.x * nblk;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += kB) s += p[b];
+    s = wsum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(kB) void k_zupdate(int64_t n, int j, const double2* __restrict__ V,
+                                                int64_t ld, const double2* __restrict__ h,
+                                                const double2* rin, double2* rout) {
+    __shared__ double2 sh[256];
+    for (int c = threadIdx.x; c < j; c += kB) sh[c] = h[c];
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        double2 r = rin[i];
+        for (int c = 0; c < j; ++c) {
+            const double2 p = cmul(V[i + (int64_t)c * ld], sh[c]);
+            r.x -= p.x;
+            r.y -= p.y;
+        }
+        rout[i] = r;
+    }
+}
+
+template <int MAXK>
+__global__ __launch_bounds__(kB) void k_zgemm(int64_t n, const double2* V, int64_t ld, int k, int nz,
+                                              const double2* __restrict__ M, double2* Z, int64_t ldz) {
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        double2 v[MAXK];
+#pragma unroll
+        for (int t = 0; t < MAXK; ++t) v[t] = (t < k) ? V[i + (int64_t)t * ld] : make_double2(0.0, 0.0);
+        for (int l = 0; l < nz; ++l) {
+            double2 o = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int t = 0; t < MAXK; ++t)
+                if (t < k) {
+                    const double2 p = cmul(v[t], M[t + (int64_t)l * k]);
+                    o.x += p.x;
+                    o.y += p.y;
+                }
+            Z[i + (int64_t)l * ldz] = o;
+        }
+    }
+}
+
+__global__ void k_zaxpby(int64_t n, double2 a, double2* y, double2 b, const double2* x) {
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        double2 r = cmul(a, y[i]);
+        if (x) {
+            const double2 p = cmul(b, x[i]);
+            r.x += p.x;
+            r.y += p.y;
+        }
+        y[i] = r;
+    }
+}
+
+__global__ void k_zger(int64_t n, int k, const double2* __restrict__ x, const double2* __restrict__ w,
+                       double2* Z, int64_t ldz) {
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        const double2 xi = x[i];
+        for (int c = 0; c < k; ++c) {
+            const double2 p = cmul(xi, w[c]);
+            Z[i + (int64_t)c * ldz].x += p.x;
+            Z[i + (int64_t)c * ldz].y += p.y;
+        }
+    }
+}
+
+// y = A x, one 64-lane wavefront per row, fixed-order lane reduction
+__global__ __launch_bounds__(kB) void k_zcsr(int64_t n, const int64_t* __restrict__ rp,
+                                             const int32_t* __restrict__ col,
+                                             const double2* __restrict__ val,
+                                             const double2* __restrict__ x, double2* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * kB + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * kB) >> 6;
+    for (int64_t r = wid; r < n; r += nw) {
+        double re = 0.0, im = 0.0;
+        for (int64_t k = rp[r] + lane; k < rp[r + 1]; k += 64) {
+            const double2 p = cmul(val[k], x[col[k]]);
+            re += p.x;
+            im += p.y;
+        }
+        re = wsum(re);
+        im = wsum(im);
+        if (lane == 0) y[r] = make_double2(re, im);
+    }
+}
+
+// ---- complex random operator (BASELINE config 5) ----------
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+constexpr int kMaxPerRow = 128;
+
+__device__ void zrow(int64_t i, int64_t n, uint32_t sm, int per_row, uint32_t* cols, double* re,
+                     double* im) {
+    for (int k = 0; k < per_row; ++k) {
+        const uint32_t h = mix32(mix32((uint32_t)i ^ sm) + (uint32_t)k * 0x9E3779B9u);
+        cols[k] = (uint32_t)((uint64_t)h % (uint64_t)n);
+        re[k] = (double)(mix32(h ^ 0x68e31da4u) >> 21) * 0x1p-10 - 1.0;
+        im[k] = (double)(mix32(h ^ 0x1b873593u) >> 21) * 0x1p-10 - 1.0;
+    }
+    for (int a = 1; a < per_row; ++a) {  // insertion sort by column (stable)
+        const uint32_t c = cols[a];
+        const double xr = re[a], xi = im[a];
+        int b = a - 1;
+        while (b >= 0 && cols[b] > c) {
+            cols[b + 1] = cols[b];
+            re[b + 1] = re[b];
+            im[b + 1] = im[b];
+            --b;
+        }
+        cols[b + 1] = c;
+        re[b + 1] = xr;
+        im[b + 1] = xi;
+    }
+}
+
+__global__ void k_zgen_count(int64_t n, uint32_t sm, int per_row, int64_t* cnt) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t cols[kMaxPerRow];
+        double re[kMaxPerRow], im[kMaxPerRow];
+        zrow(i, n, sm, per_row, cols, re, im);
+        int64_t c = 0;
+        bool diag = false;
+        for (int k = 0; k < per_row; ++k) {
+            if (k == 0 || cols[k] != cols[k - 1]) ++c;
+            if (cols[k] == (uint32_t)i) diag = true;
+        }
+        cnt[i] = c + (diag ? 0 : 1);
+    }
+}
+
+__global__ void k_zgen_fill(int64_t n, uint32_t sm, int per_row, double dshift, const int64_t* rp,
+                            int32_t* col, double2* val) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t cols[kMaxPerRow];
+        double re[kMaxPerRow], im[kMaxPerRow];
+        zrow(i, n, sm, per_row, cols, re, im);
+        int64_t o = rp[i];
+        bool dput = false;
+        for (int k = 0; k < per_row;) {
+            const uint32_t c = cols[k];
+            if (!dput && c > (uint32_t)i) {  // diagonal not hit by the hash: insert it
+                col[o] = (int32_t)i;
+                val[o++] = make_double2(dshift, 0.0);
+                dput = true;
+            }
+            double sr = 0.0, si = 0.0;
+            while (k < per_row && cols[k] == c) {  // duplicates summed (exact: 2^-10 grid)
+                sr += re[k];
+                si += im[k];
+                ++k;
+            }
+            if (c == (uint32_t)i) {
+                sr += dshift;
+                dput = true;
+            }
+            col[o] = (int32_t)c;
+            val[o++] = make_double2(sr, si);
+        }
+        if (!dput) {
+            col[o] = (int32_t)i;
+            val[o++] = make_double2(dshift, 0.0);
+        }
+    }
+}
+
+inline int grid(int64_t n, int cap = 8192) {
+    int64_t g = (n + kB - 1) / kB;
+    if (g > cap) g = cap;
+    return (int)(g < 1 ? 1 : g);
+}
+}  // namespace
+
+void dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
+          const double* w, std::complex<double>* out) {
+    const double2* V2 = reinterpret_cast<const double2*>(V);
+    const double2* u2 = reinterpret_cast<const double2*>(u);
+    for (int c0 = 0; c0 < j; c0 += 8) {
+        const int cnt = j - c0 < 8 ? j - c0 : 8;
+        hipLaunchKernelGGL(k_zdots<8>, dim3(ws.nblk), dim3(kB), 0, ws.stream, n, c0, cnt, V2, ld, u2,
+                           ws.part, ws.nblk);
+    }
+    // slot j: w^H u (a "column" at w with ld irrelevant)
+    if (w) {
+        hipLaunchKernelGGL(k_zdots<1>, dim3(ws.nblk), dim3(kB), 0, ws.stream, n, 0, 1,
+                           reinterpret_cast<const double2*>(w), 0, u2, ws.part + (int64_t)2 * j * ws.nblk,
+                           ws.nblk);
+    }
+    const int m = 2 * (j + (w ? 1 : 0));
+    hipLaunchKernelGGL(k_sum_slots, dim3(m), dim3(kB), 0, ws.stream, ws.part, ws.nblk, ws.sums);
+    (void)hipMemcpyAsync(ws.host, ws.sums, sizeof(double) * m, hipMemcpyDeviceToHost, ws.stream);
+    (void)hipStreamSynchronize(ws.stream);
+    for (int c = 0; c < m / 2; ++c) out[c] = std::complex<double>(ws.host[2 * c], ws.host[2 * c + 1]);
+}
+
+void update(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const std::complex<double>* h,
+            const double* rin, double* rout) {
+    if (j > 0) (void)hipMemcpyAsync(ws.coef, h, sizeof(double) * 2 * j, hipMemcpyHostToDevice, ws.stream);
+    hipLaunchKernelGGL(k_zupdate, dim3(grid(n)), dim3(kB), 0, ws.stream, n, j,
+                       reinterpret_cast<const double2*>(V), ld, reinterpret_cast<const double2*>(ws.coef),
+                       reinterpret_cast<const double2*>(rin), reinterpret_cast<double2*>(rout));
+    (void)hipStreamSynchronize(ws.stream);  // h is host memory
+}
+
+void gemm(const Ws& ws, int64_t n, const double* V, int64_t ld, int k, int nz, const std::complex<double>* M,
+          double* Z, int64_t ldz) {
+    (void)hipMemcpyAsync(ws.q, M, sizeof(double) * 2 * (size_t)k * nz, hipMemcpyHostToDevice, ws.stream);
+    auto V2 = reinterpret_cast<const double2*>(V);
+    auto M2 = reinterpret_cast<const double2*>(ws.q);
+    auto Z2 = reinterpret_cast<double2*>(Z);
+    if (k <= 16)
+        hipLaunchKernelGGL(k_zgemm<16>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+    else if (k <= 32)
+        hipLaunchKernelGGL(k_zgemm<32>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+    else
+        hipLaunchKernelGGL(k_zgemm<64>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+    (void)hipStreamSynchronize(ws.stream);
+}
+
+void axpby(const Ws& ws, int64_t n, std::complex<double> a, double* y, std::complex<double> b,
+           const double* x) {
+    hipLaunchKernelGGL(k_zaxpby, dim3(grid(n)), dim3(kB), 0, ws.stream, n, make_double2(a.real(), a.imag()),
+                       reinterpret_cast<double2*>(y), make_double2(b.real(), b.imag()),
+                       reinterpret_cast<const double2*>(x));
+}
+
+void ger(const Ws& ws, int64_t n, int k, const double* x, const std::complex<double>* w, double* Z,
+         int64_t ldz) {
+    (void)hipMemcpyAsync(ws.coef, w, sizeof(double) * 2 * k, hipMemcpyHostToDevice, ws.stream);
+    hipLaunchKernelGGL(k_zger, dim3(grid(n)), dim3(kB), 0, ws.stream, n, k,
+                       reinterpret_cast<const double2*>(x), reinterpret_cast<const double2*>(ws.coef),
+                       reinterpret_cast<double2*>(Z), ldz);
+    (void)hipStreamSynchronize(ws.stream);
+}
+
+hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s) {
+    ws.stream = s;
+    int64_t g = (n + kB - 1) / kB;
+    ws.nblk = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+    const int slots = 2 * (ncv + 2);
+    hipError_t e;
+    if ((e = hipMalloc(&ws.part, sizeof(double) * (size_t)ws.nblk * slots))) return e;
+    if ((e = hipMalloc(&ws.sums, sizeof(double) * slots))) return e;
+    if ((e = hipMalloc(&ws.coef, sizeof(double) * slots))) return e;
+    if ((e = hipMalloc(&ws.q, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
+    if ((e = hipHostMalloc(&ws.host, sizeof(double) * slots))) return e;
+    return hipSuccess;
+}
+
+void ws_destroy(Ws& ws) {
+    if (ws.part) (void)hipFree(ws.part);
+    if (ws.sums) (void)hipFree(ws.sums);
+    if (ws.coef) (void)hipFree(ws.coef);
+    if (ws.q) (void)hipFree(ws.q);
+    if (ws.host) (void)hipHostFree(ws.host);
+    ws = Ws{};
+}
+
+void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y) {
+    hipLaunchKernelGGL(k_zcsr, dim3(grid(A.n * 64, 65536)), dim3(kB), 0, s, A.n, A.rowptr, A.col,
+                       reinterpret_cast<const double2*>(A.val), reinterpret_cast<const double2*>(x),
+                       reinterpret_cast<double2*>(y));
+}
+
+int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift) {
+    if (per_row < 1 || per_row > kMaxPerRow) return -1;
+    int64_t *cnt = nullptr, *rp = nullptr;
+    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
+    const uint32_t sm = mix32(seed);
+    hipLaunchKernelGGL(k_zgen_count, dim3(grid(n, 65536)), dim3(kB), 0, nullptr, n, sm, per_row, cnt);
+    std::vector<int64_t> h(n + 1);
+    (void)hipMemcpy(h.data(), cnt, sizeof(int64_t) * n, hipMemcpyDeviceToHost);
+    int64_t acc = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c = h[i];
+        h[i] = acc;
+        acc += c;
+    }
+    h[n] = acc;
+    (void)hipMemcpy(rp, h.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice);
+    (void)hipFree(cnt);
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    if (hipMalloc(&col, sizeof(int32_t) * acc) || hipMalloc(&val, sizeof(double) * 2 * acc)) return -1;
+    hipLaunchKernelGGL(k_zgen_fill, dim3(grid(n, 65536)), dim3(kB), 0, nullptr, n, sm, per_row, dshift, rp,
+                       col, reinterpret_cast<double2*>(val));
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    A.n = n;
+    A.nnz = acc;
+    A.rowptr = rp;
+    A.col = col;
+    A.val = val;
+    A.owned = true;
+    return 0;
+}
+
+}  // namespace ahip::zdev

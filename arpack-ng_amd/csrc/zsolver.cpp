@@ -1,0 +1,774 @@
+// Complex implicitly restarted Arnoldi (znaupd family), re-hosted as
+// coroutines over the complex device kernels (zkernels.hip).
+//
+// Reference map:
+//   ZSolver::run     SRC/znaup2.f  (restart loop)
+//   ZSolver::naitr   SRC/znaitr.f  (Arnoldi step, CGS + DGKS with zgemv 'C')
+//   ZSolver::getv0   SRC/zgetv0.f  (zlarnv start vector, restart vector)
+//   host             zneigh / zngets / zsortc / znapps chase (zdense.cpp)
+//   z_aupd           SRC/znaupd.f  (checks, workl layout, iparam)
+//   z_eupd           SRC/zneupd.f  (Schur form, ztrsen, Ritz vectors)
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+
+#include "../../include/arpack_hip.h"
+#include "zengine.hpp"
+
+namespace ahip {
+
+using cd = std::complex<double>;
+
+ZSolver::~ZSolver() {
+    root.reset();
+    zdev::ws_destroy(ws);
+    a.release();
+}
+
+RciAwait ZSolver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
+    op_x = nullptr;
+    op_y = nullptr;
+    return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+RciAwait ZSolver::op(int ido, int64_t x, int64_t y, int64_t bx) {
+    op_x = wd(x);
+    op_y = wd(y);
+    return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+double ZSolver::cnorm(const double* x) {
+    cd s;
+    zdev::dots(ws, n, 0, a.d_v, ldc(), x, x, &s);
+    return std::sqrt(std::fabs(s.real()));
+}
+
+// zgetv0 (SRC/zgetv0.f): start vector in range(OP), B-orthogonal to V(:,1:j-1)
+Task ZSolver::getv0(bool initv, int j, int itry, int& ierr) {
+    const int64_t nn = n;
+    ierr = 0;
+    if (!initv) {  // zlarnv(idist=2): re/im pairs of one dlaruv stream
+        dev::Workspace tmp;
+        tmp.stream = a.stream;
+        dev::larnv_uniform(tmp, 2 * nn, g_dseed, a.d_resid);
+        g_dseed = lcg_advance(g_dseed, (uint64_t)(2 * nn));
+    }
+    if (itry == 1) {
+        g_stats.nopx += 1;
+        dev::copy(a.stream, 2 * nn, a.d_resid, wd(0));
+        co_await op(-1, 0, nn, -1);
+        dev::copy(a.stream, 2 * nn, wd(nn), a.d_resid);
+    } else if (bmat == 'G') {
+        dev::copy(a.stream, 2 * nn, a.d_resid, wd(nn));
+    }
+    double rnorm0;
+    if (bmat == 'G') {
+        g_stats.nbx += 1;
+        if (itry == 1) dev::copy(a.stream, 2 * nn, a.d_resid, wd(nn));
+        co_await rci(2, nn, 0);
+        cd s;
+        zdev::dots(ws, nn, 0, a.d_v, ldc(), wd(0), a.d_resid, &s);
+        rnorm0 = std::sqrt(std::abs(s));
+    } else {
+        dev::copy(a.stream, 2 * nn, a.d_resid, wd(0));
+        rnorm0 = cnorm(a.d_resid);
+    }
+    rnorm = rnorm0;
+    if (j == 1) co_return;
+    std::vector<cd> c(j);
+    for (int iter = 0;;) {
+        zdev::dots(ws, nn, j - 1, a.d_v, ldc(), wd(0), nullptr, c.data());
+        zdev::update(ws, nn, j - 1, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
+        if (bmat == 'G') {
+            g_stats.nbx += 1;
+            dev::copy(a.stream, 2 * nn, a.d_resid, wd(nn));
+            co_await rci(2, nn, 0);
+            cd s;
+            zdev::dots(ws, nn, 0, a.d_v, ldc(), wd(0), a.d_resid, &s);
+            rnorm = std::sqrt(std::abs(s));
+        } else {
+            dev::copy(a.stream, 2 * nn, a.d_resid, wd(0));
+            rnorm = cnorm(a.d_resid);
+        }
+        if (rnorm > 0.717 * rnorm0) break;
+        ++iter;
+        if (iter <= 5) {
+            rnorm0 = rnorm;
+            continue;
+        }
+        dev::fill(a.stream, 2 * nn, 0.0, a.d_resid);
+        rnorm = 0.0;
+        ierr = -1;
+        break;
+    }
+    co_return;
+}
+
+// znaitr: extend a k-step Arnoldi factorization to k+npk steps (host-driven).
+Task ZSolver::naitr(int k, int npk, int& iinfo) {
+    const int64_t nn = n;
+    const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
+    const int ldh = ncv;
+    cd* h = workl + ih;
+    const double unfl = la::kSafmin;
+    iinfo = 0;
+    std::vector<cd> c(ncv + 1);
+    for (int j = k + 1; j <= k + npk; ++j) {
+        double betaj = rnorm;
+        if (!(rnorm > 0.0)) {  // restart with a vector orthogonal to V (SRC/znaitr.f:373-422)
+            betaj = 0.0;
+            g_stats.nrstrt += 1;
+            int itry = 1, ierr = 0;
+            for (;;) {
+                co_await getv0(false, j, itry, ierr);
+                if (ierr >= 0) break;
+                if (++itry <= 3) continue;
+                iinfo = j - 1;
+                co_return;
+            }
+        }
+        // v_j = r / rnorm (and workd(ipj) for bmat = 'G') (SRC/znaitr.f:434-450)
+        dev::copy(a.stream, 2 * nn, a.d_resid, col(j));
+        if (rnorm >= unfl) {
+            const double t = 1.0 / rnorm;
+            dev::scal(a.stream, 2 * nn, t, col(j));
+            dev::scal(a.stream, 2 * nn, t, wd(ipj));
+        } else {
+            double mul[4];
+            const int nm = la::lascl_factors(rnorm, 1.0, mul);
+            for (int q = 0; q < nm; ++q) {
+                dev::scal(a.stream, 2 * nn, mul[q], col(j));
+                dev::scal(a.stream, 2 * nn, mul[q], wd(ipj));
+            }
+        }
+        g_stats.nopx += 1;
+        dev::copy(a.stream, 2 * nn, col(j), wd(ivj));
+        co_await op(1, ivj, irj, ipj);
+        dev::copy(a.stream, 2 * nn, wd(irj), a.d_resid);
+        double wnorm;
+        if (bmat == 'G') {
+            g_stats.nbx += 1;
+            co_await rci(2, irj, ipj);
+            cd s;
+            zdev::dots(ws, nn, 0, a.d_v, ldc(), wd(ipj), a.d_resid, &s);
+            wnorm = std::sqrt(std::abs(s));
+        } else {
+            dev::copy(a.stream, 2 * nn, a.d_resid, wd(ipj));
+            wnorm = cnorm(a.d_resid);
+        }
+        // CGS: h(1:j,j) = V' B r ; r -= V h (SRC/znaitr.f:567-590)
+        zdev::dots(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
+        for (int i = 0; i < j; ++i) h[i + (size_t)(j - 1) * ldh] = c[i];
+        zdev::update(ws, nn, j, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
+        if (j > 1) h[(j - 1) + (size_t)(j - 2) * ldh] = cd(betaj, 0.0);
+        auto bnorm = [&]() -> Task {  // rnorm of the current resid (with its RCI for 'G')
+            if (bmat == 'G') {
+                g_stats.nbx += 1;
+                dev::copy(a.stream, 2 * nn, a.d_resid, wd(irj));
+                co_await rci(2, irj, ipj);
+                cd s;
+                zdev::dots(ws, nn, 0, a.d_v, ldc(), wd(ipj), a.d_resid, &s);
+                rnorm = std::sqrt(std::abs(s));
+            } else {
+                dev::copy(a.stream, 2 * nn, a.d_resid, wd(ipj));
+                rnorm = cnorm(a.d_resid);
+            }
+        };
+        co_await bnorm();
+        if (!(rnorm > 0.717 * wnorm)) {  // DGKS (SRC/znaitr.f:651-780)
+            g_stats.nrorth += 1;
+            for (int iter = 0;;) {
+                const double rprev = rnorm;
+                zdev::dots(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
+                zdev::update(ws, nn, j, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
+                for (int i = 0; i < j; ++i) h[i + (size_t)(j - 1) * ldh] += c[i];
+                co_await bnorm();
+                if (rnorm > 0.717 * rprev) break;
+                g_stats.nitref += 1;
+                ++iter;
+                if (iter <= 1) continue;
+                dev::fill(a.stream, 2 * nn, 0.0, a.d_resid);
+                rnorm = 0.0;
+                break;
+            }
+        }
+    }
+    // negligible subdiagonals (SRC/znaitr.f:812-830)
+    const double ulp = 2.0 * la::kEps, smlnum = la::kSafmin * ((double)n / ulp);
+    const int kp = k + npk;
+    for (int i = std::max(1, k); i <= kp - 1; ++i) {
+        double tst1 = zla::cabs1(h[(i - 1) + (size_t)(i - 1) * ldh]) + zla::cabs1(h[i + (size_t)i * ldh]);
+        if (tst1 == 0.0) tst1 = zla::lanhs1(kp, h, ldh);
+        cd& sub = h[i + (size_t)(i - 1) * ldh];
+        if (std::fabs(sub.real()) <= std::max(ulp * tst1, smlnum)) sub = 0.0;
+    }
+    co_return;
+}
+
+Task ZSolver::run() {
+    using la::Which;
+    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    int nev = nev0;
+    const int np0 = np, kplusp = nev0 + np0;
+    int nconv = 0, iter = 0;
+    const bool initv = (info != 0);
+    info = 0;
+    cd* h = workl + ih;
+    cd* ritz = workl + iritz;
+    cd* bounds = workl + ibounds;
+    cd* wl = workl + iw;
+    cd* q = workl + iq;
+    int ierr = 0, sinfo = 0;
+    if (initv) a.upload_resid();
+    co_await getv0(initv, 1, 1, ierr);
+    if (rnorm == 0.0) {
+        info = -9;
+        goto done;
+    }
+    co_await naitr(0, nev, sinfo);
+    if (sinfo > 0) {
+        np = sinfo;
+        mxiter = iter;
+        info = -9999;
+        goto fail;
+    }
+    for (;;) {  // SRC/znaup2.f main loop
+        ++iter;
+        np = kplusp - nev;
+        co_await naitr(nev, np, sinfo);
+        if (sinfo > 0) {
+            np = sinfo;
+            mxiter = iter;
+            info = -9999;
+            goto fail;
+        }
+        if (zla::zneigh(rnorm, kplusp, h, ncv, ritz, bounds, q, ncv, wl) != 0) {
+            info = -8;
+            goto fail;
+        }
+        nev = nev0;
+        np = np0;
+        std::memcpy(wl + kplusp * kplusp, ritz, sizeof(cd) * kplusp);
+        std::memcpy(wl + kplusp * kplusp + kplusp, bounds, sizeof(cd) * kplusp);
+        zla::zngets(ishift, which, nev, np, ritz, bounds);
+        nconv = 0;
+        for (int i = 0; i < nev; ++i) {
+            const double rtemp = std::max(eps23, la::lapy2(ritz[np + i].real(), ritz[np + i].imag()));
+            if (la::lapy2(bounds[np + i].real(), bounds[np + i].imag()) <= tol * rtemp) ++nconv;
+        }
+        {
+            const int nptemp = np;
+            for (int j = 0; j < nptemp; ++j)
+                if (bounds[j] == cd(0.0)) {
+                    --np;
+                    ++nev;
+                }
+        }
+        if (nconv >= nev0 || iter > mxiter || np == 0) {
+            h[2] = cd(rnorm, 0.0);  // h(3,1) (SRC/znaup2.f:566)
+            Which wp = which;
+            switch (which) {
+                case Which::LM: wp = Which::SM; break;
+                case Which::SM: wp = Which::LM; break;
+                case Which::LR: wp = Which::SR; break;
+                case Which::SR: wp = Which::LR; break;
+                case Which::LI: wp = Which::SI; break;
+                case Which::SI: wp = Which::LI; break;
+                default: break;
+            }
+            zla::zsortc(wp, true, kplusp, ritz, bounds);
+            for (int j = 0; j < nev0; ++j)
+                bounds[j] /= std::max(eps23, la::lapy2(ritz[j].real(), ritz[j].imag()));
+            zla::zsortc(Which::LM, true, nev0, bounds, ritz);
+            for (int j = 0; j < nev0; ++j)
+                bounds[j] *= std::max(eps23, la::lapy2(ritz[j].real(), ritz[j].imag()));
+            zla::zsortc(which, true, nconv, ritz, bounds);
+            if (iter > mxiter && nconv < nev0) info = 1;
+            if (np == 0 && nconv < nev0) info = 2;
+            np = nconv;
+            goto done;
+        } else if (nconv < nev0 && ishift == 1) {
+            const int nevbef = nev;
+            nev += std::min(nconv, np / 2);
+            if (nev == 1 && kplusp >= 6) nev = kplusp / 2;
+            else if (nev == 1 && kplusp > 3) nev = 2;
+            np = kplusp - nev;
+            if (nevbef < nev) zla::zngets(ishift, which, nev, np, ritz, bounds);
+        }
+        if (ishift == 0) {
+            iparam[7] = np;
+            co_await rci(3, -1, -1);
+            std::memcpy(ritz, wl, sizeof(cd) * np);
+        }
+        {   // znapps: chase on the host, V*Q and resid update on the device
+            zla::znapps_host(nev, np, ritz, h, ncv, q, ncv, wl, n);
+            const int kev = nev;
+            const bool next = h[kev + (size_t)(kev - 1) * ncv].real() > 0.0;
+            const int nz = kev + (next ? 1 : 0);
+            std::vector<cd> M((size_t)kplusp * nz);
+            for (int cc = 0; cc < nz; ++cc)
+                for (int r = 0; r < kplusp; ++r) M[(size_t)cc * kplusp + r] = q[r + (size_t)cc * ncv];
+            zdev::gemm(ws, n, a.d_v, ldc(), kplusp, nz, M.data(), a.d_v, ldc());
+            const cd sigmak = q[(kplusp - 1) + (size_t)(kev - 1) * ncv];
+            const cd betak = h[kev + (size_t)(kev - 1) * ncv];
+            zdev::axpby(ws, n, sigmak, a.d_resid, betak, next ? col(kev + 1) : nullptr);
+        }
+        if (bmat == 'G') {
+            g_stats.nbx += 1;
+            dev::copy(a.stream, 2 * (int64_t)n, a.d_resid, wd(n));
+            co_await rci(2, n, 0);
+            cd s;
+            zdev::dots(ws, n, 0, a.d_v, ldc(), wd(0), a.d_resid, &s);
+            rnorm = std::sqrt(la::lapy2(s.real(), s.imag()));
+        } else {
+            dev::copy(a.stream, 2 * (int64_t)n, a.d_resid, wd(0));
+            rnorm = cnorm(a.d_resid);
+        }
+    }
+done:
+    mxiter = iter;
+fail:
+    iparam[2] = mxiter;
+    co_return;
+}
+
+// ---------------------------------------------------------------- drivers ---
+static std::mutex g_zmu;
+static std::unordered_map<const void*, std::unique_ptr<ZSolver>> g_z;
+
+static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
+                   cd* resid, int ncv, cd* v, int ldv, int* iparam, int* ipntr, cd* workd,
+                   cd* workl, int lworkl, double* rwork, int* info, const zdev::ZCsr* csr) {
+    std::lock_guard<std::mutex> lk(g_zmu);
+    ZSolver* S = nullptr;
+    if (*ido == 0) {
+        ahip_ensure_seed();
+        g_stats = Stats{};
+        const la::Which w = la::parse_which(which);
+        const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
+        int ierr = 0;  // SRC/znaupd.f:473-505
+        if (n <= 0) ierr = -1;
+        else if (nev <= 0) ierr = -2;
+        else if (ncv <= nev || ncv > n) ierr = -3;
+        else if (mxiter <= 0) ierr = -4;
+        else if (w != la::Which::LM && w != la::Which::SM && w != la::Which::LR &&
+                 w != la::Which::SR && w != la::Which::LI && w != la::Which::SI)
+            ierr = -5;
+        else if (bmat[0] != 'I' && bmat[0] != 'G') ierr = -6;
+        else if (lworkl < 3 * ncv * ncv + 5 * ncv) ierr = -7;
+        else if (mode < 1 || mode > 3) ierr = -10;
+        else if (mode == 1 && bmat[0] == 'G') ierr = -11;
+        if (csr && (mode != 1 || csr->n != n)) ierr = ierr ? ierr : -11;
+        if (ierr != 0) {
+            *info = ierr;
+            *ido = 99;
+            return;
+        }
+        if (*tol <= 0.0) *tol = la::kEps;
+        auto up = std::make_unique<ZSolver>();
+        S = up.get();
+        S->bmat = bmat[0];
+        S->which = w;
+        S->n = n;
+        S->ncv = ncv;
+        S->mode = mode;
+        S->ishift = ishift;
+        S->mxiter = mxiter;
+        S->nev0 = nev;
+        S->np = ncv - nev;
+        S->lworkl = lworkl;
+        S->info = *info;
+        std::memset(static_cast<void*>(workl), 0, sizeof(cd) * (size_t)(3 * ncv * ncv + 5 * ncv));
+        S->ih = 0;  // SRC/znaupd.f:541-555
+        S->iritz = S->ih + ncv * ncv;
+        S->ibounds = S->iritz + ncv;
+        S->iq = S->ibounds + ncv;
+        S->iw = S->iq + ncv * ncv;
+        const int next = S->iw + ncv * ncv + 3 * ncv;
+        ipntr[3] = next + 1;
+        ipntr[4] = S->ih + 1;
+        ipntr[5] = S->iritz + 1;
+        ipntr[6] = S->iq + 1;
+        ipntr[7] = S->ibounds + 1;
+        ipntr[13] = S->iw + 1;
+        if (S->a.attach(2 * (int64_t)n, ncv, reinterpret_cast<double*>(resid),
+                        reinterpret_cast<double*>(v), 2 * ldv, reinterpret_cast<double*>(workd)) != 0 ||
+            zdev::ws_create(S->ws, n, ncv, S->a.stream) != hipSuccess) {
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
+        S->csr = csr;
+        S->tol = *tol;
+        S->iparam = iparam;
+        S->ipntr = ipntr;
+        S->workl = workl;
+        S->rwork = rwork;
+        S->root.emplace(S->run());
+        start_root(*S->root, S->ctx);
+        g_z[v] = std::move(up);
+    } else {
+        auto it = g_z.find(v);
+        if (it == g_z.end()) {
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
+        S = it->second.get();
+        S->tol = *tol;
+        S->iparam = iparam;
+        S->ipntr = ipntr;
+        S->workl = workl;
+        S->rwork = rwork;
+        const RciReq& r = S->ctx.req;
+        if (r.ido == -1 || r.ido == 1 || r.ido == 2) S->a.h2d_workd(2 * r.y, 2 * (int64_t)n);
+    }
+    for (;;) {
+        S->ctx.leaf.resume();
+        if (S->ctx.done) break;
+        const RciReq r = S->ctx.req;
+        if (S->csr && (r.ido == -1 || r.ido == 1)) {
+            zdev::zcsr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            continue;
+        }
+        if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
+            S->a.d2h_workd(2 * r.x, 2 * (int64_t)n);
+            if (r.ido == 1 && r.bx >= 0 && S->mode == 3) S->a.d2h_workd(2 * r.bx, 2 * (int64_t)n);
+            ipntr[0] = (int)(r.x + 1);
+            ipntr[1] = (int)(r.y + 1);
+            if (r.bx >= 0) ipntr[2] = (int)(r.bx + 1);
+        }
+        S->a.sync();
+        *ido = r.ido;
+        return;
+    }
+    *ido = 99;  // SRC/znaupd.f:585-600
+    iparam[2] = S->mxiter;
+    iparam[4] = S->np;
+    iparam[8] = g_stats.nopx;
+    iparam[9] = g_stats.nbx;
+    iparam[10] = g_stats.nrorth;
+    int inf = S->info;
+    if (inf == 2) inf = 3;
+    *info = inf;
+    S->a.download_all();
+    S->a.sync();
+    g_z.erase(v);
+}
+
+// zneupd (SRC/zneupd.f): Schur form of H, ztrsen reordering, V <- V*Qh and
+// Z = V(:,1:nconv) * X (ztrevc eigenvectors of T) on the device.
+static int z_eupd(bool rvec, char howmny, cd* d, cd* z, int ldz, cd sigma, cd* workev, char bmat,
+                  int n, const char* which_s, int nev, double tol, cd* resid, int ncv, cd* v,
+                  int ldv, int* iparam, int* ipntr, cd* workd, cd* workl, int lworkl) {
+    using la::Which;
+    const int mode = iparam[6];
+    int nconv = iparam[4];
+    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const Which which = la::parse_which(which_s);
+    int ierr = 0;
+    if (nconv <= 0) ierr = -14;
+    else if (n <= 0) ierr = -1;
+    else if (nev <= 0) ierr = -2;
+    else if (ncv <= nev || ncv > n) ierr = -3;
+    else if (which != Which::LM && which != Which::SM && which != Which::LR && which != Which::SR &&
+             which != Which::LI && which != Which::SI)
+        ierr = -5;
+    else if (bmat != 'I' && bmat != 'G') ierr = -6;
+    else if (lworkl < 3 * ncv * ncv + 4 * ncv) ierr = -7;
+    else if ((howmny != 'A' && howmny != 'P' && howmny != 'S') && rvec) ierr = -13;
+    else if (howmny == 'S') ierr = -12;
+    enum { REGULR, SHIFTI } type = REGULR;
+    if (mode == 1 || mode == 2) type = REGULR;
+    else if (mode == 3) type = SHIFTI;
+    else ierr = -10;
+    if (mode == 1 && bmat == 'G') ierr = -11;
+    if (ierr != 0) return ierr;
+    // workl layout (SRC/zneupd.f:458-480)
+    const int ih = ipntr[4] - 1, iritz = ipntr[5] - 1, ibounds = ipntr[7] - 1;
+    const int ldh = ncv, ldq = ncv;
+    const int iheig = ibounds + ldh, ihbds = iheig + ldh, iuptri = ihbds + ldh;
+    const int invsub = iuptri + ldh * ncv;
+    ipntr[8] = iheig + 1;
+    ipntr[10] = ihbds + 1;
+    ipntr[11] = iuptri + 1;
+    ipntr[12] = invsub + 1;
+    const int irz = ipntr[13] - 1 + ncv * ncv, ibd = irz + ncv;
+    const double rnorm = workl[ih + 2].real();
+    workl[ih + 2] = 0.0;
+    cd* T = workl + iuptri;
+    cd* Qs = workl + invsub;
+    std::vector<int> sel(ncv, 0);
+    std::vector<cd> Qh, X;
+    if (rvec) {
+        bool reord = false;
+        for (int j = 0; j < ncv; ++j) workl[ibounds + j] = (double)(j + 1);
+        zla::zngets(0, which, nev, ncv - nev, workl + irz, workl + ibounds);
+        int numcnv = 0;
+        for (int j = 1; j <= ncv; ++j) {
+            const cd rz = workl[irz + ncv - j];
+            const double rtemp = std::max(eps23, la::lapy2(rz.real(), rz.imag()));
+            const int jj = (int)workl[ibounds + ncv - j].real();
+            const cd bd = workl[ibd + jj - 1];
+            if (numcnv < nconv && la::lapy2(bd.real(), bd.imag()) <= tol * rtemp) {
+                sel[jj - 1] = 1;
+                ++numcnv;
+                if (jj > nconv) reord = true;
+            }
+        }
+        if (numcnv != nconv) return -15;
+        std::memcpy(static_cast<void*>(T), workl + ih, sizeof(cd) * ldh * ncv);
+        for (int j = 0; j < ncv; ++j)
+            for (int i = 0; i < ncv; ++i) Qs[i + (size_t)j * ldq] = (i == j) ? 1.0 : 0.0;
+        if (zla::lahqr(true, true, ncv, 1, ncv, T, ldh, workl + iheig, 1, ncv, Qs, ldq) != 0) return -8;
+        if (reord) {
+            int nconv2 = 0;
+            zla::trsen(sel.data(), ncv, T, ldh, Qs, ldq, workl + iheig, nconv2);
+            if (nconv2 < nconv) nconv = nconv2;
+        }
+        for (int j = 0; j < ncv; ++j) workl[ihbds + j] = Qs[(ncv - 1) + (size_t)j * ldq];
+        if (type == REGULR) std::memcpy(static_cast<void*>(d), workl + iheig, sizeof(cd) * nconv);
+        std::vector<cd> work(ncv + 1);
+        zla::geqr2(ncv, nconv, Qs, ldq, workev, workev + ncv);
+        Qh.assign((size_t)ncv * ncv, 0.0);
+        for (int j = 0; j < ncv; ++j) Qh[(size_t)j * ncv + j] = 1.0;
+        zla::unm2r_ln(ncv, ncv, nconv, Qs, ldq, workev, Qh.data(), ncv, work.data());
+        for (int j = 0; j < nconv; ++j)
+            if (Qs[j + (size_t)j * ldq].real() < 0.0) {
+                for (int cc = 0; cc < nconv; ++cc) T[j + (size_t)cc * ldq] = -T[j + (size_t)cc * ldq];
+                for (int r = 0; r < nconv; ++r) T[r + (size_t)j * ldq] = -T[r + (size_t)j * ldq];
+            }
+        if (howmny == 'A') {
+            for (int j = 0; j < ncv; ++j) sel[j] = j < nconv;
+            std::vector<cd> tw(2 * ncv);
+            zla::trevc_right('S', sel.data(), ncv, T, ldq, Qs, ldq, tw.data());
+            for (int j = 0; j < nconv; ++j) {
+                cd* cj = Qs + (size_t)j * ldq;
+                const double s = 1.0 / zla::dznrm2(ncv, cj, 1);
+                for (int r = 0; r < ncv; ++r) cj[r] *= s;
+                cd dot = 0.0;  // zzdotc(j, ihbds, 1, col j, 1)
+                for (int r = 0; r <= j; ++r) dot += std::conj(workl[ihbds + r]) * cj[r];
+                workev[j] = dot;
+            }
+            std::memcpy(static_cast<void*>(workl + ihbds), workev, sizeof(cd) * nconv);
+            X.assign((size_t)nconv * nconv, 0.0);  // upper triangular eigenvector block
+            for (int cc = 0; cc < nconv; ++cc)
+                for (int r = 0; r <= cc; ++r) X[r + (size_t)cc * nconv] = Qs[r + (size_t)cc * ldq];
+        }
+    } else {
+        std::memcpy(static_cast<void*>(d), workl + iritz, sizeof(cd) * nconv);
+        std::memcpy(static_cast<void*>(workl + iheig), workl + iritz, sizeof(cd) * nconv);
+        std::memcpy(static_cast<void*>(workl + ihbds), workl + ibounds, sizeof(cd) * nconv);
+    }
+    if (rvec)
+        for (int k = 0; k < ncv; ++k) workl[ihbds + k] *= rnorm;
+    if (type != REGULR) {
+        for (int k = 0; k < ncv; ++k) {
+            const cd t = workl[iheig + k];
+            workl[ihbds + k] = workl[ihbds + k] / t / t;
+        }
+        for (int k = 0; k < nconv; ++k) d[k] = 1.0 / workl[iheig + k] + sigma;
+    }
+    if (!rvec) return 0;
+    std::vector<cd> wpur;
+    if (howmny == 'A' && type == SHIFTI) {
+        wpur.assign(nconv, 0.0);
+        for (int j = 0; j < nconv; ++j)
+            if (workl[iheig + j] != cd(0.0)) wpur[j] = Qs[(ncv - 1) + (size_t)j * ldq] / workl[iheig + j];
+        std::memcpy(static_cast<void*>(workev), wpur.data(), sizeof(cd) * nconv);
+    }
+    // ---- device: V <- V*Qh ; Z = V(:,1:nconv) * X (+ resid w^T)
+    Arrays a;
+    if (a.attach(2 * (int64_t)n, ncv, reinterpret_cast<double*>(resid), reinterpret_cast<double*>(v),
+                 2 * ldv, reinterpret_cast<double*>(workd)) != 0)
+        return -9999;
+    zdev::Ws ws;
+    if (zdev::ws_create(ws, n, ncv, a.stream) != hipSuccess) {
+        a.release();
+        return -9999;
+    }
+    if (a.host_mode) {
+        (void)hipMemcpy2DAsync(a.d_v, sizeof(double) * a.d_ld, v, sizeof(cd) * ldv, sizeof(cd) * n, ncv,
+                               hipMemcpyHostToDevice, a.stream);
+        a.upload_resid();
+    }
+    const int64_t ldc = a.d_ld / 2;
+    zdev::gemm(ws, n, a.d_v, ldc, ncv, ncv, Qh.data(), a.d_v, ldc);
+    const bool zdevp = is_device_pointer(z);
+    double* zd = nullptr;
+    int64_t ldzd = ldc;
+    if (zdevp) {
+        zd = reinterpret_cast<double*>(z);
+        ldzd = ldz;
+    } else {
+        (void)hipMalloc(&zd, sizeof(cd) * (size_t)ldc * nconv);
+    }
+    if (howmny == 'A') {
+        zdev::gemm(ws, n, a.d_v, ldc, nconv, nconv, X.data(), zd, ldzd);
+        if (type == SHIFTI) zdev::ger(ws, n, nconv, a.d_resid, wpur.data(), zd, ldzd);
+    } else if (zd != a.d_v) {
+        (void)hipMemcpy2DAsync(zd, sizeof(cd) * ldzd, a.d_v, sizeof(double) * a.d_ld, sizeof(cd) * n, nconv,
+                               hipMemcpyDeviceToDevice, a.stream);
+    }
+    if (!zdevp) {
+        (void)hipMemcpy2DAsync(z, sizeof(cd) * ldz, zd, sizeof(cd) * ldc, sizeof(cd) * n, nconv,
+                               hipMemcpyDeviceToHost, a.stream);
+    }
+    if (a.host_mode)
+        (void)hipMemcpy2DAsync(v, sizeof(cd) * ldv, a.d_v, sizeof(double) * a.d_ld, sizeof(cd) * n, ncv,
+                               hipMemcpyDeviceToHost, a.stream);
+    a.sync();
+    if (!zdevp) (void)hipFree(zd);
+    zdev::ws_destroy(ws);
+    a.release();
+    return 0;
+}
+
+}  // namespace ahip
+
+// ---------------------------------------------------------------- C-ABI -----
+struct arpack_hip_zcsr {
+    ahip::zdev::ZCsr A;
+};
+
+using ahip::cd;
+
+extern "C" {
+
+void znaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, double tol, a_dcomplex* resid,
+              int ncv, a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl,
+              double* rwork, int* info) {
+    ahip::z_aupd(ido, bmat, n, which, nev, &tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr, (cd*)workd,
+                 (cd*)workl, lworkl, rwork, info, nullptr);
+}
+
+void znaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, double* tol, a_dcomplex* resid,
+             int* ncv, a_dcomplex* v, int* ldv, int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int* lworkl,
+             double* rwork, int* info, size_t, size_t) {
+    ahip::z_aupd(ido, bmat, *n, which, *nev, tol, (cd*)resid, *ncv, (cd*)v, *ldv, iparam, ipntr,
+                 (cd*)workd, (cd*)workl, *lworkl, rwork, info, nullptr);
+}
+
+void zneupd_c(int rvec, char const* howmny, int const* select, a_dcomplex* d, a_dcomplex* z, int ldz, a_dcomplex sigma,
+              a_dcomplex* workev, char const* bmat, int n, char const* which, int nev, double tol, a_dcomplex* resid,
+              int ncv, a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl,
+              double* rwork, int* info) {
+    (void)select;
+    (void)rwork;
+    const cd s(__real__ sigma, __imag__ sigma);
+    *info = ahip::z_eupd(rvec != 0, howmny[0], (cd*)d, (cd*)z, ldz, s, (cd*)workev, bmat[0], n, which, nev,
+                         tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr, (cd*)workd, (cd*)workl, lworkl);
+}
+
+void zneupd_(int* rvec, char const* howmny, int* select, a_dcomplex* d, a_dcomplex* z, int* ldz, a_dcomplex* sigma,
+             a_dcomplex* workev, char const* bmat, int* n, char const* which, int* nev, double* tol, a_dcomplex* resid,
+             int* ncv, a_dcomplex* v, int* ldv, int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int* lworkl,
+             double* rwork, int* info, size_t, size_t, size_t) {
+    (void)select;
+    (void)rwork;
+    const cd s = *reinterpret_cast<const cd*>(sigma);
+    *info = ahip::z_eupd(*rvec != 0, howmny[0], (cd*)d, (cd*)z, *ldz, s, (cd*)workev, bmat[0], *n, which,
+                         *nev, *tol, (cd*)resid, *ncv, (cd*)v, *ldv, iparam, ipntr, (cd*)workd, (cd*)workl,
+                         *lworkl);
+}
+
+// ---- complex host kit exports (CPU-testable; tests/test_kit_z.py) ----
+int arpack_hip_kit_zlahqr(int n, a_dcomplex* h, int ldh, a_dcomplex* w, a_dcomplex* z, int ldz) {
+    return ahip::zla::lahqr(true, true, n, 1, n, (cd*)h, ldh, (cd*)w, 1, n, (cd*)z, ldz);
+}
+int arpack_hip_kit_ztrevc(char howmny, int* select, int n, a_dcomplex* t, int ldt, a_dcomplex* vr,
+                          int ldvr) {
+    std::vector<cd> work(2 * (size_t)n + 1);
+    return ahip::zla::trevc_right(howmny, select, n, (cd*)t, ldt, (cd*)vr, ldvr, work.data());
+}
+int arpack_hip_kit_ztrsen(const int* select, int n, a_dcomplex* t, int ldt, a_dcomplex* q, int ldq,
+                          a_dcomplex* w, int* m) {
+    return ahip::zla::trsen(select, n, (cd*)t, ldt, (cd*)q, ldq, (cd*)w, *m);
+}
+void arpack_hip_kit_zsortc(char const* which, int apply, int n, a_dcomplex* x, a_dcomplex* y) {
+    ahip::zla::zsortc(ahip::la::parse_which(which), apply != 0, n, (cd*)x, (cd*)y);
+}
+void arpack_hip_kit_zngets(int ishift, char const* which, int kev, int np, a_dcomplex* ritz,
+                           a_dcomplex* bounds) {
+    ahip::zla::zngets(ishift, ahip::la::parse_which(which), kev, np, (cd*)ritz, (cd*)bounds);
+}
+int arpack_hip_kit_zneigh(double rnorm, int n, const a_dcomplex* h, int ldh, a_dcomplex* ritz,
+                          a_dcomplex* bounds, a_dcomplex* q, int ldq) {
+    std::vector<cd> wk((size_t)n * n + 2 * (size_t)n + 1);
+    return ahip::zla::zneigh(rnorm, n, (const cd*)h, ldh, (cd*)ritz, (cd*)bounds, (cd*)q, ldq, wk.data());
+}
+void arpack_hip_kit_znapps_host(int kev, int np, const a_dcomplex* shift, a_dcomplex* h, int ldh,
+                                a_dcomplex* q, int ldq, int64_t nglob) {
+    std::vector<cd> wk((size_t)kev + np + 1);
+    ahip::zla::znapps_host(kev, np, (const cd*)shift, (cd*)h, ldh, (cd*)q, ldq, wk.data(), nglob);
+}
+
+int arpack_hip_zcsr_create(arpack_hip_zcsr** out, int64_t n, int64_t nnz, const int64_t* rowptr,
+                           const int32_t* col, const double* val) {
+    auto* Z = new arpack_hip_zcsr;
+    int64_t* rp = nullptr;
+    int32_t* c = nullptr;
+    double* v = nullptr;
+    if (hipMalloc(&rp, sizeof(int64_t) * (n + 1)) || hipMalloc(&c, sizeof(int32_t) * (nnz ? nnz : 1)) ||
+        hipMalloc(&v, sizeof(double) * 2 * (nnz ? nnz : 1))) {
+        delete Z;
+        return -1;
+    }
+    (void)hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault);
+    (void)hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault);
+    (void)hipMemcpy(v, val, sizeof(double) * 2 * nnz, hipMemcpyDefault);
+    Z->A = ahip::zdev::ZCsr{n, nnz, rp, c, v, true};
+    *out = Z;
+    return 0;
+}
+
+int arpack_hip_gen_zrandom(arpack_hip_zcsr** out, int64_t n, int per_row, uint32_t seed, double dshift) {
+    auto* Z = new arpack_hip_zcsr;
+    if (ahip::zdev::gen_zrandom(Z->A, n, per_row, seed, dshift) != 0) {
+        delete Z;
+        return -1;
+    }
+    *out = Z;
+    return 0;
+}
+
+void arpack_hip_zcsr_destroy(arpack_hip_zcsr* Z) {
+    if (!Z) return;
+    if (Z->A.owned) {
+        (void)hipFree((void*)Z->A.rowptr);
+        (void)hipFree((void*)Z->A.col);
+        (void)hipFree((void*)Z->A.val);
+    }
+    delete Z;
+}
+
+int arpack_hip_zcsr_info(const arpack_hip_zcsr* Z, int64_t* n, int64_t* nnz) {
+    *n = Z->A.n;
+    *nnz = Z->A.nnz;
+    return 0;
+}
+
+int arpack_hip_zcsr_download(const arpack_hip_zcsr* Z, int64_t* rowptr, int32_t* col, double* val) {
+    const auto& A = Z->A;
+    if (hipMemcpy(rowptr, A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost) ||
+        hipMemcpy(col, A.col, sizeof(int32_t) * A.nnz, hipMemcpyDeviceToHost) ||
+        hipMemcpy(val, A.val, sizeof(double) * 2 * A.nnz, hipMemcpyDeviceToHost))
+        return -1;
+    return 0;
+}
+
+int arpack_hip_zcsr_spmv(const arpack_hip_zcsr* Z, const double* x, double* y) {
+    ahip::zdev::zcsr_spmv(nullptr, Z->A, x, y);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* Z, int* ido, char const* bmat, int n, char const* which,
+                            int nev, double* tol, a_dcomplex* resid, int ncv, a_dcomplex* v, int ldv, int* iparam,
+                            int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl, double* rwork, int* info) {
+    ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr, (cd*)workd,
+                 (cd*)workl, lworkl, rwork, info, &Z->A);
+}
+
+}  // extern "C"

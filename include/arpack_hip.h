@@ -30,6 +30,11 @@
 #define a_int int /* LP64, arpackdef.h.in:6-14 with INTERFACE64=0 */
 #endif
 
+/* complex128 as the ICB passes it (arpackdef.h.in:40-41): C99 double _Complex */
+#ifndef a_dcomplex
+#define a_dcomplex _Complex double
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -58,6 +63,18 @@ void dneupd_c(a_int rvec, char const* howmny, a_int const* select, double* dr, d
               a_int ncv, double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
               double* workl, a_int lworkl, a_int* info);
 
+/* znaupd_c / zneupd_c (ICB/arpack.h:20-21; SRC/icbazn.F90): complex128 arrays,
+ * lworkl >= 3*ncv^2 + 5*ncv, rwork(ncv), workev(2*ncv). */
+void znaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev, double tol,
+              a_dcomplex* resid, a_int ncv, a_dcomplex* v, a_int ldv, a_int* iparam,
+              a_int* ipntr, a_dcomplex* workd, a_dcomplex* workl, a_int lworkl, double* rwork,
+              a_int* info);
+void zneupd_c(a_int rvec, char const* howmny, a_int const* select, a_dcomplex* d,
+              a_dcomplex* z, a_int ldz, a_dcomplex sigma, a_dcomplex* workev, char const* bmat,
+              a_int n, char const* which, a_int nev, double tol, a_dcomplex* resid, a_int ncv,
+              a_dcomplex* v, a_int ldv, a_int* iparam, a_int* ipntr, a_dcomplex* workd,
+              a_dcomplex* workl, a_int lworkl, double* rwork, a_int* info);
+
 /* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
  *      argument by reference + hidden trailing CHARACTER lengths ---------------- */
 void dsaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
@@ -73,6 +90,16 @@ void dneupd_(a_int* rvec, char const* howmny, a_int* select, double* dr, double*
              a_int* n, char const* which, a_int* nev, double* tol, double* resid, a_int* ncv,
              double* v, a_int* ldv, a_int* iparam, a_int* ipntr, double* workd, double* workl,
              a_int* lworkl, a_int* info, size_t howmny_len, size_t bmat_len, size_t which_len);
+void znaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
+             double* tol, a_dcomplex* resid, a_int* ncv, a_dcomplex* v, a_int* ldv,
+             a_int* iparam, a_int* ipntr, a_dcomplex* workd, a_dcomplex* workl, a_int* lworkl,
+             double* rwork, a_int* info, size_t bmat_len, size_t which_len);
+void zneupd_(a_int* rvec, char const* howmny, a_int* select, a_dcomplex* d, a_dcomplex* z,
+             a_int* ldz, a_dcomplex* sigma, a_dcomplex* workev, char const* bmat, a_int* n,
+             char const* which, a_int* nev, double* tol, a_dcomplex* resid, a_int* ncv,
+             a_dcomplex* v, a_int* ldv, a_int* iparam, a_int* ipntr, a_dcomplex* workd,
+             a_dcomplex* workl, a_int* lworkl, double* rwork, a_int* info, size_t howmny_len,
+             size_t bmat_len, size_t which_len);
 void dseupd_(a_int* rvec, char const* howmny, a_int* select, double* d, double* z,
              a_int* ldz, double* sigma, char const* bmat, a_int* n, char const* which,
              a_int* nev, double* tol, double* resid, a_int* ncv, double* v, a_int* ldv,
@@ -149,6 +176,27 @@ void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_i
                                   double* tol, double* resid, a_int ncv, double* v, a_int ldv,
                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
                                   a_int lworkl, a_int* info);
+
+/* Complex CSR operator (rowptr int64[n+1], col int32[nnz], val complex128[nnz]
+ * interleaved) and the complex random operator of BASELINE config 5 (SURVEY.md
+ * §8d S5: per_row hashed columns, U(-1,1)+iU(-1,1) on a 2^-10 grid, duplicate
+ * columns summed, diagonal += dshift). */
+typedef struct arpack_hip_zcsr arpack_hip_zcsr;
+int arpack_hip_zcsr_create(arpack_hip_zcsr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
+                           const int32_t* col, const double* val);
+int arpack_hip_gen_zrandom(arpack_hip_zcsr** A, int64_t n, int per_row, uint32_t seed,
+                           double dshift);
+void arpack_hip_zcsr_destroy(arpack_hip_zcsr* A);
+int arpack_hip_zcsr_info(const arpack_hip_zcsr* A, int64_t* n, int64_t* nnz);
+int arpack_hip_zcsr_download(const arpack_hip_zcsr* A, int64_t* rowptr, int32_t* col,
+                             double* val);
+int arpack_hip_zcsr_spmv(const arpack_hip_zcsr* A, const double* x, double* y);
+/* znaupd (mode 1) with OP = A served on the GPU; returns with ido = 99. */
+void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* A, a_int* ido, char const* bmat, a_int n,
+                            char const* which, a_int nev, double* tol, a_dcomplex* resid,
+                            a_int ncv, a_dcomplex* v, a_int ldv, a_int* iparam, a_int* ipntr,
+                            a_dcomplex* workd, a_dcomplex* workl, a_int lworkl, double* rwork,
+                            a_int* info);
 
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
@@ -228,6 +276,19 @@ int arpack_hip_kit_dneigh(double rnorm, int n, const double* h, int ldh, double*
                           double* ritzi, double* bounds, double* q, int ldq, double* workl);
 int arpack_hip_kit_dtrsen(const int* select, int n, double* t, int ldt, double* q, int ldq,
                           double* wr, double* wi, int* m); /* job='N', compq='V' */
+/* complex kit (zdense.cpp; tests/test_kit_z.py) */
+int arpack_hip_kit_zlahqr(int n, a_dcomplex* h, int ldh, a_dcomplex* w, a_dcomplex* z, int ldz);
+int arpack_hip_kit_ztrevc(char howmny, int* select, int n, a_dcomplex* t, int ldt, a_dcomplex* vr,
+                          int ldvr);
+int arpack_hip_kit_ztrsen(const int* select, int n, a_dcomplex* t, int ldt, a_dcomplex* q, int ldq,
+                          a_dcomplex* w, int* m);
+void arpack_hip_kit_zsortc(char const* which, int apply, int n, a_dcomplex* x, a_dcomplex* y);
+void arpack_hip_kit_zngets(int ishift, char const* which, int kev, int np, a_dcomplex* ritz,
+                           a_dcomplex* bounds);
+int arpack_hip_kit_zneigh(double rnorm, int n, const a_dcomplex* h, int ldh, a_dcomplex* ritz,
+                          a_dcomplex* bounds, a_dcomplex* q, int ldq);
+void arpack_hip_kit_znapps_host(int kev, int np, const a_dcomplex* shift, a_dcomplex* h, int ldh,
+                                a_dcomplex* q, int ldq, int64_t nglob);
 int arpack_hip_kit_dnapps_host(int kev, int np, const double* shiftr, const double* shifti,
                                double* h, int ldh, double* q, int ldq, double* workl,
                                int64_t nglob);

@@ -136,6 +136,38 @@ def convdiff2d(m, rho):
     return rowptr, c.astype(np.int32), v
 
 
+def zrandom(n, per_row=100, seed=5, dshift=100.0):
+    """Complex random CSR of BASELINE config 5, the numpy twin
+    of arpack_hip_gen_zrandom: row i draws per_row columns hash(seed,i,k) mod n
+    with values U(-1,1)+iU(-1,1) on a 2^-10 grid (duplicates summed -- exact),
+    plus dshift on the diagonal."""
+    sm = _mix32(np.uint64(seed))
+    i = np.repeat(np.arange(n, dtype=np.uint64), per_row)
+    k = np.tile(np.arange(per_row, dtype=np.uint64), n)
+    h = _mix32((_mix32(i ^ sm) + k * np.uint64(0x9E3779B9)) & M32)
+    col = (h % np.uint64(n)).astype(np.int64)
+    re = (_mix32(h ^ np.uint64(0x68E31DA4)) >> np.uint64(21)).astype(np.float64) * 2.0 ** -10 - 1.0
+    im = (_mix32(h ^ np.uint64(0x1B873593)) >> np.uint64(21)).astype(np.float64) * 2.0 ** -10 - 1.0
+    rows = i.astype(np.int64)
+    rows = np.concatenate([rows, np.arange(n, dtype=np.int64)])
+    col = np.concatenate([col, np.arange(n, dtype=np.int64)])
+    val = np.concatenate([re + 1j * im, np.full(n, dshift + 0j)])
+    key = rows * n + col
+    uk, inv = np.unique(key, return_inverse=True)
+    v = np.zeros(len(uk), np.complex128)
+    np.add.at(v, inv, val)
+    r, c = uk // n, uk % n
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(r, minlength=n), out=rowptr[1:])
+    return rowptr, c.astype(np.int32), v
+
+
+def zdiag_icb(n=1000):
+    """TESTS/icb_arpack_c.c:93-96 zMatVec: y_i = (i+1)(1+i) x_i, as CSR."""
+    i = np.arange(n, dtype=np.int64)
+    return np.arange(n + 1, dtype=np.int64), i.astype(np.int32), (i + 1.0) * (1 + 1j)
+
+
 def laplace2d(m, scale=1.0):
     return laplace(m, 2, scale)
 

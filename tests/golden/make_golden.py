@@ -91,6 +91,46 @@ def nonsym_fixtures():
     run_ns("n8_convdiff_capped", cd30, ["convdiff2d", 30, 100.0], 10, 40, "LM", 1e-14, mxiter=4)
 
 
+def run_z(name, mat, spec, nev, ncv, which, tol, mxiter=300, mode=1, sigma=0j, keep_z=True,
+          **extra):
+    """znaupd/zneupd fixture (SRC/znaupd.f, SRC/zneupd.f).  Mode 3 applies
+    OP = inv(A - sigma I) with a sparse LU on the host, as a caller would."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+    rowptr, col, val = mat
+    n = len(rowptr) - 1
+    A = sp.csr_matrix((val, col, rowptr), shape=(n, n))
+    v0 = M.dlarnv_uniform(2 * n)[0].view(np.complex128)
+    if mode == 1:
+        op = lambda x, *_: A @ x  # noqa: E731
+    else:
+        lu = spl.splu((A - sigma * sp.identity(n, format="csr")).tocsc())
+        op = lambda x, *_: lu.solve(x)  # noqa: E731
+    r = ref.znaupd_solve(op, n, nev, ncv, which, tol, v0=v0, mxiter=mxiter, mode=mode,
+                         sigma=sigma, return_state=True)
+    assert r["info"] >= 0, r
+    o = ncv * ncv
+    out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
+               mxiter=mxiter, mode=mode, sigma=sigma, v0=v0, info=r["info"],
+               iparam=r["iparam"], d=r["d"], ritz=r["workl"][o:o + ncv],
+               bounds=r["workl"][o + ncv:o + 2 * ncv], eupd_info=r["eupd_info"])
+    if keep_z:
+        out["z"] = r["z"]
+    out.update(extra)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(name, "info", r["info"], "iparam", r["iparam"][[2, 4, 8, 10]], "d", r["d"][:3])
+    return r
+
+
+def complex_fixtures():
+    run_z("z1_icb_zn", M.zdiag_icb(1000), ["zdiag_icb", 1000], 9, 19, "LM", 1e-6, mxiter=10000)
+    zr = M.zrandom(2000, 20, 5, 100.0)
+    run_z("z2_zrandom_lm", zr, ["zrandom", 2000, 20, 5, 100.0], 6, 20, "LM", 1e-10)
+    run_z("z3_zrandom_si", zr, ["zrandom", 2000, 20, 5, 100.0], 6, 20, "LM", 1e-10, mode=3,
+          sigma=0j)
+    run_z("z4_zrandom_sr", zr, ["zrandom", 2000, 20, 5, 100.0], 5, 20, "SR", 1e-9, mxiter=3000)
+
+
 def g7_dlarnv():
     lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
                                  "scipy.libs", "libscipy_openblas*.so"))[0]
@@ -120,6 +160,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["ns"]:
         nonsym_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["z"]:
+        complex_fixtures()
+        sys.exit(0)
     g7_dlarnv()
     r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
                  keep_z=True)
@@ -143,3 +186,4 @@ if __name__ == "__main__":
     run_sym("g8_banded_capped", M.banded_sym(20000, 1234, 512, 25),
             ["banded_sym", 20000, 1234, 512, 25], 10, 30, "LA", 1e-14, mxiter=5)
     nonsym_fixtures()
+    complex_fixtures()

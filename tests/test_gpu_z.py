@@ -1,0 +1,104 @@
+"""GPU parity of the complex Arnoldi engine (znaupd/zneupd) against the
+reference's golden outputs (tests/golden/z*.npz from oracle/_ref's znaupd_/
+zneupd_ on the same operators and start vectors).
+
+  * z1 is TESTS/icb_arpack_c.c's zn() case (diag (k+1)(1+i), nev 9, ncv 19,
+    tol 1e-6): the reference test's own acceptance (|d - ref| <= 1e-5) and
+    equal iteration counts;
+  * z2-z4 use BASELINE config 5's complex random operator (n = 2000 here), in
+    mode 1 and in shift-invert mode 3 (sigma = 0; the caller solves with a
+    sparse LU, as the reference's zndrv2 does with zgttrs).  The wanted
+    eigenvalues sit in a dense random spectrum, so restart counts are
+    rounding-driven (the reference needs 89-198 cycles): we require the same
+    converged set -- eigenvalues to max(1e-9, 10 tol) relative -- and Ritz
+    residuals ||Az - λz|| / ||A||_1 within 10x the reference's own.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spl
+
+from oracle import matrices as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _mat(spec):
+    if str(spec[0]) == "zdiag_icb":
+        return M.zdiag_icb(int(spec[1]))
+    return M.zrandom(int(spec[1]), int(spec[2]), int(spec[3]), float(spec[4]))
+
+
+def _resid(A, z, d):
+    anorm = abs(A).sum(axis=0).max()
+    return max(np.linalg.norm(A @ z[:, k] - d[k] * z[:, k]) / (anorm * np.linalg.norm(z[:, k]))
+               for k in range(len(d)))
+
+
+def _run_host(pkg, g):
+    rp, col, val = _mat(g["spec"])
+    n = len(rp) - 1
+    A = sp.csr_matrix((val, col, rp), shape=(n, n))
+    mode = int(g["mode"])
+    s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=mode,
+                 mxiter=int(g["mxiter"]), v0=g["v0"])
+    sigma = complex(g["sigma"])
+    lu = spl.splu((A - sigma * sp.identity(n, format="csr")).tocsc()) if mode == 3 else None
+    while True:
+        ido = s.aupd()
+        if ido in (-1, 1):
+            x = s.slice(0)
+            s.slice(1)[:] = A @ x if mode == 1 else lu.solve(x.copy())
+        elif ido == 99:
+            break
+        else:
+            raise AssertionError(ido)
+    return s, A
+
+
+def _check(g, s, A, name):
+    assert int(s.info[0]) == int(g["info"]) == 0
+    nconv = int(s.iparam[4])
+    assert nconv == int(g["iparam"][4])
+    if name == "z1_icb_zn":
+        assert int(s.iparam[2]) == int(g["iparam"][2])
+    d, z, nc = s.eupd(sigma=complex(g["sigma"]))
+    dref = g["d"]
+    tol = max(1e-9, 10 * float(g["tol"])) * np.abs(dref).max()
+    for x in dref:
+        assert np.abs(d - x).min() <= tol, (x, d)
+    if name == "z1_icb_zn":  # the reference test's own check (icb_arpack_c.c:151-160)
+        ref = np.arange(1000 - 8, 1001) * (1 + 1j)
+        for x in ref:
+            assert np.abs(d - x).min() <= 1e-5
+    ours = _resid(A, z, d)
+    theirs = _resid(A, g["z"], dref)
+    assert ours <= max(10 * theirs, 1e-12), (ours, theirs)
+
+
+@pytest.mark.parametrize("name", ["z1_icb_zn", "z2_zrandom_lm", "z3_zrandom_si", "z4_zrandom_sr"])
+def test_znaupd_rci_host_op(pkg, golden, name):
+    g = golden(name)
+    s, A = _run_host(pkg, g)
+    _check(g, s, A, name)
+
+
+@pytest.mark.parametrize("name", ["z1_icb_zn", "z2_zrandom_lm"])
+def test_znaupd_zcsr_free_run(pkg, golden, name):
+    g = golden(name)
+    spec = g["spec"]
+    rp, col, val = _mat(spec)
+    n = len(rp) - 1
+    Ad = pkg.ZCSR.from_arrays(rp, col, val) if str(spec[0]) == "zdiag_icb" else \
+        pkg.ZCSR.random(int(spec[1]), int(spec[2]), int(spec[3]), float(spec[4]))
+    s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
+                 mxiter=int(g["mxiter"]), v0=g["v0"])
+    assert s.aupd_zcsr(Ad) == 99
+    _check(g, s, sp.csr_matrix((val, col, rp), shape=(n, n)), name)
+
+
+def test_zrandom_generator_bitwise(pkg):
+    for n, per, seed in [(2000, 20, 5), (777, 100, 9)]:
+        rp, col, val = M.zrandom(n, per, seed, 100.0)
+        drp, dcol, dval = pkg.ZCSR.random(n, per, seed, 100.0).download()
+        assert np.array_equal(rp, drp) and np.array_equal(col, dcol) and np.array_equal(val, dval)
