@@ -122,6 +122,50 @@ def run_z(name, mat, spec, nev, ncv, which, tol, mxiter=300, mode=1, sigma=0j, k
     return r
 
 
+def mode_fixtures():
+    """Spectral-transformation modes (EXAMPLES/SYM/dsdrv2-6.f, NONSYM/dndrv2-3.f)
+    with the caller operators of tests/modes.py."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import modes
+    n = 400
+    v0, _ = M.dlarnv_uniform(n)
+    cases = [("m2_sym_std_si", "sym", modes.StdShiftInvert("fem1d", n, 0.0), 4, 20, "LM", 0.0),
+             ("m3_sym_gen", "sym", modes.Caller("fem1d", 2, n), 4, 20, "LM", 0.0),
+             ("m4_sym_gen_si", "sym", modes.Caller("fem1d", 3, n, 0.0), 4, 20, "LM", 0.0),
+             ("m5_sym_buckling", "sym", modes.Caller("fem1d", 4, n, 1.0), 4, 20, "LM", 1.0),
+             ("m6_sym_cayley", "sym", modes.Caller("fem1d", 5, n, 150.0), 4, 20, "LM", 150.0),
+             ("m7_ns_std_si", "ns", modes.StdShiftInvert("convdiff1d", n, 1.0), 4, 20, "LM", 1.0),
+             ("m8_ns_gen", "ns", modes.Caller("convdiff1d", 2, n), 4, 20, "LM", 0.0),
+             ("m9_ns_gen_si", "ns", modes.Caller("convdiff1d", 3, n, 1.0), 4, 20, "LM", 1.0)]
+    for name, fam, c, nev, ncv, which, sigma in cases:
+        op = c.op
+        if c.mode == 2:
+            class Op:  # ref.dsaupd_solve reads op.ax for mode 2 (A*x written back over x)
+                def __call__(self, x, k, bx):
+                    return c.op(x, k, bx)
+
+                @property
+                def ax(self):
+                    return c.ax
+            op = Op()
+        if fam == "sym":
+            r = ref.dsaupd_solve(op, n, nev, ncv, which, 1e-10, v0=v0, mxiter=300, mode=c.mode,
+                                 bmat=c.bmat, bop=c.bop, sigma=sigma)
+            out = dict(d=r["d"], z=r["z"])
+        else:
+            r = ref.dnaupd_solve(op, n, nev, ncv, which, 1e-10, v0=v0, mxiter=300, mode=c.mode,
+                                 bmat=c.bmat, bop=c.bop, sigmar=sigma)
+            out = dict(dr=r["dr"], di=r["di"], z=r["z"])
+        assert r["info"] >= 0 and r["eupd_info"] == 0, (name, r["info"], r.get("eupd_info"))
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), family=fam, mode=c.mode,
+                            kind=np.array("fem1d" if "sym" in name else "convdiff1d"), n=n,
+                            nev=nev, ncv=ncv, which=np.array(which), tol=1e-10, sigma=sigma,
+                            v0=v0, info=r["info"], iparam=r["iparam"],
+                            nopx=r["stats"]["nopx"], nbx=r["stats"]["nbx"], **out)
+        print(name, "mode", c.mode, "iparam", r["iparam"][[2, 4, 8, 9, 10]],
+              "d", out.get("d", out.get("dr"))[:4])
+
+
 def complex_fixtures():
     run_z("z1_icb_zn", M.zdiag_icb(1000), ["zdiag_icb", 1000], 9, 19, "LM", 1e-6, mxiter=10000)
     zr = M.zrandom(2000, 20, 5, 100.0)
@@ -160,6 +204,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["ns"]:
         nonsym_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["modes"]:
+        mode_fixtures()
+        sys.exit(0)
     if sys.argv[1:] == ["z"]:
         complex_fixtures()
         sys.exit(0)
@@ -187,3 +234,4 @@ if __name__ == "__main__":
             ["banded_sym", 20000, 1234, 512, 25], 10, 30, "LA", 1e-14, mxiter=5)
     nonsym_fixtures()
     complex_fixtures()
+    mode_fixtures()

@@ -22,8 +22,26 @@ def test_header_symbols_exported(pkg):
 def test_reference_icb_names_covered():
     """Every ICB symbol of the implemented families is declared (ICB/arpack.h:10-21)."""
     names = _declared()
-    for s in ("dsaupd_c", "dseupd_c", "dsaupd_", "dseupd_", "stat_c", "debug_c", "sstats_c"):
+    for s in ("dsaupd_c", "dseupd_c", "dsaupd_", "dseupd_", "dnaupd_c", "dneupd_c", "dnaupd_",
+              "dneupd_", "znaupd_c", "zneupd_c", "znaupd_", "zneupd_", "stat_c", "debug_c",
+              "sstats_c"):
         assert s in names
+
+
+def build_c_drop_in(out):
+    """Compile tests/c/icb_drop_in.c (a C caller written to the reference's ICB
+    contract) against include/arpack_hip.h and link libarpack_hip.so."""
+    import subprocess
+    src = os.path.join(ROOT, "tests", "c", "icb_drop_in.c")
+    lib = os.path.join(ROOT, "arpack-ng_amd")
+    cmd = ["gcc", "-std=c11", "-Wall", "-Werror", "-O1", "-I", os.path.join(ROOT, "include"), src,
+           "-L", lib, "-larpack_hip", "-Wl,-rpath," + lib, "-lm", "-o", out]
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+def test_c_caller_compiles_and_links(pkg, tmp_path):
+    r = build_c_drop_in(str(tmp_path / "icb_drop_in"))
+    assert r.returncode == 0, r.stderr
 
 
 def test_version_and_no_gpu_probe(pkg):
