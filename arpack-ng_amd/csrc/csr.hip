@@ -205,7 +205,7 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
     if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVec;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVecX;
     return A;
 }
 
@@ -265,7 +265,7 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
         A->A.kernel = kernel;
         return 0;
     }
-    if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVec8) {
+    if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVecP4) {
         if (!A->win) return -1;
         A->A.kernel = kernel;
         return 0;
@@ -413,6 +413,6 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     A->win = nullptr;
     A->A.w_nsb = 0;
     A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVec;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVecX;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -130,6 +130,9 @@ enum CsrKernel : int {
     kCsrWVec = 5,
     kCsrWVecNT = 6,
     kCsrWVec8 = 7,
+    kCsrWVecX = 8,  // wvec with the XCD-contiguous superblock order
+    kCsrWVecP3 = 9,  // XCD order, 3 row passes in flight
+    kCsrWVecP4 = 10, // XCD order, 4 row passes in flight
 };
 // Superblock analysis for the LDS x-window kernel; -1 if some row's column
 // span exceeds the window (then the stream kernel is used).  *owned receives

@@ -123,12 +123,32 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double
     double aw = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const double* Vb = V + (int64_t)j0 * ld;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const double ui = u[i];
-        if constexpr (WM == 1) aw += ui * ui;
-        if constexpr (WM == 2) aw += w[i] * ui;
+    // Software-pipelined: the next row's J+1 loads are issued before the
+    // current row is consumed.  Without it the compiler serialises each
+    // load->FMA pair for some J (26..29 here: one load in flight per wave,
+    // 4.1 TB/s measured); the per-thread row order -- hence the rounding -- is
+    // unchanged.
+    constexpr int JL = J > 0 ? J : 1;
+    double cur[JL], cu = 0.0, cw = 0.0;
+    auto load = [&](int64_t r, double (&dst)[JL], double& du, double& dw) {
 #pragma unroll
-        for (int k = 0; k < J; ++k) acc[k] += Vb[i + (int64_t)k * ld] * ui;
+        for (int k = 0; k < J; ++k) dst[k] = Vb[r + (int64_t)k * ld];
+        du = u[r];
+        if constexpr (WM == 2) dw = w[r];
+    };
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) load(i, cur, cu, cw);
+    for (; i < n; i += stride) {
+        double nxt[JL], nu = 0.0, nw = 0.0;
+        if (i + stride < n) load(i + stride, nxt, nu, nw);
+        if constexpr (WM == 1) aw += cu * cu;
+        if constexpr (WM == 2) aw += cw * cu;
+#pragma unroll
+        for (int k = 0; k < J; ++k) acc[k] += cur[k] * cu;
+#pragma unroll
+        for (int k = 0; k < J; ++k) cur[k] = nxt[k];
+        cu = nu;
+        cw = nw;
     }
     constexpr int JJ = J > 0 ? J : 1;
     block_partials<JJ>(acc, J, aw, WM != 0, part, j0, wslot);

@@ -217,7 +217,18 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_window(
 // CW: read the 16-bit window-relative column indices (colw = col - c0 of the
 // superblock, built by the analysis) instead of int32 col: 10 instead of 12
 // bytes per nonzero.
-template <int L, int U, bool NT, bool CW>
+// XCD-aware superblock order: the hardware deals workgroup b to XCD b % 8, so
+// consecutive superblocks (whose x windows overlap by ~80%) would land on
+// different XCDs and fetch their windows from HBM eight times over.  Remap so
+// each XCD walks one contiguous range of superblocks: its 4 MB L2 then serves
+// the overlapping window loads.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    constexpr int64_t X = 8;
+    const int64_t q = nb / X, r = nb % X, x = b % X, i = b / X;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+template <int L, int U, bool NT, bool CW, bool XCD = false>
 __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
     const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
     const int64_t* __restrict__ sb_c0, const int32_t* __restrict__ sb_span,
@@ -228,9 +239,10 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
     double* xw = lds;
     constexpr int RPP = kWinThreads / L;  // rows per pass
     const int t = threadIdx.x, sub = t % L;
-    const int64_t c0 = sb_c0[blockIdx.x];
-    const int span = sb_span[blockIdx.x];
-    const int64_t R0 = tiles[sb_tile0[blockIdx.x]], R1 = tiles[sb_tile0[blockIdx.x + 1]];
+    const int64_t sb = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t c0 = sb_c0[sb];
+    const int span = sb_span[sb];
+    const int64_t R0 = tiles[sb_tile0[sb]], R1 = tiles[sb_tile0[sb + 1]];
     const int64_t npass = (R1 - R0 + RPP - 1) / RPP;
     // Pipeline: row bounds are loaded two passes ahead of the val/col loads,
     // which run two passes ahead of the reduction.
@@ -290,6 +302,70 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
             if (p + 3 < npass) {
                 issue(p + 3, nB, B);
                 nB = bounds(p + 5);
+            }
+        }
+    }
+}
+
+// Same kernel with P row passes in flight (P = 2 is k_csr_wvec's schedule):
+// more outstanding loads per wave to cover HBM latency.
+template <int L, int U, int P, bool XCD>
+__global__ __launch_bounds__(kWinThreads) void k_csr_wvecp(
+    const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
+    const int64_t* __restrict__ sb_c0, const int32_t* __restrict__ sb_span,
+    const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+    const uint16_t* __restrict__ colw, const double* __restrict__ val,
+    const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xw = lds;
+    constexpr int RPP = kWinThreads / L;
+    const int t = threadIdx.x, sub = t % L;
+    const int64_t sb = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t c0 = sb_c0[sb];
+    const int span = sb_span[sb];
+    const int64_t R0 = tiles[sb_tile0[sb]], R1 = tiles[sb_tile0[sb + 1]];
+    const int64_t npass = (R1 - R0 + RPP - 1) / RPP;
+    struct Buf {
+        double v[U];
+        int c[U];
+        int64_t row, b, e;
+    };
+    auto issue = [&](int64_t pass, Buf& B) {
+        B.row = R0 + pass * RPP + t / L;
+        B.b = 0;
+        B.e = 0;
+        if (pass < npass && B.row < R1) {
+            B.b = rp[B.row];
+            B.e = rp[B.row + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = B.b + sub + u * L;
+            const bool in = k < B.e;
+            B.v[u] = in ? val[k] : 0.0;
+            B.c[u] = in ? (int)colw[k] : 0;
+        }
+    };
+    auto finish = [&](Buf& B) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += B.v[u] * xw[B.c[u]];
+        for (int64_t k = B.b + sub + U * L; k < B.e; k += L) s += val[k] * xw[col[k] - c0];
+#pragma unroll
+        for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        if (B.row < R1 && sub == 0) y[B.row] = s;
+    };
+    Buf buf[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) issue(q, buf[q]);
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    __syncthreads();
+    for (int64_t p = 0; p < npass; p += P) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            if (p + q < npass) {
+                finish(buf[q]);
+                if (p + q + P < npass) issue(p + q + P, buf[q]);
             }
         }
     }
@@ -437,16 +513,16 @@ double csr_bytes(const Csr& A) {
     return (cw ? 10.0 : 12.0) * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
 }
 
-template <int L, int U, bool NT, bool CW>
+template <int L, int U, bool NT, bool CW, bool XCD = false>
 static void launch_wvec1(hipStream_t s, const Csr& A, const double* x, double* y) {
     const size_t lds = sizeof(double) * kWinX;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, NT, CW>,
+        (void)hipFuncSetAttribute((const void*)k_csr_wvec<L, U, NT, CW, XCD>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((k_csr_wvec<L, U, NT, CW>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+    hipLaunchKernelGGL((k_csr_wvec<L, U, NT, CW, XCD>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
                        A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.w_colw,
                        A.val, x, y);
 }
@@ -454,13 +530,14 @@ static void launch_wvec1(hipStream_t s, const Csr& A, const double* x, double* y
 template <int L, int U>
 static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y, bool nt) {
     const bool cw = A.w_colw != nullptr && A.kernel != kCsrWVecNT;
-    if (cw) launch_wvec1<L, U, false, true>(s, A, x, y);
+    if (cw && A.kernel == kCsrWVecX) launch_wvec1<L, U, false, true, true>(s, A, x, y);
+    else if (cw) launch_wvec1<L, U, false, true>(s, A, x, y);
     else if (nt) launch_wvec1<L, U, true, false>(s, A, x, y);
     else launch_wvec1<L, U, false, false>(s, A, x, y);
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
-    if ((A.kernel == kCsrWVec || A.kernel == kCsrWVecNT) && A.w_nsb > 0) {
+    if ((A.kernel == kCsrWVec || A.kernel == kCsrWVecNT || A.kernel == kCsrWVecX) && A.w_nsb > 0) {
         const bool nt = A.kernel == kCsrWVecNT;
         const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;
         if (avg <= 6) launch_wvec<4, 2>(s, A, x, y, nt);
@@ -469,6 +546,20 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
         else if (avg <= 60) launch_wvec<16, 4>(s, A, x, y, nt);
         else if (avg <= 120) launch_wvec<32, 4>(s, A, x, y, nt);
         else launch_wvec<64, 4>(s, A, x, y, nt);
+        return;
+    }
+    if ((A.kernel == kCsrWVecP3 || A.kernel == kCsrWVecP4) && A.w_nsb > 0 && A.w_colw) {
+        const size_t lds = sizeof(double) * kWinX;
+        const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.w_sb_tile0, A.w_tiles,
+                               A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.w_colw, A.val, x, y);
+        };
+        const bool p4 = A.kernel == kCsrWVecP4;
+        if (avg <= 28) p4 ? go(k_csr_wvecp<8, 4, 4, true>) : go(k_csr_wvecp<8, 4, 3, true>);
+        else if (avg <= 60) p4 ? go(k_csr_wvecp<16, 4, 4, true>) : go(k_csr_wvecp<16, 4, 3, true>);
+        else p4 ? go(k_csr_wvecp<32, 4, 4, true>) : go(k_csr_wvecp<32, 4, 3, true>);
         return;
     }
     if (A.kernel == kCsrWVec8 && A.w_nsb > 0) {  // fewer lanes per row, more loads per lane

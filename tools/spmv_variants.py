@@ -13,7 +13,9 @@ out = {}
 for name, k, tile in [("vector", 0, 4096), ("stream2048", 1, 2048), ("stream4096", 1, 4096),
                       ("stream2048_nt", 2, 2048), ("stream4096_nt", 2, 4096),
                       ("window", 3, 4096), ("window_nt", 4, 4096), ("wvec", 5, 4096),
-                      ("wvec_nt", 6, 4096), ("wvec8", 7, 4096)]:
+                      ("wvec_nt", 6, 4096), ("wvec8", 7, 4096), ("wvec_xcd", 8, 4096),
+                      ("wvec_p3", 9, 4096), ("wvec_p4", 10, 4096),
+                      ("wvec_again", 5, 4096), ("wvec_xcd_again", 8, 4096)]:
     if name.startswith("wvec"):
         pass
     A.set_kernel(k, tile)
