@@ -509,7 +509,9 @@ int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
 
 double csr_bytes(const Csr& A) {
     // bytes the selected kernel must move: val + column index (+ rowptr, x, y)
-    const bool cw = A.w_colw != nullptr && (A.kernel == kCsrWVec || A.kernel == kCsrWVec8);
+    const bool cw = A.w_colw != nullptr && (A.kernel == kCsrWVec || A.kernel == kCsrWVec8 ||
+                                          A.kernel == kCsrWVecX || A.kernel == kCsrWVecP3 ||
+                                          A.kernel == kCsrWVecP4);
     return (cw ? 10.0 : 12.0) * (double)A.nnz + 8.0 * (double)(A.n + 1) + 16.0 * (double)A.n;
 }
 

@@ -21,4 +21,15 @@ for name, k, tile in [("vector", 0, 4096), ("stream2048", 1, 2048), ("stream4096
     A.set_kernel(k, tile)
     ms = min(A.time_spmv(10) for _ in range(3))
     out[name] = dict(ms=ms, gbs=by / (ms * 1e-3) / 1e9)
+# correctness of every variant against the default kernel's output
+import numpy as np  # noqa: E402
+x = pkg.DeviceBuffer.from_numpy(np.random.default_rng(0).standard_normal(A.n))
+y0, y1 = pkg.DeviceBuffer(A.n), pkg.DeviceBuffer(A.n)
+A.set_kernel(8, 4096)
+A.matvec_device(x.at(0), y0.at(0))
+ref = y0.numpy()
+for name, k in [("wvec", 5), ("wvec_p3", 9), ("wvec_p4", 10), ("window", 3)]:
+    A.set_kernel(k, 4096)
+    A.matvec_device(x.at(0), y1.at(0))
+    out[name]["maxdiff"] = float(np.abs(y1.numpy() - ref).max())
 print(json.dumps(out))
