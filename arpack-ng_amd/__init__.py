@@ -669,6 +669,11 @@ def _declare_dist(L):
     L.arpack_hip_dist_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_int64, C.c_int64]
     L.arpack_hip_dist_destroy.argtypes = [C.c_void_p]
     L.arpack_hip_dist_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int64)] * 4
+    L.arpack_hip_dist_rows.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64, C.c_int64]
+    for f in (L.arpack_hip_pdsaupd_c, L.arpack_hip_pdnaupd_c):
+        f.argtypes = [C.c_void_p, _PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD,
+                      _I, _PI, _PI, _PD, _PD, _I, _PI]
+        f.restype = None
     L.arpack_hip_pdsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p,
                                                 _I, C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI,
                                                 _PI, _PD, _PD, _I, _PI]
@@ -728,6 +733,40 @@ class DistOp:
                 self.h = None
         except Exception:
             pass
+
+
+class DistRows:
+    """This rank's row block [row0, row0 + nloc) of an n_global-row problem with
+    no operator attached: the PARPACK RCI use, where the caller applies OP to its
+    local rows (arpack_hip_dist_rows)."""
+
+    def __init__(self, nloc: int, row0: int, n_global: int):
+        L = lib()
+        _declare_dist(L)
+        h = C.c_void_p()
+        rc = L.arpack_hip_dist_rows(C.byref(h), nloc, row0, n_global)
+        if rc != 0:
+            raise RuntimeError(f"arpack_hip_dist_rows failed ({rc})")
+        self.h = h
+        self.n_global, self.row0, self.nloc = n_global, row0, nloc
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_dist_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def pxaupd(s, D: DistRows) -> int:
+    """One collective pdsaupd_c / pdnaupd_c call (ICB/parpack.h:17-33) on this
+    rank's slice: s is a SymRci or NsRci built with n = local rows."""
+    f = lib().arpack_hip_pdnaupd_c if isinstance(s, NsRci) else lib().arpack_hip_pdsaupd_c
+    f(D.h, _ip(s.ido), s.bmat.encode(), s.n, s.which.encode(), s.nev, s.tol, _ptr(s.resid),
+      s.ncv, _ptr(s.v), s.ldv, _ip(s.iparam), _ip(s.ipntr), _ptr(s.workd), s.workl.ctypes.data,
+      s.lworkl, _ip(s.info))
+    return int(s.ido[0])
 
 
 def pdsaupd_cycles(s: "SymRci", D: DistOp, max_cycles: int) -> int:

@@ -321,6 +321,25 @@ void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
              info, d->A, max_cycles, d);
 }
 
+// PARPACK-style RCI (ICB/parpack.h:17-33 pdsaupd_c / pdnaupd_c): n = LOCAL rows,
+// the communicator is the engine's RCCL one (the decomposition handle from
+// arpack_hip_dist_rows); the caller's OP acts on its rows.  tol by value.
+void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr, -1, ahip_dist_view(D), false);
+}
+
+void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info) {
+    sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr, -1, ahip_dist_view(D), true);
+}
+
 void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }
 
 int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int nclass) {

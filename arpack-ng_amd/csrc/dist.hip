@@ -101,6 +101,21 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     return 0;
 }
 
+// Row-block decomposition without an operator (PARPACK's RCI use: the caller
+// applies OP to its local rows and does its own halo exchange).
+int arpack_hip_dist_rows(arpack_hip_dist** out, int64_t nloc, int64_t row0, int64_t n_global) {
+    using namespace ahip;
+    const Comm* c = comm_get();
+    if (!c || nloc <= 0 || row0 < 0 || row0 + nloc > n_global) return -1;
+    auto* D = new arpack_hip_dist;
+    D->D.n_global = n_global;
+    D->D.row0 = row0;
+    D->D.nloc = nloc;
+    D->D.comm = c;
+    *out = D;
+    return 0;
+}
+
 void arpack_hip_dist_destroy(arpack_hip_dist* D) {
     if (!D) return;
     (void)hipFree(D->D.x_ext);

@@ -244,7 +244,7 @@ Task Solver::saitr(int k, int npk, int& iinfo) {
                 write_state();
             }
             // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
-            double* xop = dist ? dist->x_mid() : (free_run ? vcol(j) : wd + ivj);
+            double* xop = (dist && dist->x_ext) ? dist->x_mid() : (free_run ? vcol(j) : wd + ivj);
             dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
                        bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)

@@ -219,6 +219,22 @@ int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_glo
 void arpack_hip_dist_destroy(arpack_hip_dist* D);
 int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
                          int64_t* send_lo, int64_t* send_hi);
+/* Row-block decomposition without an operator: rank owns rows [row0, row0+nloc)
+ * of the global n_global (collective-free; needs arpack_hip_comm_init). */
+int arpack_hip_dist_rows(arpack_hip_dist** D, int64_t nloc, int64_t row0, int64_t n_global);
+/* PARPACK-style reverse communication (ICB/parpack.h:17-33, pdsaupd_c/pdnaupd_c
+ * with n = LOCAL rows): every rank calls collectively; at ido = -1/1 the caller
+ * applies OP to its local slice (its own halo exchange), as in
+ * PARPACK/EXAMPLES/MPI/pdsdrv1.f.  Post-processing: dseupd_c / dneupd_c on the
+ * local arrays (pdseupd/pdneupd communicate only for bmat = 'G'). */
+void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
+                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
+                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
+                          double* workl, a_int lworkl, a_int* info);
+void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
+                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
+                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
+                          double* workl, a_int lworkl, a_int* info);
 /* Halo plan (host only, CPU-testable): tab = [row0, nloc, min col, max col] per
  * rank (4*P doubles, global indices); out = {halo_lo, halo_hi, send_lo, send_hi}
  * of rank r.  Returns 0, -3 (blocks not contiguous) or -4 (halo too wide). */
