@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
+from functools import partial
 
 import numpy as np
 
@@ -413,18 +414,20 @@ class SymRci:
             return self.workd.at(o)
         return self.workd[o:o + self.n]
 
-    def eupd(self, rvec=True, howmny="A", sigma=0.0, z=None):
+    def eupd(self, rvec=True, howmny="A", sigma=0.0, z=None, dist=None):
+        """dseupd_c, or arpack_hip_pdseupd_c on this rank's rows when `dist`
+        (a DistRows / DistOp) is given."""
         nconv = int(self.iparam[4])
         d = np.zeros(self.nev)
         if z is None:
             z = DeviceBuffer(self.nev * self.n) if self.device else np.zeros(self.nev * self.n)
         select = np.zeros(self.ncv, np.int32)
         info = np.zeros(1, np.int32)
-        lib().dseupd_c(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z),
-                       self.n, sigma, self.bmat.encode(), self.n, self.which.encode(), self.nev,
-                       self.tol, _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
-                       _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
-                       self.lworkl, _ip(info))
+        f = lib().dseupd_c if dist is None else partial(lib().arpack_hip_pdseupd_c, dist.h)
+        f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z), self.n, sigma,
+          self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol, _ptr(self.resid),
+          self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+          self.workl.ctypes.data, self.lworkl, _ip(info))
         if info[0] < 0:
             raise ArpackError("dseupd", int(info[0]))
         return d[:nconv], z, nconv
@@ -479,7 +482,7 @@ class NsRci(SymRci):
             self.tol = float(np.finfo(np.float64).eps / 2)
         return r
 
-    def eupd(self, rvec=True, howmny="A", sigmar=0.0, sigmai=0.0, z=None):
+    def eupd(self, rvec=True, howmny="A", sigmar=0.0, sigmai=0.0, z=None, dist=None):
         """dneupd_c: returns (dr, di, Z, nconv); Z has nev+1 columns (SRC/dneupd.f)."""
         nconv = int(self.iparam[4])
         dr, di = np.zeros(self.nev + 1), np.zeros(self.nev + 1)
@@ -489,12 +492,12 @@ class NsRci(SymRci):
         select = np.zeros(self.ncv, np.int32)
         workev = np.zeros(3 * self.ncv)
         info = np.zeros(1, np.int32)
-        lib().dneupd_c(1 if rvec else 0, howmny.encode(), _ip(select), dr.ctypes.data,
-                       di.ctypes.data, _ptr(z), self.n, sigmar, sigmai, workev.ctypes.data,
-                       self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol,
-                       _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam),
-                       _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data, self.lworkl,
-                       _ip(info))
+        f = lib().dneupd_c if dist is None else partial(lib().arpack_hip_pdneupd_c, dist.h)
+        f(1 if rvec else 0, howmny.encode(), _ip(select), dr.ctypes.data, di.ctypes.data, _ptr(z),
+          self.n, sigmar, sigmai, workev.ctypes.data, self.bmat.encode(), self.n,
+          self.which.encode(), self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
+          self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
+          self.lworkl, _ip(info))
         if info[0] < 0:
             raise ArpackError("dneupd", int(info[0]))
         self.eupd_info = int(info[0])
@@ -674,6 +677,8 @@ def _declare_dist(L):
         f.argtypes = [C.c_void_p, _PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD,
                       _I, _PI, _PI, _PD, _PD, _I, _PI]
         f.restype = None
+    L.arpack_hip_pdseupd_c.argtypes = [C.c_void_p] + L.dseupd_c.argtypes
+    L.arpack_hip_pdneupd_c.argtypes = [C.c_void_p] + L.dneupd_c.argtypes
     L.arpack_hip_pdsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p,
                                                 _I, C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI,
                                                 _PI, _PD, _PD, _I, _PI]

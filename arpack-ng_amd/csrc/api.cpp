@@ -321,7 +321,7 @@ void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
              info, d->A, max_cycles, d);
 }
 
-// PARPACK-style RCI (ICB/parpack.h:17-33 pdsaupd_c / pdnaupd_c): n = LOCAL rows,
+// PARPACK-style RCI (ICB/parpack.h:20 pdsaupd_c, :26 pdnaupd_c): n = LOCAL rows,
 // the communicator is the engine's RCCL one (the decomposition handle from
 // arpack_hip_dist_rows); the caller's OP acts on its rows.  tol by value.
 void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,

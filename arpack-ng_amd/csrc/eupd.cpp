@@ -23,7 +23,7 @@ void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w,
 static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, int ldz,
                     double sigma, char bmat, int n, const char* which_s, int nev, double tol,
                     double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
-                    double* workd, double* workl, int lworkl) {
+                    double* workd, double* workl, int lworkl, const DistOp* dist = nullptr) {
     using la::Which;
     const int mode = iparam[6];
     const int nconv = iparam[4];
@@ -87,9 +87,15 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
         (void)hipMemcpyAsync(a.d_workd, workd, sizeof(double) * n, hipMemcpyHostToDevice, a.stream);
     }
     double bnorm2 = rnorm;
-    if (bmat == 'G') {  // dnrm2(n, workd, 1)
+    if (bmat == 'G') {  // dnrm2(n, workd, 1); pdnorm2 over the ranks (pdseupd.f:456)
         dev::dots(ws, n, 0, a.d_v, a.d_ld, a.d_workd, a.d_workd, -1);
-        dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+        if (dist && dist->comm) {
+            dev::finalize(ws, 1, dev::kFinRaw, 0, 0, -1);
+            comm_allreduce_sum(dist->comm, ws.sums, 1, a.stream);
+            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1, true);
+        } else {
+            dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
+        }
         (void)hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream);
         a.sync();
         bnorm2 = ws.st_host->rnorm;
@@ -232,7 +238,22 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
 
 }  // namespace ahip
 
+const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
+
 extern "C" {
+
+// PARPACK's pdseupd_c (ICB/parpack.h:21): dseupd on this rank's rows; the
+// only collective is the B-norm of B*resid for bmat = 'G' (pdseupd.f:456).
+void arpack_hip_pdseupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, double* d, double* z, int ldz, double sigma,
+                          char const* bmat, int n, char const* which, int nev, double tol,
+                          double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
+                          double* workd, double* workl, int lworkl, int* info) {
+    (void)select;
+    *info = ahip::sym_eupd(rvec != 0, howmny[0], nullptr, d, z, ldz, sigma, bmat[0], n, which, nev,
+                           tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+                           ahip_dist_view(D));
+}
 
 void dseupd_c(int rvec, char const* howmny, int const* select, double* d, double* z, int ldz,
               double sigma, char const* bmat, int n, char const* which, int nev, double tol,

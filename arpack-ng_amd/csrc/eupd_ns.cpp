@@ -291,6 +291,21 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* 
 
 extern "C" {
 
+// PARPACK's pdneupd_c (ICB/parpack.h:27): pdneupd communicates nothing beyond
+// its debug output (PARPACK/SRC/MPI/pdneupd.f), so it is dneupd on this rank's rows.
+void arpack_hip_pdneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, double* dr, double* di, double* z, int ldz,
+                          double sigmar, double sigmai, double* workev, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info) {
+    (void)D;
+    (void)select;
+    *info = ahip::ns_eupd(rvec != 0, howmny[0], nullptr, dr, di, z, ldz, sigmar, sigmai, workev,
+                          bmat[0], n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
+                          workl, lworkl);
+}
+
 void dneupd_c(int rvec, char const* howmny, int const* select, double* dr, double* di, double* z,
               int ldz, double sigmar, double sigmai, double* workev, char const* bmat, int n,
               char const* which, int nev, double tol, double* resid, int ncv, double* v, int ldv,

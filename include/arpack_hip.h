@@ -222,16 +222,28 @@ int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* ha
 /* Row-block decomposition without an operator: rank owns rows [row0, row0+nloc)
  * of the global n_global (collective-free; needs arpack_hip_comm_init). */
 int arpack_hip_dist_rows(arpack_hip_dist** D, int64_t nloc, int64_t row0, int64_t n_global);
-/* PARPACK-style reverse communication (ICB/parpack.h:17-33, pdsaupd_c/pdnaupd_c
+/* PARPACK-style reverse communication (ICB/parpack.h:20 pdsaupd_c, :26 pdnaupd_c
  * with n = LOCAL rows): every rank calls collectively; at ido = -1/1 the caller
  * applies OP to its local slice (its own halo exchange), as in
- * PARPACK/EXAMPLES/MPI/pdsdrv1.f.  Post-processing: dseupd_c / dneupd_c on the
- * local arrays (pdseupd/pdneupd communicate only for bmat = 'G'). */
+ * PARPACK/EXAMPLES/MPI/pdsdrv1.f.  Post-processing: arpack_hip_pdseupd_c
+ * (ICB/parpack.h:21; collective B-norm for bmat = 'G', PARPACK/SRC/MPI/pdseupd.f:456)
+ * and arpack_hip_pdneupd_c (ICB/parpack.h:27; no collective). */
 void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
                           char const* which, a_int nev, double tol, double* resid, a_int ncv,
                           double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
                           double* workl, a_int lworkl, a_int* info);
 void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
+                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
+                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
+                          double* workl, a_int lworkl, a_int* info);
+void arpack_hip_pdseupd_c(const arpack_hip_dist* D, a_int rvec, char const* howmny,
+                          a_int const* select, double* d, double* z, a_int ldz, double sigma,
+                          char const* bmat, a_int n, char const* which, a_int nev, double tol,
+                          double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
+                          a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info);
+void arpack_hip_pdneupd_c(const arpack_hip_dist* D, a_int rvec, char const* howmny,
+                          a_int const* select, double* dr, double* di, double* z, a_int ldz,
+                          double sigmar, double sigmai, double* workev, char const* bmat, a_int n,
                           char const* which, a_int nev, double tol, double* resid, a_int ncv,
                           double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
                           double* workl, a_int lworkl, a_int* info);

@@ -63,7 +63,7 @@ def test_pdsaupd_c_matches_dsaupd_c(pkg, golden, comm1):
     _loop(s2, lambda: pkg.pxaupd(s2, D), op)
     _same(s1, s2)
     assert int(s1.iparam[2]) == int(g["iparam"][2])
-    d, _, nconv = s2.eupd()
+    d, _, nconv = s2.eupd(dist=D)
     np.testing.assert_allclose(np.sort(d), np.sort(g["d"]), rtol=1e-9)
 
 
@@ -82,6 +82,9 @@ def test_pdsaupd_c_generalized_mode3(pkg, golden, comm1):
     _loop(s2, lambda: pkg.pxaupd(s2, D), c.op, c.bop, c.mode)
     _same(s1, s2)
     assert int(s2.iparam[2]) == int(g["iparam"][2])
+    d1, z1, _ = s1.eupd(sigma=float(g["sigma"]))
+    d2, z2, _ = s2.eupd(sigma=float(g["sigma"]), dist=D)
+    assert np.array_equal(d1, d2) and np.array_equal(z1, z2)
 
 
 def test_pdnaupd_c_matches_dnaupd(pkg, golden, comm1):
@@ -100,3 +103,5 @@ def test_pdnaupd_c_matches_dnaupd(pkg, golden, comm1):
     _loop(s2, lambda: pkg.pxaupd(s2, D), op)
     _same(s1, s2)
     assert int(s2.iparam[2]) == int(g["iparam"][2])
+    r1, r2 = s1.eupd(), s2.eupd(dist=D)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
