@@ -682,6 +682,7 @@ def _declare_dist(L):
     L.arpack_hip_pdsaupd_csr_cycles.argtypes = [C.c_void_p, _I, _PI, C.c_char_p, _I, C.c_char_p,
                                                 _I, C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI,
                                                 _PI, _PD, _PD, _I, _PI]
+    L.arpack_hip_pdnaupd_csr_cycles.argtypes = L.arpack_hip_pdsaupd_csr_cycles.argtypes
 
 
 def comm_unique_id() -> bytes:
@@ -699,6 +700,53 @@ def comm_init(nranks: int, rank: int, uid: bytes, device: int = 0):
     _declare_dist(L)
     if L.arpack_hip_comm_init(nranks, rank, C.c_char_p(bytes(uid)), device) != 0:
         raise RuntimeError("ncclCommInitRank failed")
+
+
+_HOST_ALLREDUCE = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int, C.c_void_p)
+_HOST_HALO = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
+                         C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
+                         C.c_void_p)
+_host_cbs = None
+
+
+def comm_init_host(nranks: int, rank: int, device: int = 0):
+    """Engine communicator over the host-staged transport: every allreduce and
+    halo exchange goes through torch.distributed (the default process group,
+    e.g. gloo) instead of RCCL -- for rehearsing several ranks where RCCL
+    cannot run them (more ranks than GPUs).  arpack_hip_comm_init_host."""
+    import torch
+    import torch.distributed as dist
+    global _host_cbs
+
+    def allreduce(buf, count, ctx):
+        a = np.ctypeslib.as_array(buf, (count,))
+        t = torch.from_numpy(a.copy())
+        dist.all_reduce(t)
+        a[:] = t.numpy()
+
+    def halo(slo, nsl, rlo, nrl, shi, nsh, rhi, nrh, ctx):
+        reqs, recv, sent = [], [], []
+        for peer, sp, ns, rp_, nr in ((rank - 1, slo, nsl, rlo, nrl), (rank + 1, shi, nsh, rhi, nrh)):
+            if ns:
+                sent.append(torch.from_numpy(np.ctypeslib.as_array(sp, (ns,)).copy()))
+                reqs.append(dist.isend(sent[-1], peer))
+            if nr:
+                t = torch.empty(nr, dtype=torch.float64)
+                reqs.append(dist.irecv(t, peer))
+                recv.append((rp_, nr, t))
+        for q in reqs:
+            q.wait()
+        for rp_, nr, t in recv:
+            np.ctypeslib.as_array(rp_, (nr,))[:] = t.numpy()
+
+    L = lib()
+    _declare_dist(L)
+    cbs = (_HOST_ALLREDUCE(allreduce), _HOST_HALO(halo))
+    L.arpack_hip_comm_init_host.argtypes = [C.c_int, C.c_int, _HOST_ALLREDUCE, _HOST_HALO,
+                                            C.c_void_p, C.c_int]
+    if L.arpack_hip_comm_init_host(nranks, rank, cbs[0], cbs[1], None, device) != 0:
+        raise RuntimeError("arpack_hip_comm_init_host failed")
+    _host_cbs = cbs  # the C side holds these function pointers
 
 
 def comm_destroy():
@@ -775,11 +823,13 @@ def pxaupd(s, D: DistRows) -> int:
 
 
 def pdsaupd_cycles(s: "SymRci", D: DistOp, max_cycles: int) -> int:
-    """Distributed free-running dsaupd on this rank's slice (s.n = local rows)."""
+    """Distributed free-running dsaupd (dnaupd for an NsRci) on this rank's
+    slice (s.n = local rows)."""
     tol = C.c_double(s.tol)
-    lib().arpack_hip_pdsaupd_csr_cycles(D.h, int(max_cycles), _ip(s.ido), s.bmat.encode(), s.n,
-                                        s.which.encode(), s.nev, C.byref(tol), _ptr(s.resid),
-                                        s.ncv, _ptr(s.v), s.ldv, _ip(s.iparam), _ip(s.ipntr),
-                                        _ptr(s.workd), s.workl.ctypes.data, s.lworkl, _ip(s.info))
+    f = (lib().arpack_hip_pdnaupd_csr_cycles if isinstance(s, NsRci)
+         else lib().arpack_hip_pdsaupd_csr_cycles)
+    f(D.h, int(max_cycles), _ip(s.ido), s.bmat.encode(), s.n, s.which.encode(), s.nev,
+      C.byref(tol), _ptr(s.resid), s.ncv, _ptr(s.v), s.ldv, _ip(s.iparam), _ip(s.ipntr),
+      _ptr(s.workd), s.workl.ctypes.data, s.lworkl, _ip(s.info))
     s.tol = tol.value
     return int(s.ido[0])

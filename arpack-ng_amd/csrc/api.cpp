@@ -321,6 +321,17 @@ void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
              info, d->A, max_cycles, d);
 }
 
+// Nonsymmetric twin (PARPACK/SRC/MPI/pdnaupd.f decomposition).
+void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,
+                                   char const* bmat, int n, char const* which, int nev,
+                                   double* tol, double* resid, int ncv, double* v, int ldv,
+                                   int* iparam, int* ipntr, double* workd, double* workl,
+                                   int lworkl, int* info) {
+    const DistOp* d = ahip_dist_view(D);
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, d->A, max_cycles, d, true);
+}
+
 // PARPACK-style RCI (ICB/parpack.h:20 pdsaupd_c, :26 pdnaupd_c): n = LOCAL rows,
 // the communicator is the engine's RCCL one (the decomposition handle from
 // arpack_hip_dist_rows); the caller's OP acts on its rows.  tol by value.

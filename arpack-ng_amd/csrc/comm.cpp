@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 #include "../../include/arpack_hip.h"
 #include "dist.hpp"
@@ -13,6 +14,12 @@ namespace ahip {
 struct Comm {
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1, device = 0;
+    // host-staged transport (arpack_hip_comm_init_host): the launcher's own
+    // collectives move the scalars and halos through host memory
+    arpack_hip_host_allreduce_fn h_allreduce = nullptr;
+    arpack_hip_host_halo_fn h_halo = nullptr;
+    void* h_ctx = nullptr;
+    std::vector<double> h_buf;
 };
 
 static Comm* g_comm = nullptr;
@@ -22,7 +29,20 @@ int comm_rank(const Comm* c) { return c ? c->rank : 0; }
 int comm_size(const Comm* c) { return c ? c->nranks : 1; }
 
 void comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream) {
-    if (!c || !c->nccl) return;
+    if (!c) return;
+    if (c->h_allreduce) {
+        auto* m = const_cast<Comm*>(c);
+        m->h_buf.resize((size_t)count);
+        (void)hipMemcpyAsync(m->h_buf.data(), dev, sizeof(double) * count, hipMemcpyDeviceToHost,
+                             stream);
+        (void)hipStreamSynchronize(stream);
+        c->h_allreduce(m->h_buf.data(), count, c->h_ctx);
+        (void)hipMemcpyAsync(dev, m->h_buf.data(), sizeof(double) * count, hipMemcpyHostToDevice,
+                             stream);
+        (void)hipStreamSynchronize(stream);
+        return;
+    }
+    if (!c->nccl) return;
     (void)ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, c->nccl, stream);
 }
 
@@ -56,6 +76,22 @@ int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
     return 0;
 }
 
+int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn allreduce,
+                              arpack_hip_host_halo_fn halo, void* ctx, int device) {
+    if (!allreduce || !halo || nranks < 1 || rank < 0 || rank >= nranks) return -1;
+    if (hipSetDevice(device) != hipSuccess) return -2;
+    auto* c = new ahip::Comm;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    c->h_allreduce = allreduce;
+    c->h_halo = halo;
+    c->h_ctx = ctx;
+    if (ahip::g_comm) arpack_hip_comm_destroy();
+    ahip::g_comm = c;
+    return 0;
+}
+
 void arpack_hip_comm_destroy(void) {
     if (!ahip::g_comm) return;
     if (ahip::g_comm->nccl) (void)ncclCommDestroy(ahip::g_comm->nccl);
@@ -77,8 +113,24 @@ int arpack_hip_comm_allreduce(double* dev, int count) {
 namespace ahip {
 
 // Halo exchange of the distributed SpMV (grouped point-to-point over xGMI).
+static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s) {
+    const int r = c->rank, P = c->nranks;
+    const int64_t slo = r > 0 ? D.send_lo : 0, shi = r < P - 1 ? D.send_hi : 0;
+    const int64_t hlo = r > 0 ? D.halo_lo : 0, hhi = r < P - 1 ? D.halo_hi : 0;
+    std::vector<double> b((size_t)(slo + shi + hlo + hhi));
+    double *bsl = b.data(), *bsh = bsl + slo, *brl = bsh + shi, *brh = brl + hlo;
+    if (slo) (void)hipMemcpyAsync(bsl, D.x_mid(), 8 * slo, hipMemcpyDeviceToHost, s);
+    if (shi) (void)hipMemcpyAsync(bsh, D.x_mid() + D.nloc - shi, 8 * shi, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    c->h_halo(bsl, slo, brl, hlo, bsh, shi, brh, hhi, c->h_ctx);
+    if (hlo) (void)hipMemcpyAsync(D.x_ext, brl, 8 * hlo, hipMemcpyHostToDevice, s);
+    if (hhi) (void)hipMemcpyAsync(D.x_mid() + D.nloc, brh, 8 * hhi, hipMemcpyHostToDevice, s);
+    (void)hipStreamSynchronize(s);
+}
+
 void comm_halo(const Comm* c, const DistOp& D, hipStream_t s) {
     if (!c || c->nranks == 1) return;
+    if (c->h_halo) return comm_halo_host(c, D, s);
     const int r = c->rank, P = c->nranks;
     (void)ncclGroupStart();
     if (r > 0) {

@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--ncv", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttc", action="store_true")
+    ap.add_argument("--host-transport", action="store_true",
+                    help="rehearsal only: engine collectives over gloo instead of RCCL, so N ranks "
+                         "can share one GPU (every rank uses device 0)")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
     args = ap.parse_args()
@@ -110,9 +113,12 @@ def main():
         # the data path (allreduce of the Gram-Schmidt sums, SpMV halos) is RCCL.
         import torch.distributed as dist
         dist.init_process_group("gloo")
-        box = [pkg.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        pkg.comm_init(world, rank, box[0], device=local_rank)
+        if args.host_transport:
+            pkg.comm_init_host(world, rank, device=0)
+        else:
+            box = [pkg.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            pkg.comm_init(world, rank, box[0], device=local_rank)
         r0, r1 = pkg.partition_rows(n, world, rank)
     else:
         r0, r1 = 0, n
@@ -222,7 +228,8 @@ def main():
                    "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
                    "which": "LA", "tol": "eps (cycles never converge in the timed window)",
                    "parallelism": "single GPU" if world == 1 else
-                   f"row-block x{world} (RCCL allreduce + halo)"},
+                   f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
+                   f"REHEARSAL row-block x{world} on one GPU, host-staged gloo transport"},
         "lanczos_steps_per_s": nopx / elapsed,
         "time_to_converge": ttc,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -209,6 +209,18 @@ void arpack_hip_comm_destroy(void);
 int arpack_hip_comm_rank(void);
 int arpack_hip_comm_size(void);
 int arpack_hip_comm_allreduce(double* dev, int count); /* in-place SUM (test hook) */
+/* Host-staged transport in place of RCCL: the engine stages every allreduce
+ * (in-place SUM of `count` host doubles) and every halo exchange (send my first
+ * nsl / last nsh local entries to rank-1 / rank+1, receive nrl / nrh entries
+ * from them) through the launcher's own collectives.  For rehearsing P ranks
+ * where RCCL cannot run them (several ranks on one GPU; CI); the data path is
+ * identical to the RCCL one apart from the transport. */
+typedef void (*arpack_hip_host_allreduce_fn)(double* buf, int count, void* ctx);
+typedef void (*arpack_hip_host_halo_fn)(const double* send_lo, int64_t nsl, double* recv_lo,
+                                        int64_t nrl, const double* send_hi, int64_t nsh,
+                                        double* recv_hi, int64_t nrh, void* ctx);
+int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn allreduce,
+                              arpack_hip_host_halo_fn halo, void* ctx, int device);
 
 typedef struct arpack_hip_dist arpack_hip_dist;
 /* Distributed operator from this rank's CSR rows [row0, row0 + A.n) with GLOBAL
@@ -254,6 +266,11 @@ int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out);
 /* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
  * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
 void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
+                                   char const* bmat, a_int n, char const* which, a_int nev,
+                                   double* tol, double* resid, a_int ncv, double* v, a_int ldv,
+                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
+                                   a_int lworkl, a_int* info);
+void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
                                    char const* bmat, a_int n, char const* which, a_int nev,
                                    double* tol, double* resid, a_int ncv, double* v, a_int ldv,
                                    a_int* iparam, a_int* ipntr, double* workd, double* workl,

@@ -1,0 +1,109 @@
+"""One rank of a P-rank rehearsal of the row-block distributed engine
+(PARPACK's decomposition), launched by tests/test_gpu_dist.py with the
+torch.distributed env (RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT).
+
+All ranks share one GPU, so the engine's communicator is the host-staged
+transport (arpack_hip_comm_init_host: allreduce and halo exchange through gloo)
+in place of RCCL -- the data path (local partial sums -> allreduce -> phase
+logic, halo plan + extended-x SpMV, global-offset start vector, row-local V*Q)
+is the one the 8-GPU job runs.
+
+  python tests/dist_worker.py CASE FIXTURE OUTDIR [info0]
+CASE: sym_csr (pdsaupd_csr_cycles), ns_csr (pdnaupd_csr_cycles),
+      sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather).
+Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import GOLDEN, load_pkg  # noqa: E402
+from oracle import matrices as M  # noqa: E402
+
+
+def _mat(spec):
+    kind = str(spec[0])
+    if kind == "banded_sym":
+        return M.banded_sym(int(spec[1]), int(spec[2]), int(spec[3]), int(spec[4]))
+    if kind == "anderson":
+        return M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4]))
+    if kind == "convdiff2d":
+        return M.convdiff2d(int(spec[1]), float(spec[2]))
+    raise KeyError(kind)
+
+
+def main():
+    case, fixture, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    info0 = len(sys.argv) > 4 and sys.argv[4] == "info0"
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    pkg = load_pkg()
+    pkg.comm_init_host(world, rank, device=0)
+    g = dict(np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False))
+    rp, col, val = _mat(g["spec"])
+    n = len(rp) - 1
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    nloc = r1 - r0
+    v0 = None if info0 else g["v0"][r0:r1]
+    ns = case == "ns_csr"
+    cls = pkg.NsRci if ns else pkg.SymRci
+    s = cls(nloc, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
+            mxiter=int(g["mxiter"]), v0=v0, device=(case != "sym_rci"))
+    res = {}
+    if case in ("sym_csr", "ns_csr"):
+        if str(g["spec"][0]) == "banded_sym":  # the device generator's row-range form
+            A = pkg.CSR.banded_sym(n, int(g["spec"][2]), int(g["spec"][3]), int(g["spec"][4]),
+                                   r0, r1)
+            lrp, lcol, lval = A.download()
+            res["gen_ok"] = np.array([np.array_equal(lrp, rp[r0:r1 + 1] - rp[r0]) and
+                                      np.array_equal(lcol, col[rp[r0]:rp[r1]]) and
+                                      np.array_equal(lval, val[rp[r0]:rp[r1]])])
+        else:
+            A = pkg.CSR.from_arrays(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]])
+        D = pkg.DistOp(A, n, r0)
+        res["halo"] = np.array(list(D.info().values()))
+        assert pkg.pdsaupd_cycles(s, D, -1) == 99
+    else:
+        D = pkg.DistRows(nloc, r0, n)
+        Aloc = M.to_scipy(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]], n)
+        while True:
+            ido = pkg.pxaupd(s, D)
+            if ido in (-1, 1):  # gloo all_gather wants equal sizes: pad to the largest block
+                blocks = [pkg.partition_rows(n, world, q) for q in range(world)]
+                m = max(b - a for a, b in blocks)
+                mine = torch.zeros(m, dtype=torch.float64)
+                mine[:nloc] = torch.from_numpy(s.slice(0).copy())
+                parts = [torch.zeros(m, dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(parts, mine)
+                x = np.concatenate([p[:b - a].numpy() for p, (a, b) in zip(parts, blocks)])
+                s.slice(1)[:] = Aloc @ x
+            elif ido == 99:
+                break
+            else:
+                raise AssertionError(ido)
+    if ns:
+        dr, di, z, nconv = s.eupd(dist=D)
+        res.update(d=dr, di=di)
+        ritz = s.ritz
+    else:
+        d, z, nconv = s.eupd(dist=D)
+        res.update(d=d)
+        ritz = s.ritz
+    z = z.numpy() if hasattr(z, "numpy") else z
+    ncols = int(g["nev"]) + (1 if ns else 0)
+    res.update(iparam=s.iparam.copy(), info=s.info.copy(), ritz=np.asarray(ritz),
+               z=z.reshape(ncols, nloc)[:nconv].T.copy(), rows=np.array([r0, r1]))
+    np.savez(os.path.join(out, "rank%d.npz" % rank), **res)
+    dist.barrier()
+    del D
+    pkg.comm_destroy()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

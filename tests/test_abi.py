@@ -9,7 +9,7 @@ from conftest import ROOT
 def _declared():
     txt = open(os.path.join(ROOT, "include", "arpack_hip.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", txt)) -
+    return sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\((?!\s*\*)", txt)) -
                   {"if", "defined", "sizeof"})
 
 

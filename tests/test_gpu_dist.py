@@ -1,0 +1,133 @@
+"""GPU: P-rank rehearsals of the row-block distributed engine (P = 1, 2, 3
+processes sharing the one GPU, tests/dist_worker.py), against the single-GPU
+engine and the reference's golden outputs.
+
+The communicator is the host-staged transport (allreduce + halo exchange over
+gloo) because RCCL refuses two ranks on one device; everything else is the
+multi-GPU data path.  The partial sums of each inner product are combined in a
+different order for each P, so results agree to rounding, not bit for bit:
+  * restart-cycle counts iparam(3) and nconv equal across P and to the reference;
+  * eigenvalues within 1e-10 relative of the reference's (nonsymmetric, non-normal
+    n3: test_gpu_ns's pseudospectrum + selection criterion; cycles within 1);
+  * the Ritz vectors assembled from the ranks' row slices have residuals
+    ||Az - λz|| / (||A||_1 ||z||) <= 1e-8 and equal the P = 1 vectors up to sign;
+  * the device generator's row-range form == rows r0:r1 of the global operator.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import matrices as M
+from test_gpu_ns import _ritz_ok
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(tmp_path, case, fixture, P, info0=False):
+    out = tmp_path / f"{case}_{fixture}_{P}_{int(info0)}"
+    out.mkdir()
+    port = _port()
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        args = [sys.executable, os.path.join(HERE, "dist_worker.py"), case, fixture, str(out)]
+        procs.append(subprocess.Popen(args + (["info0"] if info0 else []), env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=300)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [dict(np.load(out / f"rank{r}.npz")) for r in range(P)]
+
+
+def _z(ranks):
+    return np.concatenate([r["z"] for r in ranks], axis=0)
+
+
+def _resid(A, z, d):
+    anorm = abs(A).sum(axis=0).max()
+    return max(np.linalg.norm(A @ z[:, k] - d[k] * z[:, k]) / (anorm * np.linalg.norm(z[:, k]))
+               for k in range(len(d)))
+
+
+@pytest.mark.parametrize("fixture", ["g4_banded", "g3_anderson3d"])
+def test_sym_csr_ranks(tmp_path, golden, fixture):
+    g = golden(fixture)
+    spec = g["spec"]
+    rp, col, val = (M.banded_sym(*[int(x) for x in spec[1:]]) if str(spec[0]) == "banded_sym"
+                    else M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4])))
+    A = M.to_scipy(rp, col, val)
+    runs = {P: _run(tmp_path, "sym_csr", fixture, P) for P in (1, 2, 3)}
+    z1 = _z(runs[1])
+    for P, ranks in runs.items():
+        for r in ranks:
+            assert int(r["info"][0]) == 0
+            assert int(r["iparam"][2]) == int(g["iparam"][2]), (P, r["iparam"][2])
+            assert int(r["iparam"][4]) == int(g["iparam"][4])
+            np.testing.assert_array_equal(r["d"], ranks[0]["d"])  # replicated host state
+            if "gen_ok" in r:
+                assert bool(r["gen_ok"][0])
+        d = ranks[0]["d"]
+        np.testing.assert_allclose(np.sort(d), np.sort(g["d"]), rtol=1e-10)
+        z = _z(ranks)
+        assert z.shape == (A.shape[0], len(d))
+        assert _resid(A, z, d) <= 1e-8
+        for k in range(len(d)):
+            s = np.sign(z[:, k] @ z1[:, k])
+            np.testing.assert_allclose(s * z[:, k], z1[:, k], atol=1e-7)
+    h = [r["halo"] for r in runs[3]]  # middle rank receives from both sides
+    assert h[1][0] > 0 and h[1][1] > 0 and h[0][0] == 0 and h[2][1] == 0
+
+
+def test_sym_csr_random_start(tmp_path, golden):
+    """info = 0: the dlarnv start vector is drawn at global row offsets, so P
+    ranks see the same v0 as one GPU -- same cycles and values."""
+    r1 = _run(tmp_path, "sym_csr", "g4_banded", 1, info0=True)
+    r2 = _run(tmp_path, "sym_csr", "g4_banded", 2, info0=True)
+    assert int(r1[0]["iparam"][2]) == int(r2[0]["iparam"][2])
+    np.testing.assert_allclose(r2[0]["d"], r1[0]["d"], rtol=1e-12)
+
+
+def test_ns_csr_ranks(tmp_path, golden):
+    g = golden("n3_convdiff_lm")
+    spec = g["spec"]
+    rp, col, val = M.convdiff2d(int(spec[1]), float(spec[2]))
+    A = M.to_scipy(rp, col, val)
+    runs = {P: _run(tmp_path, "ns_csr", "n3_convdiff_lm", P) for P in (1, 3)}
+    ref = g["dr"] + 1j * g["di"]
+    for P, ranks in runs.items():
+        r = ranks[0]
+        assert int(r["info"][0]) == 0 and int(r["iparam"][4]) == int(g["iparam"][4])
+        assert abs(int(r["iparam"][2]) - int(g["iparam"][2])) <= 1
+        # non-normal operator: the pseudospectrum + selection criterion of test_gpu_ns
+        _ritz_ok((rp, col, val), r["d"] + 1j * r["di"], ref, str(g["which"]), float(g["tol"]))
+        assert _z(ranks).shape[0] == A.shape[0]
+
+
+def test_sym_rci_user_op_ranks(tmp_path, golden):
+    """pdsaupd_c (RCI) with the caller's OP on its own rows (x gathered by the
+    caller, as PARPACK/EXAMPLES/MPI/pdsdrv1.f exchanges its slab boundaries)."""
+    g = golden("g4_banded")
+    for P in (2, 3):
+        ranks = _run(tmp_path, "sym_rci", "g4_banded", P)
+        r = ranks[0]
+        assert int(r["info"][0]) == 0 and int(r["iparam"][2]) == int(g["iparam"][2])
+        np.testing.assert_allclose(np.sort(r["d"]), np.sort(g["d"]), rtol=1e-10)
