@@ -86,7 +86,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--rows", "--n", dest="n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=25)
     ap.add_argument("--bandwidth", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=1234)
@@ -210,7 +210,9 @@ def main():
     step_ms = ms + orth_ms
     step_gbs = (by + orth_bytes) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
 
-    traffic, traffic_src = pmc_traffic("k_csr_wvec")
+    # PMC traffic is collected on the default single-GPU workload only
+    traffic, traffic_src = (pmc_traffic("k_csr_wvec") if world == 1 and n == 10_000_000
+                            else (None, None))
     out = {
         "metric": "Arnoldi iters/sec + time-to-converge (nev=10), n=10M CSR; %HBM roofline",
         "value": iters_per_s,
