@@ -127,6 +127,19 @@ def _declare(L):
     L.arpack_hip_kit_dsortr.argtypes = [C.c_char_p, _I, _I, _PD, _PD]
     L.arpack_hip_kit_dsapps_host.argtypes = [_I, _I, _PD, _PD, _I, _PD, _I]
     L.arpack_hip_kit_dlarnv.argtypes = [_PI, _I, _PD]
+    L.arpack_hip_kit_slarnv.argtypes = [_PI, _I, _PD]
+    # single-precision family: the d* signatures with float tol / sigma
+    def _f32(args, idx):
+        a = list(args)
+        for i in idx:
+            a[i] = C.c_float if a[i] is C.c_double else C.POINTER(C.c_float)
+        return a
+    L.ssaupd_c.argtypes = _f32(L.dsaupd_c.argtypes, [5])
+    L.snaupd_c.argtypes = _f32(L.dnaupd_c.argtypes, [5])
+    L.ssaupd_.argtypes = _f32(L.dsaupd_.argtypes, [5])
+    L.snaupd_.argtypes = _f32(L.dnaupd_.argtypes, [5])
+    L.sseupd_c.argtypes = _f32(L.dseupd_c.argtypes, [6, 11])
+    L.sneupd_c.argtypes = _f32(L.dneupd_c.argtypes, [7, 8, 14])
 
 
 def version() -> str:
@@ -334,10 +347,15 @@ class SymRci:
     (torch tensors) so the caller's OP works on device pointers; otherwise
     numpy host arrays (the engine mirrors them in HBM)."""
 
+    _fam = "s"  # dsaupd / ssaupd
+
     def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300,
-                 ishift=1, v0=None, device=False, icb=False):
+                 ishift=1, v0=None, device=False, icb=False, prec="d"):
+        """prec="s": the single-precision family (ssaupd / snaupd): float32 arrays."""
         self.n, self.nev, self.ncv = n, nev, ncv
         self.icb = icb
+        self.prec = prec
+        self.dt = np.float32 if prec == "s" else np.float64
         self.which, self.bmat, self.tol = which, bmat, float(tol)
         self.device = device
         self.ido = np.zeros(1, np.int32)
@@ -348,38 +366,40 @@ class SymRci:
         self.iparam[2] = mxiter
         self.iparam[6] = mode
         self.lworkl = ncv * ncv + 8 * ncv
-        self.workl = np.zeros(self.lworkl)
+        self.workl = np.zeros(self.lworkl, self.dt)
         self.ldv = n
         if device:
-            self.resid = DeviceBuffer(n)
-            self.v = DeviceBuffer(ncv * n)
-            self.workd = DeviceBuffer(3 * n)
+            self.resid = DeviceBuffer(n, self.dt)
+            self.v = DeviceBuffer(ncv * n, self.dt)
+            self.workd = DeviceBuffer(3 * n, self.dt)
             if v0 is not None:
-                self.resid.write(np.asarray(v0, np.float64))
+                self.resid.write(np.asarray(v0, self.dt))
         else:
-            self.resid = np.zeros(n) if v0 is None else np.array(v0, np.float64, copy=True)
-            self.v = np.zeros(ncv * n)
-            self.workd = np.zeros(3 * n)
+            self.resid = np.zeros(n, self.dt) if v0 is None else np.array(v0, self.dt, copy=True)
+            self.v = np.zeros(ncv * n, self.dt)
+            self.workd = np.zeros(3 * n, self.dt)
         self.info[0] = 0 if v0 is None else 1
 
     def aupd(self):
-        """One dsaupd call; returns ido.  Uses the Fortran entry dsaupd_ (tol by
-        reference, so tol <= 0 becomes eps for the rest of the solve exactly as in
-        SRC/dsaupd.f:550) unless icb=True selects dsaupd_c (tol by value on every
-        call, SRC/icbads.F90:14)."""
+        """One dsaupd call (dnaupd for NsRci, s* for prec="s"); returns ido.  Uses
+        the Fortran entry dsaupd_ (tol by reference, so tol <= 0 becomes eps for
+        the rest of the solve exactly as in SRC/dsaupd.f:550) unless icb=True
+        selects dsaupd_c (tol by value on every call, SRC/icbads.F90:14)."""
+        name = self.prec + self._fam + "aupd_"
         if self.icb:
-            lib().dsaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(),
-                           self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
-                           self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
-                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
+            getattr(lib(), name + "c")(
+                _ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol,
+                _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam),
+                _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data, self.lworkl,
+                _ip(self.info))
         else:
-            tol = C.c_double(self.tol)
-            lib().dsaupd_(_ip(self.ido), self.bmat.encode(), C.byref(C.c_int(self.n)),
-                          self.which.encode(), C.byref(C.c_int(self.nev)), C.byref(tol),
-                          _ptr(self.resid), C.byref(C.c_int(self.ncv)), _ptr(self.v),
-                          C.byref(C.c_int(self.ldv)), _ip(self.iparam), _ip(self.ipntr),
-                          _ptr(self.workd), self.workl.ctypes.data, C.byref(C.c_int(self.lworkl)),
-                          _ip(self.info), 1, 2)
+            tol = (C.c_float if self.prec == "s" else C.c_double)(self.tol)
+            getattr(lib(), name)(
+                _ip(self.ido), self.bmat.encode(), C.byref(C.c_int(self.n)), self.which.encode(),
+                C.byref(C.c_int(self.nev)), C.byref(tol), _ptr(self.resid),
+                C.byref(C.c_int(self.ncv)), _ptr(self.v), C.byref(C.c_int(self.ldv)),
+                _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
+                C.byref(C.c_int(self.lworkl)), _ip(self.info), 1, 2)
             self.tol = tol.value
         return int(self.ido[0])
 
@@ -418,12 +438,14 @@ class SymRci:
         """dseupd_c, or arpack_hip_pdseupd_c on this rank's rows when `dist`
         (a DistRows / DistOp) is given."""
         nconv = int(self.iparam[4])
-        d = np.zeros(self.nev)
+        d = np.zeros(self.nev, self.dt)
         if z is None:
-            z = DeviceBuffer(self.nev * self.n) if self.device else np.zeros(self.nev * self.n)
+            m = self.nev * self.n
+            z = DeviceBuffer(m, self.dt) if self.device else np.zeros(m, self.dt)
         select = np.zeros(self.ncv, np.int32)
         info = np.zeros(1, np.int32)
-        f = lib().dseupd_c if dist is None else partial(lib().arpack_hip_pdseupd_c, dist.h)
+        f = (getattr(lib(), self.prec + "seupd_c") if dist is None
+             else partial(lib().arpack_hip_pdseupd_c, dist.h))
         f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z), self.n, sigma,
           self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol, _ptr(self.resid),
           self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
@@ -442,29 +464,15 @@ class NsRci(SymRci):
     """dnaupd state (SRC/dnaupd.f:400-693): like SymRci, with ipntr(14) and
     lworkl = 3*ncv^2 + 6*ncv; Ritz values are complex (ritzr/ritzi)."""
 
+    _fam = "n"  # dnaupd / snaupd
+
     def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300,
-                 ishift=1, v0=None, device=False, icb=False):
-        super().__init__(n, nev, ncv, which, tol, bmat, mode, mxiter, ishift, v0, device, icb)
+                 ishift=1, v0=None, device=False, icb=False, prec="d"):
+        super().__init__(n, nev, ncv, which, tol, bmat, mode, mxiter, ishift, v0, device, icb,
+                         prec)
         self.ipntr = np.zeros(14, np.int32)
         self.lworkl = 3 * ncv * ncv + 6 * ncv
-        self.workl = np.zeros(self.lworkl)
-
-    def aupd(self):
-        if self.icb:
-            lib().dnaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(),
-                           self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
-                           self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
-                           self.workl.ctypes.data, self.lworkl, _ip(self.info))
-        else:
-            tol = C.c_double(self.tol)
-            lib().dnaupd_(_ip(self.ido), self.bmat.encode(), C.byref(C.c_int(self.n)),
-                          self.which.encode(), C.byref(C.c_int(self.nev)), C.byref(tol),
-                          _ptr(self.resid), C.byref(C.c_int(self.ncv)), _ptr(self.v),
-                          C.byref(C.c_int(self.ldv)), _ip(self.iparam), _ip(self.ipntr),
-                          _ptr(self.workd), self.workl.ctypes.data, C.byref(C.c_int(self.lworkl)),
-                          _ip(self.info), 1, 2)
-            self.tol = tol.value
-        return int(self.ido[0])
+        self.workl = np.zeros(self.lworkl, self.dt)
 
     def aupd_cycles(self, A: CSR, max_cycles: int):
         tol = C.c_double(self.tol)
@@ -485,14 +493,15 @@ class NsRci(SymRci):
     def eupd(self, rvec=True, howmny="A", sigmar=0.0, sigmai=0.0, z=None, dist=None):
         """dneupd_c: returns (dr, di, Z, nconv); Z has nev+1 columns (SRC/dneupd.f)."""
         nconv = int(self.iparam[4])
-        dr, di = np.zeros(self.nev + 1), np.zeros(self.nev + 1)
+        dr, di = np.zeros(self.nev + 1, self.dt), np.zeros(self.nev + 1, self.dt)
         if z is None:
             m = (self.nev + 1) * self.n
-            z = DeviceBuffer(m) if self.device else np.zeros(m)
+            z = DeviceBuffer(m, self.dt) if self.device else np.zeros(m, self.dt)
         select = np.zeros(self.ncv, np.int32)
-        workev = np.zeros(3 * self.ncv)
+        workev = np.zeros(3 * self.ncv, self.dt)
         info = np.zeros(1, np.int32)
-        f = lib().dneupd_c if dist is None else partial(lib().arpack_hip_pdneupd_c, dist.h)
+        f = (getattr(lib(), self.prec + "neupd_c") if dist is None
+             else partial(lib().arpack_hip_pdneupd_c, dist.h))
         f(1 if rvec else 0, howmny.encode(), _ip(select), dr.ctypes.data, di.ctypes.data, _ptr(z),
           self.n, sigmar, sigmai, workev.ctypes.data, self.bmat.encode(), self.n,
           self.which.encode(), self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -24,7 +25,12 @@ uint64_t g_dseed = 0;
 static bool g_dseed_init = false;
 static hipStream_t g_stream = nullptr;
 static std::mutex g_mu;
-static std::unordered_map<const void*, std::unique_ptr<Solver>> g_sym;
+// live solves keyed by the caller's V (one registry per storage type)
+template <class R>
+static std::unordered_map<const void*, std::unique_ptr<SolverT<R>>>& registry() {
+    static std::unordered_map<const void*, std::unique_ptr<SolverT<R>>> m;
+    return m;
+}
 
 hipStream_t default_stream() { return g_stream; }
 
@@ -101,13 +107,31 @@ static int ns_check(char bmat, int n, la::Which which, int nev, int ncv, int lwo
 // The *aupd driver shared by dsaupd (ns = false, SRC/dsaupd.f:408-690) and
 // dnaupd (ns = true, SRC/dnaupd.f:400-693): argument checks and workl layout
 // at ido = 0, then resume the solve coroutine until it needs the caller.
+//
+// R = float (ssaupd/snaupd): the n-length data live in fp32; the ncv-sized host
+// work runs in double on a shadow of workl that is copied (rounded) into the
+// caller's float workl at every return, and the user shifts of ido = 3 are read
+// back from it.
+template <class R>
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
-                     double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
-                     double* workd, double* workl, int lworkl, int* info, const dev::Csr* csr,
-                     int max_cycles = -1, const DistOp* dist = nullptr, bool ns = false) {
+                     R* resid, int ncv, R* v, int ldv, int* iparam, int* ipntr, R* workd,
+                     R* workl, int lworkl, int* info, const dev::Csr* csr, int max_cycles = -1,
+                     const DistOp* dist = nullptr, bool ns = false) {
+    constexpr bool kShadow = !std::is_same_v<R, double>;
     if (dist) csr = dist->A;
+    if (kShadow && (dist || csr)) {  // the float family: RCI on one GPU
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
     std::lock_guard<std::mutex> lk(g_mu);
-    Solver* S = nullptr;
+    auto& g_sym = registry<R>();
+    SolverT<R>* S = nullptr;
+    const int wlen = ns ? 3 * ncv * ncv + 6 * ncv : ncv * ncv + 8 * ncv;
+    auto wl_out = [&]() {  // shadow -> caller's workl
+        if constexpr (kShadow)
+            for (int t = 0; t < wlen; ++t) workl[t] = (R)S->wshadow[t];
+    };
     if (*ido == 0) {
         ensure_seed();
         g_stats = Stats{};  // dstats (SRC/dstats.f)
@@ -122,8 +146,8 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             *ido = 99;
             return;
         }
-        if (*tol <= 0.0) *tol = la::kEps;
-        auto up = std::make_unique<Solver>();
+        if (*tol <= 0.0) *tol = Prec<R>::eps;
+        auto up = std::make_unique<SolverT<R>>();
         S = up.get();
         S->bmat = bmat[0];
         S->which = w;
@@ -136,8 +160,13 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->np = ncv - nev;
         S->lworkl = lworkl;
         S->info = *info;
+        double* wl = reinterpret_cast<double*>(workl);
+        if constexpr (kShadow) {
+            S->wshadow.assign((size_t)wlen, 0.0);
+            wl = S->wshadow.data();
+        }
+        std::memset(workl, 0, sizeof(R) * (size_t)wlen);
         if (!ns) {  // workl layout (SRC/dsaupd.f:566-595)
-            std::memset(workl, 0, sizeof(double) * (size_t)(ncv * ncv + 8 * ncv));
             S->ih = 0;
             S->iritz = S->ih + 2 * ncv;
             S->ibounds = S->iritz + ncv;
@@ -150,7 +179,6 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             ipntr[6] = S->ibounds + 1;
             ipntr[10] = S->iw + 1;
         } else {  // workl layout (SRC/dnaupd.f:494-520)
-            std::memset(workl, 0, sizeof(double) * (size_t)(3 * ncv * ncv + 6 * ncv));
             S->arnoldi = true;
             S->ih = 0;
             S->iritz = S->ih + ncv * ncv;
@@ -184,7 +212,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
-        S->workl = workl;
+        S->workl = wl;
         if (ns) S->ws.hld = ncv;
         S->root.emplace(ns ? S->run_ns() : S->run());
         start_root(*S->root, S->ctx);
@@ -200,9 +228,16 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->tol = *tol;  // the ICB passes tol by value on every call (SRC/icbads.F90:14)
         S->iparam = iparam;
         S->ipntr = ipntr;
-        S->workl = workl;
-        // bring the caller's results of the previous request into HBM
         const RciReq& r = S->ctx.req;
+        if constexpr (kShadow) {
+            if (r.ido == 3) {  // the caller's shifts (real parts, then imaginary for dnaupd)
+                const int cnt = (ns ? 2 : 1) * iparam[7];
+                for (int t = 0; t < cnt; ++t) S->wshadow[S->iw + t] = (double)workl[S->iw + t];
+            }
+        } else {
+            S->workl = workl;
+        }
+        // bring the caller's results of the previous request into HBM
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
             S->a.h2d_workd(r.y, n);
             if (r.ido == 1 && S->mode == 2 && !S->arnoldi) S->a.h2d_workd(r.x, n);
@@ -215,12 +250,14 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const RciReq r = S->ctx.req;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             dev::prof_begin(dev::kProfSpmv, S->a.stream);
-            if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
-            else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            if constexpr (!kShadow) {
+                if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
+                else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            }
             dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
             continue;
         }
-        if (r.ido == Solver::kPauseIdo) {  // cycle budget spent: park (no sync)
+        if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park (no sync)
             *ido = r.ido;
             return;
         }
@@ -233,6 +270,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             if (r.bx >= 0) ipntr[2] = (int)(r.bx + 1);
         }
         S->a.sync();
+        wl_out();
         *ido = r.ido;
         return;
     }
@@ -248,6 +286,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
     *info = inf;
     S->a.download_all();
     S->a.sync();
+    wl_out();
     g_sym.erase(v);
 }
 
@@ -276,6 +315,42 @@ void dnaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, do
              double* workl, int* lworkl, int* info, size_t, size_t) {
     sym_aupd(ido, bmat, *n, which, *nev, tol, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl,
              *lworkl, info, nullptr, -1, nullptr, true);
+}
+
+// single-precision family (ICB/arpack.h:16,18; SRC/ssaupd.f, SRC/snaupd.f): fp32
+// n-length data and kernels, tol <= 0 -> slamch('EpsMach')
+void ssaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, float tol,
+              float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr, float* workd,
+              float* workl, int lworkl, int* info) {
+    double t = tol;
+    sym_aupd(ido, bmat, n, which, nev, &t, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr);
+}
+
+void snaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, float tol,
+              float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr, float* workd,
+              float* workl, int lworkl, int* info) {
+    double t = tol;
+    sym_aupd(ido, bmat, n, which, nev, &t, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr, -1, nullptr, true);
+}
+
+void ssaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, float* tol,
+             float* resid, int* ncv, float* v, int* ldv, int* iparam, int* ipntr, float* workd,
+             float* workl, int* lworkl, int* info, size_t, size_t) {
+    double t = *tol;
+    sym_aupd(ido, bmat, *n, which, *nev, &t, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl,
+             *lworkl, info, nullptr);
+    *tol = (float)t;
+}
+
+void snaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, float* tol,
+             float* resid, int* ncv, float* v, int* ldv, int* iparam, int* ipntr, float* workd,
+             float* workl, int* lworkl, int* info, size_t, size_t) {
+    double t = *tol;
+    sym_aupd(ido, bmat, *n, which, *nev, &t, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl,
+             *lworkl, info, nullptr, -1, nullptr, true);
+    *tol = (float)t;
 }
 
 void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* ido,
@@ -436,6 +511,23 @@ void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h,
                                 int ldq) {
     la::dsapps_host(kev, np, shift, h, ldh, q, ldq);
 }
+// The device start-vector generators (dgetv0/sgetv0's dlarnv/slarnv) on a
+// caller device buffer: prec 'd' (double*) or 's' (float*); iseed updated.
+int arpack_hip_larnv_device(char prec, int* iseed, int64_t n, void* x) {
+    dev::Workspace ws;
+    hipStream_t st = nullptr;
+    if (hipStreamCreate(&st) != hipSuccess) return -1;
+    if (dev::ws_create(ws, n, 2, st) != hipSuccess) return -1;
+    const uint64_t s0 = seed48_from_iseed(iseed);
+    const uint64_t s1 = prec == 's' ? dev::larnv_uniform(ws, n, s0, (float*)x)
+                                    : dev::larnv_uniform(ws, n, s0, (double*)x);
+    const int rc = hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+    iseed_from_seed48(s1, iseed);
+    dev::ws_destroy(ws);
+    (void)hipStreamDestroy(st);
+    return rc;
+}
+
 void arpack_hip_kit_dlarnv(int* iseed, int n, double* x) {
     // host reference of the device generator (same arithmetic)
     uint64_t s = seed48_from_iseed(iseed);
@@ -444,6 +536,12 @@ void arpack_hip_kit_dlarnv(int* iseed, int n, double* x) {
         s = (s * a) & mask;
         x[i] = 2.0 * ((double)s * 0x1p-48) - 1.0;
     }
+    iseed_from_seed48(s, iseed);
+}
+
+// host slarnv(idist=2) with slaruv's redraw rule (the device generator's fallback)
+void arpack_hip_kit_slarnv(int* iseed, int n, float* x) {
+    const uint64_t s = dev::slarnv_host(n, seed48_from_iseed(iseed), x);
     iseed_from_seed48(s, iseed);
 }
 

@@ -526,8 +526,8 @@ void dsgets(int ishift, Which which, int kev, int np, double* ritz, double* boun
     }
 }
 
-int dsconv(int n, const double* ritz, const double* bounds, double tol) {
-    const double eps23 = std::pow(kEps, 2.0 / 3.0);
+int dsconv(int n, const double* ritz, const double* bounds, double tol, double eps) {
+    const double eps23 = std::pow(eps, 2.0 / 3.0);
     int nconv = 0;
     for (int i = 0; i < n; ++i) {
         const double temp = std::max(eps23, std::fabs(ritz[i]));

@@ -66,7 +66,7 @@ void dsesrt(Which which, bool apply, int n, double* x, int na, double* a, int ld
 void dsgets(int ishift, Which which, int kev, int np, double* ritz, double* bounds,
             double* shifts);
 // dsconv (SRC/dsconv.f:59-138)
-int dsconv(int n, const double* ritz, const double* bounds, double tol);
+int dsconv(int n, const double* ritz, const double* bounds, double tol, double eps = kEps);
 // dseigt (SRC/dseigt.f:87-181): h(ldh,2), returns ierr
 int dseigt(double rnorm, int n, const double* h, int ldh, double* eig, double* bounds,
            double* workl);
@@ -94,7 +94,8 @@ int trevc_right(char howmny, int* select, int n, const double* t, int ldt, doubl
 void dsortc(Which which, bool apply, int n, double* xr, double* xi, double* y);
 void dngets(int ishift, Which which, int& kev, int& np, double* ritzr, double* ritzi,
             double* bounds);
-int dnconv(int n, const double* ritzr, const double* ritzi, const double* bounds, double tol);
+int dnconv(int n, const double* ritzr, const double* ritzi, const double* bounds, double tol,
+           double eps = kEps);
 int dneigh(double rnorm, int n, const double* h, int ldh, double* ritzr, double* ritzi,
            double* bounds, double* q, int ldq, double* workl);
 int dnapps_host(int kev, int np, const double* shiftr, const double* shifti, double* h, int ldh,

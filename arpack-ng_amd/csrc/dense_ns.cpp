@@ -968,8 +968,9 @@ void dngets(int ishift, Which which, int& kev, int& np, double* ritzr, double* r
 }
 
 // dnconv (SRC/dnconv.f)
-int dnconv(int n, const double* ritzr, const double* ritzi, const double* bounds, double tol) {
-    const double eps23 = std::pow(kEps, 2.0 / 3.0);
+int dnconv(int n, const double* ritzr, const double* ritzi, const double* bounds, double tol,
+           double eps) {
+    const double eps23 = std::pow(eps, 2.0 / 3.0);
     int nconv = 0;
     for (int i = 0; i < n; ++i) {
         const double temp = std::max(eps23, lapy2(ritzr[i], ritzi[i]));

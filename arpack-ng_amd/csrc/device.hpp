@@ -68,37 +68,58 @@ int choose_nblk(int64_t n);
 hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Workspace& ws);
 
+// The n-length launchers are templates over the storage type R of V, resid and
+// workd (double: the d* family; float: the s* family, ICB/arpack.h:10-13).  All
+// reductions and the coefficient vectors (part, sums, coef, q) stay double.
+//
 // v_j = r / rnorm -> V(:,j) (+ optional copies); aborts the cycle if rnorm==0.
-void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double* copy1,
-           double* scale_inplace, int j);
+template <class R>
+void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* scale_inplace, int j);
 // partial sums of [V(:,0:j)' u ; w' u]  (w == u allowed); gate=-1: always,
 // else only if st.dgks == gate.
-void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
-          const double* w, int gate);
+template <class R>
+void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, const R* w,
+          int gate);
 // rout = rin - V(:,0:j) * coef[which]; if spec: partials of [V' rout ; rout' rout]
-void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
-            const double* rin, double* rout, bool spec, int gate);
+template <class R>
+void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
+            R* rout, bool spec, int gate);
 // single-block fixed-order finalize of m = j+1 sums and the phase logic
 // from_sums: the m sums are already in ws.sums (reduced across ranks).
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
               bool from_sums = false);
 // resid = 0 if st.zero
-void zero_if(const Workspace& ws, int64_t n, double* r);
+template <class R>
+void zero_if(const Workspace& ws, int64_t n, R* r);
 // V(:,0:kev) = V(:,0:kplusp) * Q(:,0:kev) in place (row-local) and
 // r = sigmak*r + betak*Vnew(:,kev); partial r'r for the new rnorm.
-void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp, int kev,
-               double sigmak, double betak, double* r);
+template <class R>
+void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int kev,
+               double sigmak, double betak, R* r);
 // Z(:,0:nz) = V(:,0:k) * M(k x nz) (M in ws.q, ld k); Z may alias V.
-void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k, int nz,
-             double* Z, int64_t ldz);
-// dlarnv(idist=2) continuation: x[m] = 2*(seed*a^(m+1) mod 2^48)/2^48 - 1
-// offset: global index of x[0] in the stream (row-block sharding)
-void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x, int64_t offset = 0);
-void copy(hipStream_t s, int64_t n, const double* src, double* dst);
-void scal(hipStream_t s, int64_t n, double a, double* x);
-void fill(hipStream_t s, int64_t n, double a, double* x);
+template <class R>
+void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int nz, R* Z,
+             int64_t ldz);
+// dlarnv / slarnv(idist=2) continuation: x[m] = 2*u(seed*a^(m+1) mod 2^48) - 1;
+// offset: global index of x[0] in the stream (row-block sharding).  Returns the
+// advanced 48-bit seed (seed*a^n unless slaruv's float redraw rule fired).
+uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,
+                       int64_t offset = 0);
+uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x,
+                       int64_t offset = 0);
+uint64_t slarnv_host(int64_t n, uint64_t seed48, float* x);
+template <class R>
+void copy(hipStream_t s, int64_t n, const R* src, R* dst);
+template <class R>
+void scal(hipStream_t s, int64_t n, double a, R* x);
+template <class R>
+void fill(hipStream_t s, int64_t n, double a, R* x);
 // y = alpha*y + beta*x
-void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const double* x);
+template <class R>
+void axpby(hipStream_t s, int64_t n, double alpha, R* y, double beta, const R* x);
+// Z(:,l) += x * w[l], l < k (dseupd purification)
+template <class R>
+void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z, int64_t ldz);
 
 // ------------------------------- CSR operator --------------------------------
 struct Csr {

@@ -3,9 +3,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <cstdint>
 #include <memory>
 #include <optional>
+#include <vector>
 
 #include "dense.hpp"
 #include "device.hpp"
@@ -31,30 +33,46 @@ void ahip_ensure_seed();  // iseed = (1,3,5,7) once per process
 
 // Caller-visible arrays in one place. `dev_*` are what the kernels use: the
 // caller's own buffers in device-pointer mode, engine-owned mirrors in
-// host-pointer mode.
-struct Arrays {
+// host-pointer mode.  R is the storage type (double: d*, float: s*).
+template <class R>
+struct ArraysT {
     bool host_mode = true;
     int64_t n = 0;
     int ncv = 0;
-    double* h_resid = nullptr;
-    double* h_v = nullptr;
+    R* h_resid = nullptr;
+    R* h_v = nullptr;
     int h_ldv = 0;
-    double* h_workd = nullptr;
-    double* d_resid = nullptr;
-    double* d_v = nullptr;
+    R* h_workd = nullptr;
+    R* d_resid = nullptr;
+    R* d_v = nullptr;
     int64_t d_ld = 0;
-    double* d_workd = nullptr;
+    R* d_workd = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
 
     // fails with a negative code if pointer kinds are mixed
-    int attach(int64_t n, int ncv, double* resid, double* v, int ldv, double* workd);
+    int attach(int64_t n, int ncv, R* resid, R* v, int ldv, R* workd);
     void release();
     void upload_resid();
     void download_all();           // V, resid, workd -> caller (host mode)
     void d2h_workd(int64_t off, int64_t len);
     void h2d_workd(int64_t off, int64_t len);
     void sync();
+};
+using Arrays = ArraysT<double>;
+
+// dlamch / slamch constants of a family (SRC/dsaupd.f:550, SRC/ssaupd.f:550)
+template <class R>
+struct Prec;
+template <>
+struct Prec<double> {
+    static constexpr double eps = DBL_EPSILON * 0.5;  // dlamch('E')
+    static constexpr double safmin = DBL_MIN;         // dlamch('S')
+};
+template <>
+struct Prec<float> {
+    static constexpr double eps = FLT_EPSILON * 0.5;  // slamch('E')
+    static constexpr double safmin = FLT_MIN;         // slamch('S')
 };
 
 bool is_device_pointer(const void* p);
@@ -63,8 +81,11 @@ hipStream_t default_stream();  // set through arpack_hip_set_stream()
 // One implicitly restarted Krylov solve: symmetric Lanczos (dsaupd family,
 // sym.cpp) or nonsymmetric Arnoldi (dnaupd family, ns.cpp).  The n-length
 // step machinery (getv0, the Lanczos/Arnoldi step with CGS + DGKS, V*Q) is
-// shared; only the ncv-sized host work differs.
-class Solver {
+// shared; only the ncv-sized host work differs.  R is the storage type of the
+// n-length data (double: dsaupd/dnaupd, float: ssaupd/snaupd); the ncv-sized
+// host work is done in double in both (workl is a double shadow for float).
+template <class R>
+class SolverT {
 public:
     // configuration fixed at ido == 0 (SRC/dsaupd.f:473-596)
     char bmat = 'I';
@@ -79,7 +100,7 @@ public:
     double* workl = nullptr;   // host view of the caller's workl
     int info = 0;
 
-    Arrays a;
+    ArraysT<R> a;
     dev::Workspace ws;
     RciCtx ctx;
     std::optional<Task> root;
@@ -104,8 +125,12 @@ public:
     // workl offsets (0-based) of h, ritz (ritzr), ritzi, bounds, q, w
     int ih = 0, iritz = 0, iritzi = 0, ibounds = 0, iq = 0, iw = 0;
     double rnorm = 0.0;  // host copy of dsaup2's rnorm
+    // machine constants of the family (convergence tests, tol <= 0 default)
+    double eps = Prec<R>::eps, safmin = Prec<R>::safmin;
+    // float family: the double shadow of the caller's workl (workl points here)
+    std::vector<double> wshadow;
 
-    ~Solver();
+    ~SolverT();
     Task run();     // dsaup2
     Task run_ns();  // dnaup2
 
@@ -115,14 +140,16 @@ private:
     void sapps(int kev, int npk);
     void vq_device(int kev, int kplusp, double sigmak, double betak);
     RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
-    RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp);
+    RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const R* xp, R* yp);
     void read_state();
     void write_state();
     void fin(int m, dev::FinPhase ph, int j, int rstart, int gate);
-    double* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
+    R* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
+    R* dist_x();  // the distributed operator's x window (double only)
 public:
-    const double* op_x = nullptr;  // device pointers of the pending OP request
-    double* op_y = nullptr;
+    const R* op_x = nullptr;  // device pointers of the pending OP request
+    R* op_y = nullptr;
 };
+using Solver = SolverT<double>;
 
 }  // namespace ahip

@@ -8,6 +8,7 @@
 // purification Z += resid * w' for the spectral-transform modes (:840-857).
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/arpack_hip.h"
@@ -15,16 +16,35 @@
 
 namespace ahip {
 
-namespace dev {
-void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
-              int64_t ldz);
-}
-
-static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, int ldz,
-                    double sigma, char bmat, int n, const char* which_s, int nev, double tol,
-                    double* resid, int ncv, double* v, int ldv, int* iparam, int* ipntr,
-                    double* workd, double* workl, int lworkl, const DistOp* dist = nullptr) {
+// R = float (sseupd): the ncv-sized work runs in double on a shadow of the
+// caller's float workl (copied back, rounded, on return), d is rounded at the end.
+template <class R>
+static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz, double sigma,
+                    char bmat, int n, const char* which_s, int nev, double tol, R* resid, int ncv,
+                    R* v, int ldv, int* iparam, int* ipntr, R* workd, R* workl_in, int lworkl,
+                    const DistOp* dist = nullptr) {
     using la::Which;
+    constexpr bool kShadow = !std::is_same_v<R, double>;
+    std::vector<double> wsh, dsh;
+    double* workl = reinterpret_cast<double*>(workl_in);
+    double* d = reinterpret_cast<double*>(d_out);
+    if constexpr (kShadow) {
+        wsh.assign(workl_in, workl_in + (lworkl > 0 ? lworkl : 0));
+        dsh.assign((size_t)(nev > 0 ? nev : 0) + 1, 0.0);
+        workl = wsh.data();
+        d = dsh.data();
+    }
+    struct Back {  // float family: results back into the caller's arrays
+        std::vector<double>&wsh, &dsh;
+        R *workl_in, *d_out;
+        int nd;
+        ~Back() {
+            if constexpr (kShadow) {
+                for (size_t t = 0; t < wsh.size(); ++t) workl_in[t] = (R)wsh[t];
+                for (int t = 0; t < nd && t < (int)dsh.size(); ++t) d_out[t] = (R)dsh[t];
+            }
+        }
+    } back{wsh, dsh, workl_in, d_out, iparam[4]};
     const int mode = iparam[6];
     const int nconv = iparam[4];
     if (nconv == 0) return 0;
@@ -61,11 +81,11 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
     ipntr[8] = ihb + 1;
     ipntr[9] = iq + 1;
     const int irz = ipntr[10] - 1 + ncv, ibd = irz + ncv;
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(Prec<R>::eps, 2.0 / 3.0);
     const double rnorm = workl[ih];
 
     // device context (V, resid, workd may be host or device memory)
-    Arrays a;
+    ArraysT<R> a;
     if (a.attach(n, ncv, resid, v, ldv, workd) != 0) return -9999;
     dev::Workspace ws;
     if (dev::ws_create(ws, n, ncv, a.stream) != hipSuccess) {
@@ -73,7 +93,7 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
         return -9999;
     }
     struct Guard {
-        Arrays& a;
+        ArraysT<R>& a;
         dev::Workspace& ws;
         ~Guard() {
             dev::ws_destroy(ws);
@@ -81,10 +101,10 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
         }
     } guard{a, ws};
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(double) * a.d_ld, v, sizeof(double) * ldv,
-                               sizeof(double) * n, ncv, hipMemcpyHostToDevice, a.stream);
+        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
+                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream);
         a.upload_resid();
-        (void)hipMemcpyAsync(a.d_workd, workd, sizeof(double) * n, hipMemcpyHostToDevice, a.stream);
+        (void)hipMemcpyAsync(a.d_workd, workd, sizeof(R) * n, hipMemcpyHostToDevice, a.stream);
     }
     double bnorm2 = rnorm;
     if (bmat == 'G') {  // dnrm2(n, workd, 1); pdnorm2 over the ranks (pdseupd.f:456)
@@ -206,16 +226,16 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
     }
     if (rvec && howmny == 'A') {
         // Z := V(:,1:nconv) (+ resid * w' purification for the transform modes)
-        double* zd = nullptr;
+        R* zd = nullptr;
         int64_t ldzd = a.d_ld;
         if (zdev) {
             zd = z;
             ldzd = ldz;
-            (void)hipMemcpy2DAsync(zd, sizeof(double) * ldz, a.d_v, sizeof(double) * a.d_ld,
-                                   sizeof(double) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
+            (void)hipMemcpy2DAsync(zd, sizeof(R) * ldz, a.d_v, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
         } else {
-            (void)hipMallocAsync(&zd, sizeof(double) * (size_t)a.d_ld * nconv, a.stream);
-            (void)hipMemcpyAsync(zd, a.d_v, sizeof(double) * (size_t)a.d_ld * nconv,
+            (void)hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream);
+            (void)hipMemcpyAsync(zd, a.d_v, sizeof(R) * (size_t)a.d_ld * nconv,
                                  hipMemcpyDeviceToDevice, a.stream);
         }
         if (type != REGULR) {
@@ -224,13 +244,13 @@ static int sym_eupd(int rvec, char howmny, int* select, double* d, double* z, in
             dev::ger_cols(a.stream, n, nconv, a.d_resid, ws.coef, zd, ldzd);
         }
         if (!zdev) {
-            (void)hipMemcpy2DAsync(z, sizeof(double) * ldz, zd, sizeof(double) * a.d_ld,
-                                   sizeof(double) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+            (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
             (void)hipFreeAsync(zd, a.stream);
         }
         if (a.host_mode)  // the reference leaves V * Q in V (dorm2r in place)
-            (void)hipMemcpy2DAsync(v, sizeof(double) * ldv, a.d_v, sizeof(double) * a.d_ld,
-                                   sizeof(double) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+            (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
         a.sync();
     }
     return 0;
@@ -268,6 +288,24 @@ void dseupd_(int* rvec, char const* howmny, int* select, double* d, double* z, i
              double* sigma, char const* bmat, int* n, char const* which, int* nev, double* tol,
              double* resid, int* ncv, double* v, int* ldv, int* iparam, int* ipntr, double* workd,
              double* workl, int* lworkl, int* info, size_t, size_t, size_t) {
+    *info = ahip::sym_eupd(*rvec != 0, howmny[0], select, d, z, *ldz, *sigma, bmat[0], *n, which,
+                           *nev, *tol, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl, *lworkl);
+}
+
+// single-precision family (ICB/arpack.h:19; SRC/sseupd.f)
+void sseupd_c(int rvec, char const* howmny, int const* select, float* d, float* z, int ldz,
+              float sigma, char const* bmat, int n, char const* which, int nev, float tol,
+              float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr, float* workd,
+              float* workl, int lworkl, int* info) {
+    (void)select;
+    *info = ahip::sym_eupd(rvec != 0, howmny[0], nullptr, d, z, ldz, sigma, bmat[0], n, which, nev,
+                           tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl);
+}
+
+void sseupd_(int* rvec, char const* howmny, int* select, float* d, float* z, int* ldz,
+             float* sigma, char const* bmat, int* n, char const* which, int* nev, float* tol,
+             float* resid, int* ncv, float* v, int* ldv, int* iparam, int* ipntr, float* workd,
+             float* workl, int* lworkl, int* info, size_t, size_t, size_t) {
     *info = ahip::sym_eupd(*rvec != 0, howmny[0], select, d, z, *ldz, *sigma, bmat[0], *n, which,
                            *nev, *tol, resid, *ncv, v, *ldv, iparam, ipntr, workd, workl, *lworkl);
 }

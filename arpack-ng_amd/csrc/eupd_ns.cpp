@@ -10,6 +10,7 @@
 // rank-1 purification Z += resid * w' in shift-invert mode (:1019-1059).
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/arpack_hip.h"
@@ -17,19 +18,42 @@
 
 namespace ahip {
 
-namespace dev {
-void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
-              int64_t ldz);
-}
-
-static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* di, double* z,
-                   int ldz, double sigmar, double sigmai, double* workev, char bmat, int n,
-                   const char* which_s, int nev, double tol, double* resid, int ncv, double* v,
-                   int ldv, int* iparam, int* ipntr, double* workd, double* workl, int lworkl) {
+// R = float (sneupd): ncv-sized work in double on shadows of workl, dr, di and
+// workev, rounded back into the caller's arrays on return.
+template <class R>
+static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out, R* z, int ldz,
+                   double sigmar, double sigmai, R* workev_out, char bmat, int n,
+                   const char* which_s, int nev, double tol, R* resid, int ncv, R* v, int ldv,
+                   int* iparam, int* ipntr, R* workd, R* workl_in, int lworkl) {
     using la::Which;
+    constexpr bool kShadow = !std::is_same_v<R, double>;
+    double* workl = reinterpret_cast<double*>(workl_in);
+    double* dr = reinterpret_cast<double*>(dr_out);
+    double* di = reinterpret_cast<double*>(di_out);
+    double* workev = reinterpret_cast<double*>(workev_out);
+    std::vector<double> sh[4];  // workl, dr, di, workev
+    if constexpr (kShadow) {
+        sh[0].assign(workl_in, workl_in + (lworkl > 0 ? lworkl : 0));
+        sh[1].assign((size_t)(nev > 0 ? nev : 0) + 1, 0.0);
+        sh[2].assign((size_t)(nev > 0 ? nev : 0) + 1, 0.0);
+        sh[3].assign(3 * (size_t)(ncv > 0 ? ncv : 0), 0.0);
+        workl = sh[0].data();
+        dr = sh[1].data();
+        di = sh[2].data();
+        workev = sh[3].data();
+    }
+    struct Back {
+        std::vector<double>* sh;
+        R* out[4];
+        ~Back() {
+            if constexpr (kShadow)
+                for (int k = 0; k < 4; ++k)
+                    for (size_t t = 0; t < sh[k].size(); ++t) out[k][t] = (R)sh[k][t];
+        }
+    } back{sh, {workl_in, dr_out, di_out, workev_out}};
     const int mode = iparam[6];
     int nconv = iparam[4];
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(Prec<R>::eps, 2.0 / 3.0);
     const Which which = la::parse_which(which_s);
     int ierr = 0;
     if (nconv <= 0) ierr = -14;
@@ -230,7 +254,7 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* 
     }
 
     // ---- device part: V <- V*Qh, Z = V(:,1:nconv)*M2 (+ resid w')
-    Arrays a;
+    ArraysT<R> a;
     if (a.attach(n, ncv, resid, v, ldv, workd) != 0) return -9999;
     dev::Workspace ws;
     if (dev::ws_create(ws, n, ncv, a.stream) != hipSuccess) {
@@ -238,7 +262,7 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* 
         return -9999;
     }
     struct Guard {
-        Arrays& a;
+        ArraysT<R>& a;
         dev::Workspace& ws;
         ~Guard() {
             dev::ws_destroy(ws);
@@ -246,20 +270,20 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* 
         }
     } guard{a, ws};
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(double) * a.d_ld, v, sizeof(double) * ldv,
-                               sizeof(double) * n, ncv, hipMemcpyHostToDevice, a.stream);
+        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
+                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream);
         a.upload_resid();
     }
     (void)hipMemcpyAsync(ws.q, Qh.data(), sizeof(double) * Qh.size(), hipMemcpyHostToDevice, a.stream);
     dev::vq_gemm(ws, n, a.d_v, a.d_ld, ncv, ncv, a.d_v, a.d_ld);
     const bool zdev = is_device_pointer(z);
-    double* zd = nullptr;
+    R* zd = nullptr;
     int64_t ldzd = a.d_ld;
     if (zdev) {
         zd = z;
         ldzd = ldz;
     } else {
-        (void)hipMallocAsync(&zd, sizeof(double) * (size_t)a.d_ld * nconv, a.stream);
+        (void)hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream);
     }
     if (howmny == 'A') {
         a.sync();  // ws.q (Qh) consumed before it is overwritten
@@ -272,17 +296,17 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, double* dr, double* 
             dev::ger_cols(a.stream, n, nconv, a.d_resid, ws.coef, zd, ldzd);
         }
     } else if (zd != a.d_v) {  // 'P': Z = the Schur vectors
-        (void)hipMemcpy2DAsync(zd, sizeof(double) * ldzd, a.d_v, sizeof(double) * a.d_ld,
-                               sizeof(double) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
+        (void)hipMemcpy2DAsync(zd, sizeof(R) * ldzd, a.d_v, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
     }
     if (!zdev) {
-        (void)hipMemcpy2DAsync(z, sizeof(double) * ldz, zd, sizeof(double) * a.d_ld,
-                               sizeof(double) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+        (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
         (void)hipFreeAsync(zd, a.stream);
     }
     if (a.host_mode)  // the reference leaves V*Qh (the Schur basis) in V
-        (void)hipMemcpy2DAsync(v, sizeof(double) * ldv, a.d_v, sizeof(double) * a.d_ld,
-                               sizeof(double) * n, ncv, hipMemcpyDeviceToHost, a.stream);
+        (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, ncv, hipMemcpyDeviceToHost, a.stream);
     a.sync();
     return 0;
 }
@@ -321,6 +345,27 @@ void dneupd_(int* rvec, char const* howmny, int* select, double* dr, double* di,
              char const* which, int* nev, double* tol, double* resid, int* ncv, double* v,
              int* ldv, int* iparam, int* ipntr, double* workd, double* workl, int* lworkl,
              int* info, size_t, size_t, size_t) {
+    *info = ahip::ns_eupd(*rvec != 0, howmny[0], select, dr, di, z, *ldz, *sigmar, *sigmai, workev,
+                          bmat[0], *n, which, *nev, *tol, resid, *ncv, v, *ldv, iparam, ipntr,
+                          workd, workl, *lworkl);
+}
+
+// single-precision family (ICB/arpack.h:17; SRC/sneupd.f)
+void sneupd_c(int rvec, char const* howmny, int const* select, float* dr, float* di, float* z,
+              int ldz, float sigmar, float sigmai, float* workev, char const* bmat, int n,
+              char const* which, int nev, float tol, float* resid, int ncv, float* v, int ldv,
+              int* iparam, int* ipntr, float* workd, float* workl, int lworkl, int* info) {
+    (void)select;
+    *info = ahip::ns_eupd(rvec != 0, howmny[0], nullptr, dr, di, z, ldz, sigmar, sigmai, workev,
+                          bmat[0], n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
+                          workl, lworkl);
+}
+
+void sneupd_(int* rvec, char const* howmny, int* select, float* dr, float* di, float* z, int* ldz,
+             float* sigmar, float* sigmai, float* workev, char const* bmat, int* n,
+             char const* which, int* nev, float* tol, float* resid, int* ncv, float* v, int* ldv,
+             int* iparam, int* ipntr, float* workd, float* workl, int* lworkl, int* info, size_t,
+             size_t, size_t) {
     *info = ahip::ns_eupd(*rvec != 0, howmny[0], select, dr, di, z, *ldz, *sigmar, *sigmai, workev,
                           bmat[0], *n, which, *nev, *tol, resid, *ncv, v, *ldv, iparam, ipntr,
                           workd, workl, *lworkl);

@@ -19,6 +19,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "device.hpp"
 
@@ -77,11 +78,11 @@ __device__ __forceinline__ bool gate_closed(const LzState* st, int gate) {
 }
 
 // ------------------------------------------------------------------ place ---
-__global__ __launch_bounds__(kBlock) void k_place(int64_t n, const double* __restrict__ r,
-                                                  double* __restrict__ vcol,
-                                                  double* __restrict__ copy1,
-                                                  double* __restrict__ sc,
-                                                  LzState* __restrict__ st, int j) {
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_place(int64_t n, const R* __restrict__ r,
+                                                  R* __restrict__ vcol, R* __restrict__ copy1,
+                                                  R* __restrict__ sc, LzState* __restrict__ st,
+                                                  int j) {
     if (st->abort) return;
     const double rn = st->rnorm;
     if (!(rn > 0.0)) {  // invariant subspace: restart needed (SRC/dsaitr.f:378)
@@ -100,20 +101,20 @@ __global__ __launch_bounds__(kBlock) void k_place(int64_t n, const double* __res
     }
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const double v = r[i] * m0 * m1 * m2;
+        const R v = (R)((double)r[i] * m0 * m1 * m2);
         vcol[i] = v;
         if (copy1) copy1[i] = v;
-        if (sc) sc[i] = sc[i] * m0 * m1 * m2;
+        if (sc) sc[i] = (R)((double)sc[i] * m0 * m1 * m2);
     }
 }
 
 // ------------------------------------------------------------------- dots ---
 // Exact compile-time column count J (branch-free unrolled loads: all J column
 // loads of a row are in flight together).  WM: 0 no w'u, 1 w == u, 2 w != u.
-template <int J, int WM>
-__global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double* __restrict__ V,
-                                                 int64_t ld, const double* __restrict__ u,
-                                                 const double* __restrict__ w,
+template <class R, int J, int WM>
+__global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __restrict__ V,
+                                                 int64_t ld, const R* __restrict__ u,
+                                                 const R* __restrict__ w,
                                                  double* __restrict__ part, int pstride, int wslot,
                                                  const LzState* __restrict__ st, int gate) {
     if (gate_closed(st, gate)) return;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double
     for (int k = 0; k < J; ++k) acc[k] = 0.0;
     double aw = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    const double* Vb = V + (int64_t)j0 * ld;
+    const R* Vb = V + (int64_t)j0 * ld;
     // Software-pipelined: the next row's J+1 loads are issued before the
     // current row is consumed.  Without it the compiler serialises each
     // load->FMA pair for some J (26..29 here: one load in flight per wave,
@@ -157,10 +158,10 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const double
 // ----------------------------------------------------------------- update ---
 // rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
 // same pass (the V row stays in registers: one HBM read of V serves both).
-template <int J, bool SPEC>
+template <class R, int J, bool SPEC>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
-    int64_t n, const double* __restrict__ V, int64_t ld, const double* __restrict__ c,
-    const double* rin, double* rout, double* __restrict__ part, int pstride,
+    int64_t n, const R* __restrict__ V, int64_t ld, const double* __restrict__ c,
+    const R* rin, R* rout, double* __restrict__ part, int pstride,
     const LzState* __restrict__ st, int gate) {
     if (gate_closed(st, gate)) return;
     double acc[J];
@@ -175,31 +176,32 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < J; ++k) s += vrow[k] * c[k];
-        const double r = rin[i] - s;
+        const R r = (R)((double)rin[i] - s);
         rout[i] = r;
         if constexpr (SPEC) {
-            rr += r * r;
+            const double rd = (double)r;
+            rr += rd * rd;
 #pragma unroll
-            for (int k = 0; k < J; ++k) acc[k] += vrow[k] * r;
+            for (int k = 0; k < J; ++k) acc[k] += vrow[k] * rd;
         }
     }
     if constexpr (SPEC) block_partials<J>(acc, J, rr, true, part, 0, J);
 }
 
 // generic (any j): no fused dots
+template <class R>
 __global__ __launch_bounds__(kBlock) void k_update_generic(int64_t n, int j,
-                                                           const double* __restrict__ V,
-                                                           int64_t ld,
+                                                           const R* __restrict__ V, int64_t ld,
                                                            const double* __restrict__ c,
-                                                           const double* rin, double* rout,
+                                                           const R* rin, R* rout,
                                                            const LzState* __restrict__ st,
                                                            int gate) {
     if (gate_closed(st, gate)) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         double s = 0.0;
-        for (int k = 0; k < j; ++k) s += V[i + (int64_t)k * ld] * c[k];
-        rout[i] = rin[i] - s;
+        for (int k = 0; k < j; ++k) s += (double)V[i + (int64_t)k * ld] * c[k];
+        rout[i] = (R)((double)rin[i] - s);
     }
 }
 
@@ -316,19 +318,20 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
 }
 
-__global__ void k_zero_if(int64_t n, double* r, const LzState* st) {
+template <class R>
+__global__ void k_zero_if(int64_t n, R* r, const LzState* st) {
     if (st->abort || !st->zero) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) r[i] = 0.0;
 }
 
 // -------------------------------------------------------------- V*Q update --
-template <int MAXK>
-__global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, double* V, int64_t ld,
+template <class R, int MAXK>
+__global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t ld,
                                                       int kplusp, int kev,
                                                       const double* __restrict__ Q, int ldq,
                                                       double sigmak, double betak,
-                                                      double* __restrict__ r,
+                                                      R* __restrict__ r,
                                                       double* __restrict__ part, int pstride) {
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -348,23 +351,26 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, double* V, int6
 #pragma unroll
             for (int k = 0; k < MAXK; ++k)
                 if (k < kplusp) o += v[k] * Q[k + (int64_t)l * ldq];
-            V[i + (int64_t)l * ld] = o;
+            V[i + (int64_t)l * ld] = (R)o;
         }
-        double ri = sigmak * r[i];
+        double ri = sigmak * (double)r[i];
         if (next) {
-            V[i + (int64_t)kev * ld] = vnext;
-            ri += betak * vnext;
+            const R vn = (R)vnext;
+            V[i + (int64_t)kev * ld] = vn;
+            ri += betak * (double)vn;
         }
-        r[i] = ri;
-        rr += ri * ri;
+        const R rs = (R)ri;
+        r[i] = rs;
+        rr += (double)rs * (double)rs;
     }
     double acc[1] = {0.0};
     block_partials<1>(acc, 0, rr, true, part, 0, 0);
 }
 
+template <class R>
 __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
-    int64_t n, double* V, int64_t ld, int kplusp, int kev, const double* __restrict__ Q,
-    int ldq, double sigmak, double betak, double* __restrict__ r, double* __restrict__ tmp,
+    int64_t n, R* V, int64_t ld, int kplusp, int kev, const double* __restrict__ Q,
+    int ldq, double sigmak, double betak, R* __restrict__ r, double* __restrict__ tmp,
     double* __restrict__ part, int pstride) {
     // tmp: n x (kev+1) scratch (column-major, ld n) — used when kplusp > 64
     double rr = 0.0;
@@ -373,28 +379,29 @@ __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         for (int l = 0; l <= kev; ++l) {
             double o = 0.0;
-            for (int k = 0; k < kplusp; ++k) o += V[i + (int64_t)k * ld] * Q[k + (int64_t)l * ldq];
+            for (int k = 0; k < kplusp; ++k) o += (double)V[i + (int64_t)k * ld] * Q[k + (int64_t)l * ldq];
             tmp[i + (int64_t)l * n] = o;
         }
-        for (int l = 0; l < kev; ++l) V[i + (int64_t)l * ld] = tmp[i + (int64_t)l * n];
-        double ri = sigmak * r[i];
+        for (int l = 0; l < kev; ++l) V[i + (int64_t)l * ld] = (R)tmp[i + (int64_t)l * n];
+        double ri = sigmak * (double)r[i];
         if (next) {
-            const double vn = tmp[i + (int64_t)kev * n];
+            const R vn = (R)tmp[i + (int64_t)kev * n];
             V[i + (int64_t)kev * ld] = vn;
-            ri += betak * vn;
+            ri += betak * (double)vn;
         }
-        r[i] = ri;
-        rr += ri * ri;
+        const R rs = (R)ri;
+        r[i] = rs;
+        rr += (double)rs * (double)rs;
     }
     double acc[1] = {0.0};
     block_partials<1>(acc, 0, rr, true, part, 0, 0);
 }
 
 // Z = V(:,0:k) * M(k x nz) ; row-local, so Z may alias V (rows held in registers)
-template <int MAXK>
-__global__ __launch_bounds__(kBlock) void k_vq_gemm(int64_t n, const double* V, int64_t ld,
+template <class R, int MAXK>
+__global__ __launch_bounds__(kBlock) void k_vq_gemm(int64_t n, const R* V, int64_t ld,
                                                     int k, int nz, const double* __restrict__ M,
-                                                    double* Z, int64_t ldz) {
+                                                    R* Z, int64_t ldz) {
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         double v[MAXK];
@@ -405,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_vq_gemm(int64_t n, const double* V, 
 #pragma unroll
             for (int t = 0; t < MAXK; ++t)
                 if (t < k) o += v[t] * M[t + (int64_t)l * k];
-            Z[i + (int64_t)l * ldz] = o;
+            Z[i + (int64_t)l * ldz] = (R)o;
         }
     }
 }
@@ -417,7 +424,20 @@ __global__ __launch_bounds__(kBlock) void k_vq_gemm(int64_t n, const double* V, 
 constexpr uint64_t kLcgA = 33952834046453ull;
 constexpr uint64_t kMask48 = (1ull << 48) - 1;
 
-__device__ __forceinline__ uint64_t mulmod48(uint64_t a, uint64_t b) { return (a * b) & kMask48; }
+__device__ __host__ __forceinline__ uint64_t mulmod48(uint64_t a, uint64_t b) {
+    return (a * b) & kMask48;
+}
+
+// seed * a^steps mod 2^48 (host)
+uint64_t lcg_pow(uint64_t seed, uint64_t steps) {
+    uint64_t base = kLcgA, p = 1;
+    while (steps) {
+        if (steps & 1) p = mulmod48(p, base);
+        base = mulmod48(base, base);
+        steps >>= 1;
+    }
+    return mulmod48(seed, p);
+}
 
 __global__ void k_larnv(int64_t n, uint64_t seed, int64_t offset, double* __restrict__ x) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -434,32 +454,70 @@ __global__ void k_larnv(int64_t n, uint64_t seed, int64_t offset, double* __rest
     }
 }
 
+// slarnv(idist=2) in single precision (LAPACK slaruv): the same 48-bit stream,
+// converted with REAL arithmetic X = R*(IT1 + R*(IT2 + R*(IT3 + R*IT4))),
+// R = 1/4096 (unfused, as the Fortran evaluates it), then 2X - 1.  With 24-bit
+// floats X rounds to 1.0 about once in 2^25 draws; slaruv then bumps every seed
+// digit by 2 and redraws, which shifts the rest of its 64-draw batch and every
+// later batch.  The closed form below flags the first such index (atomicMin) and
+// the launcher regenerates the vector sequentially on the host (slarnv_host).
+__device__ __host__ inline float slaruv_real(uint64_t xm) {
+#pragma clang fp contract(off)
+    const float r = 1.0f / 4096.0f;
+    const float i1 = (float)((xm >> 36) & 4095), i2 = (float)((xm >> 24) & 4095);
+    const float i3 = (float)((xm >> 12) & 4095), i4 = (float)(xm & 4095);
+    return r * (i1 + r * (i2 + r * (i3 + r * i4)));
+}
+
+__global__ void k_larnv_f(int64_t n, uint64_t seed, int64_t offset, float* __restrict__ x,
+                          unsigned long long* __restrict__ flag) {
+#pragma clang fp contract(off)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t e = (uint64_t)(i + offset) + 1, base = kLcgA, p = 1;
+        while (e) {
+            if (e & 1) p = mulmod48(p, base);
+            base = mulmod48(base, base);
+            e >>= 1;
+        }
+        const float u = slaruv_real(mulmod48(seed, p));
+        if (u == 1.0f) atomicMin(flag, (unsigned long long)i);
+        x[i] = 2.0f * u - 1.0f;
+    }
+}
+
 // ------------------------------------------------------------ elementwise ---
-__global__ void k_copy(int64_t n, const double* __restrict__ s, double* __restrict__ d) {
+template <class R>
+__global__ void k_copy(int64_t n, const R* __restrict__ s, R* __restrict__ d) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] = s[i];
 }
-__global__ void k_scal(int64_t n, double a, double* x) {
+template <class R>
+__global__ void k_scal(int64_t n, double a, R* x) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= a;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = (R)((double)x[i] * a);
 }
-__global__ void k_fill(int64_t n, double a, double* x) {
+template <class R>
+__global__ void k_fill(int64_t n, double a, R* x) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = (R)a;
 }
-__global__ void k_axpby(int64_t n, double alpha, double* y, double beta, const double* x) {
+template <class R>
+__global__ void k_axpby(int64_t n, double alpha, R* y, double beta, const R* x) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        y[i] = alpha * y[i] + beta * x[i];
+        y[i] = (R)(alpha * (double)y[i] + beta * (double)x[i]);
 }
 
 // Z(:,l) += x * w[l]  (dseupd purification, SRC/dseupd.f:840-857)
-__global__ void k_ger_cols(int64_t n, int k, const double* __restrict__ x,
-                           const double* __restrict__ w, double* Z, int64_t ldz) {
+template <class R>
+__global__ void k_ger_cols(int64_t n, int k, const R* __restrict__ x,
+                           const double* __restrict__ w, R* Z, int64_t ldz) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const double xi = x[i];
-        for (int l = 0; l < k; ++l) Z[i + (int64_t)l * ldz] += xi * w[l];
+        for (int l = 0; l < k; ++l)
+            Z[i + (int64_t)l * ldz] = (R)((double)Z[i + (int64_t)l * ldz] + xi * w[l]);
     }
 }
 
@@ -525,10 +583,11 @@ struct ProfScope {  // event pair around one launch when profiling is on
 };
 }  // namespace
 
-void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double* copy1,
-           double* sc, int j) {
-    ProfScope ps(kProfPlace, ws.stream, 8.0 * n * (2 + (copy1 != nullptr) + 2 * (sc != nullptr)));
-    hipLaunchKernelGGL(k_place, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
+template <class R>
+void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc, int j) {
+    ProfScope ps(kProfPlace, ws.stream,
+                 (double)sizeof(R) * n * (2 + (copy1 != nullptr) + 2 * (sc != nullptr)));
+    hipLaunchKernelGGL(k_place<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
                        sc, ws.st, j);
 }
 
@@ -536,18 +595,18 @@ void place(const Workspace& ws, int64_t n, const double* r, double* vcol, double
     M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16) \
     M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
 
-template <int WM>
-static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const double* V,
-                        int64_t ld, const double* u, const double* w, int wslot, int gate) {
+template <class R, int WM>
+static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R* V, int64_t ld,
+                        const R* u, const R* w, int wslot, int gate) {
     const dim3 g(ws.nblk), b(kBlock);
     switch (jc) {
         case 0:
-            hipLaunchKernelGGL((k_dots<0, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,
+            hipLaunchKernelGGL((k_dots<R, 0, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,
                                ws.stride, wslot, ws.st, gate);
             break;
 #define AHIP_DOTS_CASE(J)                                                                          \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_dots<J, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,       \
+        hipLaunchKernelGGL((k_dots<R, J, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,    \
                            ws.stride, wslot, ws.st, gate);                                         \
         break;
         AHIP_CASES_1_32(AHIP_DOTS_CASE)
@@ -556,48 +615,50 @@ static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const do
     }
 }
 
-void dots(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
-          const double* w, int gate) {
+template <class R>
+void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, const R* w,
+          int gate) {
     ProfScope ps(gate == 2 ? kProfOther : kProfDots, ws.stream,
-                 gate == 2 ? 0.0 : 8.0 * n * (j + 1 + (w != u)));
+                 gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 1 + (w != u)));
     if (j == 0) {
-        if (w == u) launch_dots<1>(ws, n, 0, 0, V, ld, u, w, 0, gate);
-        else launch_dots<2>(ws, n, 0, 0, V, ld, u, w, 0, gate);
+        if (w == u) launch_dots<R, 1>(ws, n, 0, 0, V, ld, u, w, 0, gate);
+        else launch_dots<R, 2>(ws, n, 0, 0, V, ld, u, w, 0, gate);
         return;
     }
     for (int j0 = 0; j0 < j; j0 += 32) {
         const int jc = (j - j0 < 32) ? j - j0 : 32;
-        if (j0 > 0) launch_dots<0>(ws, n, j0, jc, V, ld, u, w, j, gate);
-        else if (w == u) launch_dots<1>(ws, n, j0, jc, V, ld, u, w, j, gate);
-        else launch_dots<2>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        if (j0 > 0) launch_dots<R, 0>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else if (w == u) launch_dots<R, 1>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else launch_dots<R, 2>(ws, n, j0, jc, V, ld, u, w, j, gate);
     }
 }
 
-void update(const Workspace& ws, int64_t n, int j, const double* V, int64_t ld, int which,
-            const double* rin, double* rout, bool spec, int gate) {
+template <class R>
+void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
+            R* rout, bool spec, int gate) {
     const double* c = ws.coef + (size_t)which * ws.stride;
     ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
-                 gate == 2 ? 0.0 : 8.0 * n * (j + 2));
+                 gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 2));
     const dim3 g(ws.nblk), b(kBlock);
     if (j >= 1 && j <= 32) {
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
     case J:                                                                                        \
         if (spec)                                                                                  \
-            hipLaunchKernelGGL((k_update_fused<J, true>), g, b, 0, ws.stream, n, V, ld, c, rin,    \
+            hipLaunchKernelGGL((k_update_fused<R, J, true>), g, b, 0, ws.stream, n, V, ld, c, rin, \
                                rout, ws.part, ws.stride, ws.st, gate);                             \
         else                                                                                       \
-            hipLaunchKernelGGL((k_update_fused<J, false>), g, b, 0, ws.stream, n, V, ld, c, rin,   \
-                               rout, ws.part, ws.stride, ws.st, gate);                             \
+            hipLaunchKernelGGL((k_update_fused<R, J, false>), g, b, 0, ws.stream, n, V, ld, c,     \
+                               rin, rout, ws.part, ws.stride, ws.st, gate);                        \
         break;
             AHIP_CASES_1_32(AHIP_UPD_CASE)
 #undef AHIP_UPD_CASE
             default: break;
         }
     } else {
-        hipLaunchKernelGGL(k_update_generic, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
+        hipLaunchKernelGGL(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
                            gate);
-        if (spec) dots(ws, n, j, V, ld, rout, rout, gate);
+        if (spec) dots<R>(ws, n, j, V, ld, rout, rout, gate);
     }
 }
 
@@ -613,70 +674,141 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
                        rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
 }
 
-void zero_if(const Workspace& ws, int64_t n, double* r) {
+template <class R>
+void zero_if(const Workspace& ws, int64_t n, R* r) {
     ProfScope ps(kProfOther, ws.stream, 0.0);
-    hipLaunchKernelGGL(k_zero_if, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
+    hipLaunchKernelGGL(k_zero_if<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
 }
 
-void vq_update(const Workspace& ws, int64_t n, double* V, int64_t ld, int kplusp, int kev,
-               double sigmak, double betak, double* r) {
+template <class R>
+void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int kev, double sigmak,
+               double betak, R* r) {
     const int g = ws.nblk;
-    ProfScope ps(kProfVq, ws.stream, 8.0 * n * (kplusp + kev + (betak > 0.0) + 2));
+    ProfScope ps(kProfVq, ws.stream,
+                 (double)sizeof(R) * n * (kplusp + kev + (betak > 0.0) + 2));
     if (kplusp <= 16)
-        hipLaunchKernelGGL(k_vq_update<16>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
-                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+        hipLaunchKernelGGL((k_vq_update<R, 16>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
+                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
     else if (kplusp <= 32)
-        hipLaunchKernelGGL(k_vq_update<32>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
-                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+        hipLaunchKernelGGL((k_vq_update<R, 32>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
+                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
     else if (kplusp <= 64)
-        hipLaunchKernelGGL(k_vq_update<64>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev,
-                           ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+        hipLaunchKernelGGL((k_vq_update<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
+                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
     else {
         double* tmp = nullptr;
         (void)hipMallocAsync(&tmp, sizeof(double) * (size_t)n * (kev + 1), ws.stream);
-        hipLaunchKernelGGL(k_vq_update_generic, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp,
-                           kev, ws.q, kplusp, sigmak, betak, r, tmp, ws.part, ws.stride);
+        hipLaunchKernelGGL(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
+                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, tmp, ws.part, ws.stride);
         (void)hipFreeAsync(tmp, ws.stream);
     }
 }
 
-void vq_gemm(const Workspace& ws, int64_t n, const double* V, int64_t ld, int k, int nz, double* Z,
+template <class R>
+void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int nz, R* Z,
              int64_t ldz) {
     const int g = grid_for(n);
     if (k <= 16)
-        hipLaunchKernelGGL(k_vq_gemm<16>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
-                           ldz);
+        hipLaunchKernelGGL((k_vq_gemm<R, 16>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+                           ws.q, Z, ldz);
     else if (k <= 32)
-        hipLaunchKernelGGL(k_vq_gemm<32>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
-                           ldz);
+        hipLaunchKernelGGL((k_vq_gemm<R, 32>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+                           ws.q, Z, ldz);
     else if (k <= 64)
-        hipLaunchKernelGGL(k_vq_gemm<64>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
-                           ldz);
+        hipLaunchKernelGGL((k_vq_gemm<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+                           ws.q, Z, ldz);
     else
-        hipLaunchKernelGGL(k_vq_gemm<128>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz, ws.q, Z,
-                           ldz);
+        hipLaunchKernelGGL((k_vq_gemm<R, 128>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+                           ws.q, Z, ldz);
 }
 
-void larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x, int64_t offset) {
+uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,
+                       int64_t offset) {
     hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x);
+    return lcg_pow(seed48, (uint64_t)n);
 }
 
-void copy(hipStream_t s, int64_t n, const double* src, double* dst) {
-    hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, src, dst);
-}
-void scal(hipStream_t s, int64_t n, double a, double* x) {
-    hipLaunchKernelGGL(k_scal, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
-}
-void fill(hipStream_t s, int64_t n, double a, double* x) {
-    hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
-}
-void axpby(hipStream_t s, int64_t n, double alpha, double* y, double beta, const double* x) {
-    hipLaunchKernelGGL(k_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, n, alpha, y, beta, x);
+// Sequential slarnv(idist=2, iseed, n, x) with slaruv's 64-draw batches and its
+// redraw rule (LAPACK slarnv.f / slaruv.f); returns the updated 48-bit seed.
+uint64_t slarnv_host(int64_t n, uint64_t seed, float* x) {
+#pragma clang fp contract(off)
+    // every seed digit + 2 (slaruv.f: I1..I4 = I1..I4 + 2 when X(I) = 1)
+    const uint64_t bump = 2 * ((1ull << 36) + (1ull << 24) + (1ull << 12) + 1);
+    for (int64_t iv = 0; iv < n; iv += 64) {
+        const int il = (int)((n - iv) < 64 ? (n - iv) : 64);
+        uint64_t s = seed, p = 1, last = seed;
+        for (int i = 0; i < il; ++i) {
+            p = mulmod48(p, kLcgA);
+            for (;;) {
+                last = mulmod48(s, p);
+                const float u = slaruv_real(last);
+                if (u != 1.0f) {
+                    x[iv + i] = 2.0f * u - 1.0f;
+                    break;
+                }
+                s = (s + bump) & kMask48;
+            }
+        }
+        seed = last;
+    }
+    return seed;
 }
 
-void ger_cols(hipStream_t s, int64_t n, int k, const double* x, const double* w, double* Z,
-              int64_t ldz) {
-    hipLaunchKernelGGL(k_ger_cols, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
+uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x,
+                       int64_t offset) {
+    unsigned long long* flag = reinterpret_cast<unsigned long long*>(ws.host_scratch);
+    *flag = ~0ull;  // pinned host memory, visible to the kernel
+    hipLaunchKernelGGL(k_larnv_f, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x,
+                       flag);
+    (void)hipStreamSynchronize(ws.stream);
+    if (*flag == ~0ull) return lcg_pow(seed48, (uint64_t)n);
+    // a draw rounded to 1.0: slaruv's redraw shifts the stream from there on
+    std::vector<float> h((size_t)n);
+    const uint64_t s = slarnv_host(n, seed48, h.data());
+    (void)hipMemcpyAsync(x, h.data(), sizeof(float) * n, hipMemcpyHostToDevice, ws.stream);
+    (void)hipStreamSynchronize(ws.stream);
+    return s;
 }
+
+template <class R>
+void copy(hipStream_t s, int64_t n, const R* src, R* dst) {
+    hipLaunchKernelGGL(k_copy<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, src, dst);
+}
+template <class R>
+void scal(hipStream_t s, int64_t n, double a, R* x) {
+    hipLaunchKernelGGL(k_scal<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+}
+template <class R>
+void fill(hipStream_t s, int64_t n, double a, R* x) {
+    hipLaunchKernelGGL(k_fill<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+}
+template <class R>
+void axpby(hipStream_t s, int64_t n, double alpha, R* y, double beta, const R* x) {
+    hipLaunchKernelGGL(k_axpby<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, alpha, y, beta, x);
+}
+
+template <class R>
+void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z, int64_t ldz) {
+    hipLaunchKernelGGL(k_ger_cols<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
+}
+
+#define AHIP_INST(R)                                                                               \
+    template void place<R>(const Workspace&, int64_t, const R*, R*, R*, R*, int);                  \
+    template void dots<R>(const Workspace&, int64_t, int, const R*, int64_t, const R*, const R*,   \
+                          int);                                                                    \
+    template void update<R>(const Workspace&, int64_t, int, const R*, int64_t, int, const R*, R*,  \
+                            bool, int);                                                            \
+    template void zero_if<R>(const Workspace&, int64_t, R*);                                       \
+    template void vq_update<R>(const Workspace&, int64_t, R*, int64_t, int, int, double, double,  \
+                               R*);                                                                \
+    template void vq_gemm<R>(const Workspace&, int64_t, const R*, int64_t, int, int, R*, int64_t); \
+    template void copy<R>(hipStream_t, int64_t, const R*, R*);                                     \
+    template void scal<R>(hipStream_t, int64_t, double, R*);                                       \
+    template void fill<R>(hipStream_t, int64_t, double, R*);                                       \
+    template void axpby<R>(hipStream_t, int64_t, double, R*, double, const R*);                    \
+    template void ger_cols<R>(hipStream_t, int64_t, int, const R*, const double*, R*, int64_t);
+AHIP_INST(double)
+AHIP_INST(float)
+#undef AHIP_INST
 
 }  // namespace ahip::dev

@@ -16,10 +16,11 @@
 
 namespace ahip {
 
-Task Solver::run_ns() {
+template <class R>
+Task SolverT<R>::run_ns() {
     using la::Which;
     // ---- dnaup2 initialisation (SRC/dnaup2.f:272-317)
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(eps, 2.0 / 3.0);
     int nev = nev0;
     const int np0 = np;
     const int kplusp = nev0 + np0;
@@ -77,7 +78,7 @@ Task Solver::run_ns() {
         la::dngets(ishift, which, nev, np, ritzr, ritzi, bounds);
         if (nev == nev0 + 1) numcnv = nev0 + 1;
         std::memcpy(wl + 2 * np, bounds + np, sizeof(double) * nev);
-        nconv = la::dnconv(nev, ritzr + np, ritzi + np, wl + 2 * np, tol);
+        nconv = la::dnconv(nev, ritzr + np, ritzi + np, wl + 2 * np, tol, eps);
         {
             const int nptemp = np;
             for (int j = 0; j < nptemp; ++j)
@@ -170,5 +171,8 @@ fail:
     iparam[2] = mxiter;
     co_return;
 }
+
+template Task SolverT<double>::run_ns();
+template Task SolverT<float>::run_ns();
 
 }  // namespace ahip

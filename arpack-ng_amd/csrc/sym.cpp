@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "engine.hpp"
@@ -33,7 +34,8 @@ bool is_device_pointer(const void* p) {
     return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
 }
 
-int Arrays::attach(int64_t nn, int nc, double* resid, double* v, int ldv, double* workd) {
+template <class R>
+int ArraysT<R>::attach(int64_t nn, int nc, R* resid, R* v, int ldv, R* workd) {
     n = nn;
     ncv = nc;
     const bool dr = is_device_pointer(resid), dv = is_device_pointer(v), dw = is_device_pointer(workd);
@@ -50,12 +52,12 @@ int Arrays::attach(int64_t nn, int nc, double* resid, double* v, int ldv, double
     }
     if (host_mode) {
         d_ld = (n + 1) & ~int64_t(1);
-        if (hipMalloc(&d_v, sizeof(double) * (size_t)d_ld * ncv) != hipSuccess) return -2;
-        if (hipMalloc(&d_resid, sizeof(double) * (size_t)n) != hipSuccess) return -2;
-        if (hipMalloc(&d_workd, sizeof(double) * 3 * (size_t)n) != hipSuccess) return -2;
-        ck(hipMemsetAsync(d_v, 0, sizeof(double) * (size_t)d_ld * ncv, stream));
-        ck(hipMemsetAsync(d_workd, 0, sizeof(double) * 3 * (size_t)n, stream));
-        ck(hipMemsetAsync(d_resid, 0, sizeof(double) * (size_t)n, stream));
+        if (hipMalloc(&d_v, sizeof(R) * (size_t)d_ld * ncv) != hipSuccess) return -2;
+        if (hipMalloc(&d_resid, sizeof(R) * (size_t)n) != hipSuccess) return -2;
+        if (hipMalloc(&d_workd, sizeof(R) * 3 * (size_t)n) != hipSuccess) return -2;
+        ck(hipMemsetAsync(d_v, 0, sizeof(R) * (size_t)d_ld * ncv, stream));
+        ck(hipMemsetAsync(d_workd, 0, sizeof(R) * 3 * (size_t)n, stream));
+        ck(hipMemsetAsync(d_resid, 0, sizeof(R) * (size_t)n, stream));
     } else {
         d_v = v;
         d_ld = ldv;
@@ -65,7 +67,8 @@ int Arrays::attach(int64_t nn, int nc, double* resid, double* v, int ldv, double
     return 0;
 }
 
-void Arrays::release() {
+template <class R>
+void ArraysT<R>::release() {
     if (host_mode) {
         if (d_v) ck(hipFree(d_v));
         if (d_resid) ck(hipFree(d_resid));
@@ -77,53 +80,70 @@ void Arrays::release() {
     own_stream = false;
 }
 
-void Arrays::upload_resid() {
-    if (host_mode) ck(hipMemcpyAsync(d_resid, h_resid, sizeof(double) * n, hipMemcpyHostToDevice, stream));
+template <class R>
+void ArraysT<R>::upload_resid() {
+    if (host_mode) ck(hipMemcpyAsync(d_resid, h_resid, sizeof(R) * n, hipMemcpyHostToDevice, stream));
 }
 
-void Arrays::d2h_workd(int64_t off, int64_t len) {
+template <class R>
+void ArraysT<R>::d2h_workd(int64_t off, int64_t len) {
     if (host_mode && off >= 0)
-        ck(hipMemcpyAsync(h_workd + off, d_workd + off, sizeof(double) * len, hipMemcpyDeviceToHost, stream));
+        ck(hipMemcpyAsync(h_workd + off, d_workd + off, sizeof(R) * len, hipMemcpyDeviceToHost, stream));
 }
 
-void Arrays::h2d_workd(int64_t off, int64_t len) {
+template <class R>
+void ArraysT<R>::h2d_workd(int64_t off, int64_t len) {
     if (host_mode && off >= 0)
-        ck(hipMemcpyAsync(d_workd + off, h_workd + off, sizeof(double) * len, hipMemcpyHostToDevice, stream));
+        ck(hipMemcpyAsync(d_workd + off, h_workd + off, sizeof(R) * len, hipMemcpyHostToDevice, stream));
 }
 
-void Arrays::download_all() {
+template <class R>
+void ArraysT<R>::download_all() {
     if (!host_mode) return;
-    ck(hipMemcpy2DAsync(h_v, sizeof(double) * h_ldv, d_v, sizeof(double) * d_ld, sizeof(double) * n, ncv,
+    ck(hipMemcpy2DAsync(h_v, sizeof(R) * h_ldv, d_v, sizeof(R) * d_ld, sizeof(R) * n, ncv,
                         hipMemcpyDeviceToHost, stream));
-    ck(hipMemcpyAsync(h_resid, d_resid, sizeof(double) * n, hipMemcpyDeviceToHost, stream));
-    ck(hipMemcpyAsync(h_workd, d_workd, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, stream));
+    ck(hipMemcpyAsync(h_resid, d_resid, sizeof(R) * n, hipMemcpyDeviceToHost, stream));
+    ck(hipMemcpyAsync(h_workd, d_workd, sizeof(R) * 3 * n, hipMemcpyDeviceToHost, stream));
 }
 
-void Arrays::sync() { ck(hipStreamSynchronize(stream)); }
+template <class R>
+void ArraysT<R>::sync() { ck(hipStreamSynchronize(stream)); }
 
 // ------------------------------------------------------------- Solver ---
 
-Solver::~Solver() {
+template <class R>
+SolverT<R>::~SolverT() {
     root.reset();
     dev::ws_destroy(ws);
     a.release();
 }
 
-RciAwait Solver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
+template <class R>
+RciAwait SolverT<R>::rci(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = nullptr;
     op_y = nullptr;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
-RciAwait Solver::op(int ido, int64_t x, int64_t y, int64_t bx, const double* xp, double* yp) {
+template <class R>
+RciAwait SolverT<R>::op(int ido, int64_t x, int64_t y, int64_t bx, const R* xp, R* yp) {
     op_x = xp;
     op_y = yp;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
+template <class R>
+R* SolverT<R>::dist_x() {
+    if constexpr (std::is_same_v<R, double>)
+        return (dist && dist->x_ext) ? dist->x_mid() : nullptr;
+    else
+        return nullptr;  // the float family runs on one GPU
+}
+
 // Finalize of a reduction; with a multi-GPU distribution the local sums are
 // allreduced across ranks (one RCCL collective) before the phase logic runs.
-void Solver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
+template <class R>
+void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
     if (dist && dist->comm) {
         dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate);
         comm_allreduce_sum(dist->comm, ws.sums, m, a.stream);
@@ -133,25 +153,28 @@ void Solver::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
     }
 }
 
-void Solver::read_state() {
+template <class R>
+void SolverT<R>::read_state() {
     ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
 
-void Solver::write_state() {
+template <class R>
+void SolverT<R>::write_state() {
     ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
 }
 
 // dgetv0: generate (or take) a start vector, force it into range(OP), and for
 // j > 1 B-orthogonalise it against V(:,1:j-1) with <= 5 refinement sweeps.
 // On exit st.rnorm and this->rnorm hold its B-norm.
-Task Solver::getv0(bool initv, int j, int itry, int& ierr) {
+template <class R>
+Task SolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
     const int64_t nn = n;
-    double* wd = a.d_workd;
+    R* wd = a.d_workd;
     ierr = 0;
     if (!initv) {  // dlarnv(idist=2, iseed, n, resid) — SRC/dgetv0.f:234-237
-        dev::larnv_uniform(ws, nn, g_dseed, a.d_resid, row0);
-        g_dseed = lcg_advance(g_dseed, (uint64_t)(dist ? dist->n_global : nn));
+        const uint64_t s1 = dev::larnv_uniform(ws, nn, g_dseed, a.d_resid, row0);
+        g_dseed = dist ? lcg_advance(g_dseed, (uint64_t)dist->n_global) : s1;
     }
     if (itry == 1) {  // force into the range of OP (SRC/dgetv0.f:245-251)
         g_stats.nopx += 1;
@@ -212,9 +235,10 @@ Task Solver::getv0(bool initv, int j, int itry, int& ierr) {
 }
 
 // dsaitr: extend a k-step Lanczos factorization to k+npk steps.
-Task Solver::saitr(int k, int npk, int& iinfo) {
+template <class R>
+Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     const int64_t nn = n;
-    double* wd = a.d_workd;
+    R* wd = a.d_workd;
     const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
     const bool bI = (bmat == 'I');
     iinfo = 0;
@@ -244,14 +268,14 @@ Task Solver::saitr(int k, int npk, int& iinfo) {
                 write_state();
             }
             // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
-            double* xop = (dist && dist->x_ext) ? dist->x_mid() : (free_run ? vcol(j) : wd + ivj);
+            R* xop = dist_x() ? dist_x() : (free_run ? vcol(j) : wd + ivj);
             dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
                        bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
             g_stats.nopx += 1;
             co_await op(1, ivj, irj, ipj, xop, wd + irj);
             // STEP 4: B*OP*v_j (skipped in mode 2: WORKD(IVJ) holds A*v_j)
-            const double* u;
+            const R* u;
             if (mode == 2 && !arnoldi) {  // dsaitr only; dnaitr has no mode-2 shortcut
                 u = wd + ivj;
             } else if (!bI) {
@@ -340,8 +364,8 @@ Task Solver::saitr(int k, int npk, int& iinfo) {
             if (jj > 1) h[(jj - 1) + (size_t)(jj - 2) * ncv] = rec[2 * (jj - 1) + 1];  // h(jj,jj-1)
         }
         // negligible subdiagonals of the new Hessenberg block (SRC/dnaitr.f:820-838)
-        const double ulp = 2.0 * la::kEps;
-        const double smlnum = la::kSafmin * ((double)n_global / ulp);
+        const double ulp = 2.0 * eps;  // dlamch / slamch('precision')
+        const double smlnum = safmin * ((double)n_global / ulp);
         const int kp = k + npk;
         for (int i = std::max(1, k); i <= kp - 1; ++i) {
             double tst1 = std::fabs(h[(i - 1) + (size_t)(i - 1) * ncv]) + std::fabs(h[i + (size_t)i * ncv]);
@@ -355,7 +379,8 @@ Task Solver::saitr(int k, int npk, int& iinfo) {
 }
 
 // dsapps: bulge chase on the host, V*Q and the residual update on the device.
-void Solver::sapps(int kev, int npk) {
+template <class R>
+void SolverT<R>::sapps(int kev, int npk) {
     const int kplusp = kev + npk;
     double* h = workl + ih;
     double* q = workl + iq;
@@ -369,7 +394,8 @@ void Solver::sapps(int kev, int npk) {
 // V(:,1:kev) = V(:,1:kplusp) * Q(:,1:kev); v_{kev+1} = V*Q(:,kev+1) if betak > 0;
 // resid = sigmak*resid + betak*v_{kev+1} (SRC/dsapps.f:450-493, dnapps.f:583-640).
 // Q is the host matrix at workl(iq) (ld ncv).
-void Solver::vq_device(int kev, int kplusp, double sigmak, double betak) {
+template <class R>
+void SolverT<R>::vq_device(int kev, int kplusp, double sigmak, double betak) {
     const double* q = workl + iq;
     std::vector<double> qbuf((size_t)kplusp * (kev + 1));  // compact, ld = kplusp
     for (int c = 0; c <= kev && c < kplusp; ++c)
@@ -379,9 +405,10 @@ void Solver::vq_device(int kev, int kplusp, double sigmak, double betak) {
     a.sync();  // qbuf lifetime
 }
 
-Task Solver::run() {
+template <class R>
+Task SolverT<R>::run() {
     // ---- dsaup2 initialisation (SRC/dsaup2.f:258-317)
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(eps, 2.0 / 3.0);
     int nev = nev0;
     const int np0 = np;
     const int kplusp = nev0 + np0;
@@ -434,7 +461,7 @@ Task Solver::run() {
         np = np0;
         la::dsgets(ishift, which, nev, np, ritz, bounds, wl);
         std::memcpy(wl + np, bounds + np, sizeof(double) * nev);
-        nconv = la::dsconv(nev, ritz + np, wl + np, tol);
+        nconv = la::dsconv(nev, ritz + np, wl + np, tol, eps);
         {
             const int nptemp = np;
             for (int jj = 0; jj < nptemp; ++jj)
@@ -510,5 +537,10 @@ done:
     iparam[2] = mxiter;
     co_return;
 }
+
+template struct ArraysT<double>;
+template struct ArraysT<float>;
+template class SolverT<double>;
+template class SolverT<float>;
 
 }  // namespace ahip

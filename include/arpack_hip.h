@@ -75,6 +75,46 @@ void zneupd_c(a_int rvec, char const* howmny, a_int const* select, a_dcomplex* d
               a_dcomplex* v, a_int ldv, a_int* iparam, a_int* ipntr, a_dcomplex* workd,
               a_dcomplex* workl, a_int lworkl, double* rwork, a_int* info);
 
+/* ---- single precision (ICB/arpack.h:16-19; SRC/ssaupd.f, snaupd.f, sseupd.f,
+ *      sneupd.f).  V, resid, workd and the kernels are fp32 in HBM (half the
+ *      bytes of the d* family); the ncv-sized host work runs in double on a
+ *      shadow of workl, rounded into the caller's float workl at every return.
+ *      tol <= 0 selects slamch('EpsMach') = 2^-24.  One GPU, reverse
+ *      communication (no device-CSR or distributed entries). */
+void ssaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev, float tol,
+              float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam, a_int* ipntr,
+              float* workd, float* workl, a_int lworkl, a_int* info);
+void sseupd_c(a_int rvec, char const* howmny, a_int const* select, float* d, float* z,
+              a_int ldz, float sigma, char const* bmat, a_int n, char const* which, a_int nev,
+              float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
+              a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info);
+void snaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev, float tol,
+              float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam, a_int* ipntr,
+              float* workd, float* workl, a_int lworkl, a_int* info);
+void sneupd_c(a_int rvec, char const* howmny, a_int const* select, float* dr, float* di,
+              float* z, a_int ldz, float sigmar, float sigmai, float* workev, char const* bmat,
+              a_int n, char const* which, a_int nev, float tol, float* resid, a_int ncv,
+              float* v, a_int ldv, a_int* iparam, a_int* ipntr, float* workd, float* workl,
+              a_int lworkl, a_int* info);
+void ssaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev, float* tol,
+             float* resid, a_int* ncv, float* v, a_int* ldv, a_int* iparam, a_int* ipntr,
+             float* workd, float* workl, a_int* lworkl, a_int* info, size_t bmat_len,
+             size_t which_len);
+void snaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev, float* tol,
+             float* resid, a_int* ncv, float* v, a_int* ldv, a_int* iparam, a_int* ipntr,
+             float* workd, float* workl, a_int* lworkl, a_int* info, size_t bmat_len,
+             size_t which_len);
+void sseupd_(a_int* rvec, char const* howmny, a_int* select, float* d, float* z, a_int* ldz,
+             float* sigma, char const* bmat, a_int* n, char const* which, a_int* nev, float* tol,
+             float* resid, a_int* ncv, float* v, a_int* ldv, a_int* iparam, a_int* ipntr,
+             float* workd, float* workl, a_int* lworkl, a_int* info, size_t howmny_len,
+             size_t bmat_len, size_t which_len);
+void sneupd_(a_int* rvec, char const* howmny, a_int* select, float* dr, float* di, float* z,
+             a_int* ldz, float* sigmar, float* sigmai, float* workev, char const* bmat, a_int* n,
+             char const* which, a_int* nev, float* tol, float* resid, a_int* ncv, float* v,
+             a_int* ldv, a_int* iparam, a_int* ipntr, float* workd, float* workl, a_int* lworkl,
+             a_int* info, size_t howmny_len, size_t bmat_len, size_t which_len);
+
 /* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
  *      argument by reference + hidden trailing CHARACTER lengths ---------------- */
 void dsaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev,
@@ -304,6 +344,10 @@ void arpack_hip_kit_dsortr(char const* which, int apply, int n, double* x1, doub
 void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h, int ldh,
                                 double* q, int ldq);
 void arpack_hip_kit_dlarnv(int* iseed, int n, double* x);
+void arpack_hip_kit_slarnv(int* iseed, int n, float* x); /* slarnv(idist=2), LAPACK slaruv rules */
+/* The device generators behind dgetv0/sgetv0's start vector on a device buffer
+ * x (prec 'd': double, 's': float); iseed is advanced like dlarnv/slarnv's. */
+int arpack_hip_larnv_device(char prec, int* iseed, int64_t n, void* x);
 /* nonsymmetric kit (restated LAPACK dlahqr/dtrevc/dlanv2/dnrm2 and ARPACK
  * dsortc/dngets/dneigh/dnapps; compared against SRC/dsortc.f, dngets.f,
  * dneigh.f, dnapps.f and the image's LAPACK in tests/test_kit_ns.py) */

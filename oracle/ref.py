@@ -62,7 +62,7 @@ def _pi(a):
 
 
 def _pd(a):
-    return a.ctypes.data_as(_d)
+    return a.ctypes.data_as(C.c_void_p)  # double* or float* (untyped Fortran entry)
 
 
 def _ci(x):
@@ -86,33 +86,36 @@ def timing() -> Timing:
 
 def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
                  mode=1, bmat="I", bop=None, rvec=True, sigma=0.0, ishift=1,
-                 shifts=None, return_state=False):
+                 shifts=None, return_state=False, prec="d"):
     """Run dsaupd_/dseupd_ to completion. Returns dict with d, z, iparam, info...
 
     `op(x, ido, bx)` computes OP*x (bx = B*x slice for modes 3-5, else None);
-    `bop(x)` computes B*x when bmat='G'.
+    `bop(x)` computes B*x when bmat='G'.  prec="s": ssaupd_/sseupd_ (SRC/ssaupd.f)
+    on float32 arrays.
     """
     L = lib()
+    dt = np.float32 if prec == "s" else np.float64
+    ct = C.c_float if prec == "s" else C.c_double
     ido = np.zeros(1, np.int32)
     info = np.zeros(1, np.int32)
-    resid = np.zeros(n) if v0 is None else np.array(v0, dtype=np.float64, copy=True)
+    resid = np.zeros(n, dt) if v0 is None else np.array(v0, dtype=dt, copy=True)
     info[0] = 0 if v0 is None else 1
     ldv = n
-    v = np.asfortranarray(np.zeros((ldv, ncv)))
+    v = np.asfortranarray(np.zeros((ldv, ncv), dt))
     iparam = np.zeros(11, np.int32)
     ipntr = np.zeros(11, np.int32)
     iparam[0] = ishift
     iparam[2] = mxiter
     iparam[6] = mode
-    workd = np.zeros(3 * n)
+    workd = np.zeros(3 * n, dt)
     lworkl = ncv * ncv + 8 * ncv
-    workl = np.zeros(lworkl)
-    tolc = C.c_double(tol)
+    workl = np.zeros(lworkl, dt)
+    tolc = ct(tol)
     bm = bmat.encode()
     wh = which.encode()
     n_rci = 0
     while True:
-        L.dsaupd_(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
+        getattr(L, prec + "saupd_")(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
                   _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
                   _pd(workd), _pd(workl), _ci(lworkl), _pi(info),
                   C.c_size_t(1), C.c_size_t(2))
@@ -143,12 +146,12 @@ def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
     if info[0] < 0:
         return out
     nconv = int(iparam[4])
-    d = np.zeros(nev)
-    z = np.asfortranarray(np.zeros((n, nev)))
+    d = np.zeros(nev, dt)
+    z = np.asfortranarray(np.zeros((n, nev), dt))
     select = np.zeros(ncv, np.int32)
     ierr = np.zeros(1, np.int32)
-    L.dseupd_(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(d), _pd(z), _ci(n),
-              C.byref(C.c_double(sigma)), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev),
+    getattr(L, prec + "seupd_")(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(d),
+              _pd(z), _ci(n), C.byref(ct(sigma)), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev),
               C.byref(tolc), _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
               _pd(workd), _pd(workl), _ci(lworkl), _pi(ierr),
               C.c_size_t(1), C.c_size_t(1), C.c_size_t(2))
@@ -158,28 +161,32 @@ def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
 
 
 def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode=1,
-                 bmat="I", bop=None, rvec=True, sigmar=0.0, sigmai=0.0, return_state=False):
-    """Run dnaupd_/dneupd_ (SRC/dnaupd.f:406, SRC/dneupd.f) to completion."""
+                 bmat="I", bop=None, rvec=True, sigmar=0.0, sigmai=0.0, return_state=False,
+                 prec="d"):
+    """Run dnaupd_/dneupd_ (SRC/dnaupd.f:406, SRC/dneupd.f) to completion
+    (prec="s": snaupd_/sneupd_ on float32 arrays)."""
     L = lib()
+    dt = np.float32 if prec == "s" else np.float64
+    ct = C.c_float if prec == "s" else C.c_double
     ido = np.zeros(1, np.int32)
     info = np.zeros(1, np.int32)
-    resid = np.zeros(n) if v0 is None else np.array(v0, dtype=np.float64, copy=True)
+    resid = np.zeros(n, dt) if v0 is None else np.array(v0, dtype=dt, copy=True)
     info[0] = 0 if v0 is None else 1
     ldv = n
-    v = np.asfortranarray(np.zeros((ldv, ncv)))
+    v = np.asfortranarray(np.zeros((ldv, ncv), dt))
     iparam = np.zeros(11, np.int32)
     ipntr = np.zeros(14, np.int32)
     iparam[0] = 1
     iparam[2] = mxiter
     iparam[6] = mode
-    workd = np.zeros(3 * n)
+    workd = np.zeros(3 * n, dt)
     lworkl = 3 * ncv * ncv + 6 * ncv
-    workl = np.zeros(lworkl)
-    tolc = C.c_double(tol)
+    workl = np.zeros(lworkl, dt)
+    tolc = ct(tol)
     bm = bmat.encode()
     wh = which.encode()
     while True:
-        L.dnaupd_(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
+        getattr(L, prec + "naupd_")(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
                   _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
                   _pd(workd), _pd(workl), _ci(lworkl), _pi(info),
                   C.c_size_t(1), C.c_size_t(2))
@@ -201,14 +208,14 @@ def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
     if info[0] < 0:
         return out
     nconv = int(iparam[4])
-    dr = np.zeros(nev + 1)
-    di = np.zeros(nev + 1)
-    z = np.asfortranarray(np.zeros((n, nev + 1)))
+    dr = np.zeros(nev + 1, dt)
+    di = np.zeros(nev + 1, dt)
+    z = np.asfortranarray(np.zeros((n, nev + 1), dt))
     select = np.zeros(ncv, np.int32)
-    workev = np.zeros(3 * ncv)
+    workev = np.zeros(3 * ncv, dt)
     ierr = np.zeros(1, np.int32)
-    L.dneupd_(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(dr), _pd(di), _pd(z),
-              _ci(n), C.byref(C.c_double(sigmar)), C.byref(C.c_double(sigmai)), _pd(workev),
+    getattr(L, prec + "neupd_")(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(dr),
+              _pd(di), _pd(z), _ci(n), C.byref(ct(sigmar)), C.byref(ct(sigmai)), _pd(workev),
               C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc), _pd(resid),
               _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr), _pd(workd), _pd(workl),
               _ci(lworkl), _pi(ierr), C.c_size_t(1), C.c_size_t(1), C.c_size_t(2))

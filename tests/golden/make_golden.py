@@ -29,13 +29,17 @@ def csr_op(rowptr, col, val):
     return lambda x, *_: A @ x
 
 
-def run_sym(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, **extra):
+def run_sym(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, prec="d",
+            **extra):
     rowptr, col, val = mat
     n = len(rowptr) - 1
     if v0 is None:
         v0, _ = M.dlarnv_uniform(n)
+    if prec == "s":
+        v0 = v0.astype(np.float32)
+        extra["prec"] = "s"
     r = ref.dsaupd_solve(csr_op(rowptr, col, val), n, nev, ncv, which, tol, v0=v0,
-                         mxiter=mxiter, return_state=True)
+                         mxiter=mxiter, return_state=True, prec=prec)
     assert r["info"] >= 0, r
     out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
                mxiter=mxiter, v0=v0, info=r["info"], iparam=r["iparam"], d=r["d"],
@@ -50,15 +54,19 @@ def run_sym(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=F
     return r
 
 
-def run_ns(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, **extra):
+def run_ns(name, mat, spec, nev, ncv, which, tol, mxiter=300, v0=None, keep_z=False, prec="d",
+           **extra):
     """dnaupd/dneupd fixture (SRC/dnaupd.f, SRC/dneupd.f); workl layout
     SRC/dnaupd.f:494-520 (ritzr at ih+ncv^2, ritzi, bounds)."""
     rowptr, col, val = mat
     n = len(rowptr) - 1
     if v0 is None:
         v0, _ = M.dlarnv_uniform(n)
+    if prec == "s":
+        v0 = v0.astype(np.float32)
+        extra["prec"] = "s"
     r = ref.dnaupd_solve(csr_op(rowptr, col, val), n, nev, ncv, which, tol, v0=v0,
-                         mxiter=mxiter, return_state=True)
+                         mxiter=mxiter, return_state=True, prec=prec)
     assert r["info"] >= 0, r
     o = ncv * ncv
     out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
@@ -200,7 +208,29 @@ def g1_fresh_process_check():
     return ref.run_fresh(code)
 
 
+def single_fixtures():
+    """ssaupd/sseupd and snaupd/sneupd (SRC/ssaupd.f, SRC/snaupd.f): the reference's
+    single-precision family on float32 arrays, OP = A @ x rounded to float32."""
+    run_sym("s1_sssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
+            keep_z=True, prec="s")
+    run_sym("s2_icb_ss", M.diag(1000), ["diag", 1000], 9, 19, "LM", 1e-4, keep_z=True,
+            mxiter=10000, prec="s")
+    run_sym("s3_anderson3d", M.anderson(20, 3, 16.0, 1234), ["anderson", 20, 3, 16.0, 1234], 10,
+            30, "LA", 1e-5, keep_z=True, prec="s")
+    run_sym("s4_banded", M.banded_sym(20000, 1234, 512, 25), ["banded_sym", 20000, 1234, 512, 25],
+            10, 30, "LA", 1e-5, keep_z=False, prec="s")
+    run_ns("s5_bug1315_single", M.diag(1000), ["diag", 1000], 9, 19, "LM", 0.0, keep_z=True,
+           mxiter=10000, prec="s")
+    run_ns("s6_snsimp", M.convdiff2d(10, 10.0), ["convdiff2d", 10, 10.0], 4, 20, "LM", 1e-5,
+           keep_z=True, prec="s")
+    run_ns("s7_convdiff_lr", M.convdiff2d(30, 10.0), ["convdiff2d", 30, 10.0], 6, 30, "LR", 1e-5,
+           keep_z=True, mxiter=3000, prec="s")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["s"]:
+        single_fixtures()
+        sys.exit(0)
     if sys.argv[1:] == ["ns"]:
         nonsym_fixtures()
         sys.exit(0)

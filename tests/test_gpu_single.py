@@ -1,0 +1,162 @@
+"""GPU parity of the single-precision family (ssaupd/sseupd, snaupd/sneupd;
+ICB/arpack.h:16-19) against the reference's own float build (tests/golden/s*.npz
+from oracle/_ref's ssaupd_/snaupd_ on float32 arrays, OP = A @ x rounded to
+float32; s5 is TESTS/bug_1315_single.c's case).
+
+The engine keeps V, resid, workd and the kernels in fp32 but reduces in fp64 and
+does the ncv-sized work in fp64, so it is at least as accurate as the reference;
+the criteria are tolerance-level, not bitwise:
+  * info, nconv equal; restart cycles within 25% (rounding-driven at float eps);
+  * every reference eigenvalue is matched by ours within max(10 max(tol, eps_f),
+    1e-5) ||A||_1 (the reference's float rounding at tol = 0 is ~1e2 eps_f);
+  * Ritz residuals ||Az - λz|| / (||A||_1 ||z||) within 10x the reference's own
+    (floor 1e-6), nonsymmetric: the which-key selection agrees too;
+  * s5 also meets the reference test's acceptance |dr_i - (1000 - i)| <= 0.1.
+The device slarnv (start vector for info = 0) equals LAPACK's bit for bit,
+including slaruv's redraw when a draw rounds to 1.0.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import matrices as M
+
+pytestmark = pytest.mark.gpu
+EPS_F = float(np.finfo(np.float32).eps) / 2
+
+
+def _mat(spec):
+    k = str(spec[0])
+    if k == "diag":
+        return M.diag(int(spec[1]))
+    if k == "laplace2d":
+        return M.laplace2d(int(spec[1]), float(spec[2]))
+    if k == "anderson":
+        return M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4]))
+    if k == "banded_sym":
+        return M.banded_sym(int(spec[1]), int(spec[2]), int(spec[3]), int(spec[4]))
+    if k == "convdiff2d":
+        return M.convdiff2d(int(spec[1]), float(spec[2]))
+    raise KeyError(k)
+
+
+def _drive(s, A, device):
+    while True:
+        ido = s.aupd()
+        if ido in (-1, 1):
+            if device:
+                x = s.workd.numpy(int(s.ipntr[0]) - 1, s.n)
+                s.workd.write((A @ x).astype(np.float32), int(s.ipntr[1]) - 1)
+            else:
+                s.slice(1)[:] = A @ s.slice(0)
+        elif ido == 99:
+            return
+        else:
+            raise AssertionError(ido)
+
+
+def _tol(g):
+    """10 max(tol, eps_f), floored at 1e-5: at tol = 0 the reference's own float
+    eigenvalues carry ~1e2 eps_f of rounding (s5: 992 comes back as 991.99835)."""
+    return max(10 * max(float(g["tol"]), EPS_F), 1e-5)
+
+
+def _resid(A, z, d):
+    anorm = abs(A).sum(axis=0).max()
+    return max(np.linalg.norm(A @ z[:, k] - d[k] * z[:, k]) / (anorm * np.linalg.norm(z[:, k]))
+               for k in range(len(d)))
+
+
+def _counts(g, s):
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    it, ref = int(s.iparam[2]), int(g["iparam"][2])
+    assert abs(it - ref) <= max(2, 0.25 * ref), (it, ref)
+
+
+@pytest.mark.parametrize("name,device", [("s1_sssimp", False), ("s2_icb_ss", False),
+                                         ("s2_icb_ss", True), ("s3_anderson3d", False),
+                                         ("s4_banded", True)])
+def test_ssaupd(pkg, golden, name, device):
+    g = golden(name)
+    rp, col, val = _mat(g["spec"])
+    A = M.to_scipy(rp, col, val)
+    n = A.shape[0]
+    s = pkg.SymRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
+                   mxiter=int(g["mxiter"]), v0=g["v0"], device=device, prec="s")
+    _drive(s, A, device)
+    _counts(g, s)
+    d, z, nconv = s.eupd()
+    assert d.dtype == np.float32
+    dref = g["d"].astype(np.float64)
+    scale = np.abs(A).sum(axis=0).max()
+    for x in dref:
+        assert np.abs(d.astype(np.float64) - x).min() <= _tol(g) * scale
+    z = (z.numpy() if device else z).reshape(int(g["nev"]), n)[:nconv].T.astype(np.float64)
+    ours = _resid(A, z, d.astype(np.float64))
+    if "z" in g:
+        theirs = _resid(A, g["z"].astype(np.float64), dref)
+        assert ours <= max(10 * theirs, 1e-6), (ours, theirs)
+    else:
+        assert ours <= max(10 * float(g["tol"]), 1e-6), ours
+
+
+KEYS = {"LM": np.abs, "LR": np.real}
+
+
+@pytest.mark.parametrize("name", ["s5_bug1315_single", "s6_snsimp", "s7_convdiff_lr"])
+def test_snaupd(pkg, golden, name):
+    g = golden(name)
+    rp, col, val = _mat(g["spec"])
+    A = M.to_scipy(rp, col, val)
+    n = A.shape[0]
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
+                  mxiter=int(g["mxiter"]), v0=g["v0"], prec="s")
+    _drive(s, A, False)
+    _counts(g, s)
+    dr, di, z, nconv = s.eupd()
+    lam = dr.astype(np.float64) + 1j * di.astype(np.float64)
+    ref = g["dr"].astype(np.float64) + 1j * g["di"].astype(np.float64)
+    key = KEYS[str(g["which"])]
+    scale = np.abs(A).sum(axis=0).max()
+    tol = _tol(g) * scale
+    np.testing.assert_allclose(np.sort(key(lam)), np.sort(key(ref)), rtol=0, atol=tol)
+    for x in ref:
+        assert np.abs(lam - x).min() <= tol, (x, lam)
+    if name == "s5_bug1315_single":  # TESTS/bug_1315_single.c:80-86
+        for i in range(int(g["nev"])):
+            assert abs(dr[i] - (1000 - i)) <= 0.1
+    zz = z.reshape(int(g["nev"]) + 1, n)[:nconv].T.astype(np.float64)
+    real = np.abs(di) == 0
+    if real.any():  # real Ritz pairs: column k is the eigenvector
+        ours = _resid(A, zz[:, real], dr[real].astype(np.float64))
+        assert ours <= 1e-5, ours
+
+
+@pytest.mark.parametrize("seed", [(1, 3, 5, 7), "redraw"])
+def test_device_slarnv_bitwise(pkg, seed):
+    a, m = 33952834046453, 1 << 48
+    n = 1_000_003
+    if seed == "redraw":  # draw 700001 (in batch 10938) rounds to 1.0 in REAL arithmetic
+        s = ((m - 1) * pow(pow(a, 700001, m), -1, m)) % m
+        seed = ((s >> 36) & 4095, (s >> 24) & 4095, (s >> 12) & 4095, s & 4095)
+    iseed_h = np.array(seed, np.int32)
+    xh = np.zeros(n, np.float32)
+    pkg.lib().arpack_hip_kit_slarnv(iseed_h.ctypes.data_as(C.POINTER(C.c_int)), n,
+                                    xh.ctypes.data_as(C.c_void_p))
+    iseed_d = np.array(seed, np.int32)
+    buf = pkg.DeviceBuffer(n, np.float32)
+    L = pkg.lib()
+    L.arpack_hip_larnv_device.argtypes = [C.c_char, C.POINTER(C.c_int), C.c_int64, C.c_void_p]
+    assert L.arpack_hip_larnv_device(b"s", iseed_d.ctypes.data_as(C.POINTER(C.c_int)), n,
+                                     buf.ptr) == 0
+    assert np.array_equal(buf.numpy(), xh)
+    assert np.array_equal(iseed_d, iseed_h)
+    # and the double generator against its host restatement
+    xd = pkg.DeviceBuffer(1000, np.float64)
+    isd = np.array([1, 3, 5, 7], np.int32)
+    assert L.arpack_hip_larnv_device(b"d", isd.ctypes.data_as(C.POINTER(C.c_int)), 1000,
+                                     xd.ptr) == 0
+    y, s_out = M.dlarnv_uniform(1000)
+    assert np.array_equal(xd.numpy(), y) and tuple(isd) == tuple(s_out)

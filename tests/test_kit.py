@@ -46,6 +46,40 @@ def test_dlarnv_host_kit_matches_lapack(pkg, golden):
     assert np.array_equal(y, g["x"]) and tuple(s) == tuple(g["iseed_out"])
 
 
+def _digits(s48):
+    return np.array([(s48 >> 36) & 4095, (s48 >> 24) & 4095, (s48 >> 12) & 4095, s48 & 4095],
+                    np.int32)
+
+
+@pytest.mark.parametrize("case", ["plain", "redraw_chunk1", "redraw_chunk3"])
+def test_slarnv_host_kit_matches_lapack(pkg, case):
+    """slarnv(idist=2) in float: LAPACK slaruv's REAL conversion, its 64-draw
+    batches and its redraw rule when a draw rounds to 1.0 (every seed digit + 2),
+    bit for bit against the image's LAPACK (scipy_slarnv_)."""
+    a, m = 33952834046453, 1 << 48
+    if case == "plain":
+        seeds, n = [np.array([1, 3, 5, 7], np.int32), np.array([4095, 17, 2, 9], np.int32)], 1000
+    else:
+        # seed such that draw k (1-based, within the first batch or the third)
+        # is 2^48 - 1, which REAL arithmetic rounds to exactly 1.0
+        k = 5 if case == "redraw_chunk1" else 2 * 64 + 7
+        s = ((m - 1) * pow(pow(a, k, m), -1, m)) % m
+        seeds, n = [_digits(s)], 300
+    B = _blas()
+    for iseed in seeds:
+        for nn in (n, 63, 64, 65):
+            x1, s1 = np.zeros(nn, np.float32), iseed.copy()
+            B.scipy_slarnv_(C.byref(C.c_int(2)), pi(s1), C.byref(C.c_int(nn)),
+                            x1.ctypes.data_as(C.c_void_p))
+            x2, s2 = np.zeros(nn, np.float32), iseed.copy()
+            pkg.lib().arpack_hip_kit_slarnv(pi(s2), nn, x2.ctypes.data)
+            assert np.array_equal(x1, x2), (case, nn, np.flatnonzero(x1 != x2)[:5])
+            assert np.array_equal(s1, s2), (case, nn, s1, s2)
+    if case != "plain":  # the redraw really happened: the closed form differs from there on
+        y, _ = M.dlarnv_uniform(n, tuple(int(t) for t in seeds[0]))
+        assert not np.array_equal(y.astype(np.float32), x1)
+
+
 @needs_ref
 @pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (5, 2), (20, 3), (30, 4), (64, 5)])
 def test_dstqrb_matches_reference(pkg, n, seed):
