@@ -567,28 +567,35 @@ class ZRci:
     applies OP on workd slices (ido = -1/1; B*x at ipntr(3) in mode 3)."""
 
     def __init__(self, n, nev, ncv, which="LM", tol=0.0, bmat="I", mode=1, mxiter=300, ishift=1,
-                 v0=None):
+                 v0=None, prec="z"):
+        """prec="c": the complex64 family (cnaupd / cneupd)."""
         self.n, self.nev, self.ncv = n, nev, ncv
         self.which, self.bmat, self.tol, self.mode = which, bmat, float(tol), mode
+        self.prec = prec
+        self.ct = np.complex64 if prec == "c" else np.complex128
         self.ido = np.zeros(1, np.int32)
         self.info = np.zeros(1, np.int32)
         self.iparam = np.zeros(11, np.int32)
         self.ipntr = np.zeros(14, np.int32)
         self.iparam[0], self.iparam[2], self.iparam[6] = ishift, mxiter, mode
         self.lworkl = 3 * ncv * ncv + 5 * ncv
-        self.workl = np.zeros(self.lworkl, np.complex128)
-        self.rwork = np.zeros(ncv)
-        self.resid = np.zeros(n, np.complex128) if v0 is None else np.array(v0, np.complex128)
-        self.v = np.zeros(ncv * n, np.complex128)
-        self.workd = np.zeros(3 * n, np.complex128)
+        self.workl = np.zeros(self.lworkl, self.ct)
+        self.rwork = np.zeros(ncv, np.float32 if prec == "c" else np.float64)
+        self.resid = np.zeros(n, self.ct) if v0 is None else np.array(v0, self.ct)
+        self.v = np.zeros(ncv * n, self.ct)
+        self.workd = np.zeros(3 * n, self.ct)
         self.info[0] = 0 if v0 is None else 1
 
     def aupd(self):
-        """One znaupd_c call (tol by value, SRC/icbazn.F90); returns ido."""
-        lib().znaupd_c(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev,
-                       self.tol, self.resid.ctypes.data, self.ncv, self.v.ctypes.data, self.n,
-                       _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
-                       self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data, _ip(self.info))
+        """One znaupd_c / cnaupd_c call (tol by value, SRC/icbazn.F90); returns ido."""
+        f = getattr(lib(), self.prec + "naupd_c")
+        f.argtypes = [_PI, C.c_char_p, _I, C.c_char_p, _I,
+                      C.c_float if self.prec == "c" else C.c_double, _PD, _I, _PD, _I, _PI, _PI,
+                      _PD, _PD, _I, _PD, _PI]
+        f(_ip(self.ido), self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol,
+          self.resid.ctypes.data, self.ncv, self.v.ctypes.data, self.n, _ip(self.iparam),
+          _ip(self.ipntr), self.workd.ctypes.data, self.workl.ctypes.data, self.lworkl,
+          self.rwork.ctypes.data, _ip(self.info))
         return int(self.ido[0])
 
     def aupd_zcsr(self, A: "ZCSR"):
@@ -610,16 +617,18 @@ class ZRci:
     def eupd(self, rvec=True, howmny="A", sigma=0j):
         """zneupd_c: returns (d, Z (n x nconv), nconv)."""
         nconv = int(self.iparam[4])
-        d = np.zeros(self.nev + 1, np.complex128)
-        z = np.zeros((self.nev + 1) * self.n, np.complex128)
+        d = np.zeros(self.nev + 1, self.ct)
+        z = np.zeros((self.nev + 1) * self.n, self.ct)
         select = np.zeros(self.ncv, np.int32)
-        workev = np.zeros(2 * self.ncv, np.complex128)
+        workev = np.zeros(2 * self.ncv, self.ct)
         info = np.zeros(1, np.int32)
-        f = lib().zneupd_c
-        f.argtypes = [_I, C.c_char_p, _PI, _PD, _PD, _I, _CD, _PD, C.c_char_p, _I, C.c_char_p, _I,
-                      C.c_double, _PD, _I, _PD, _I, _PI, _PI, _PD, _PD, _I, _PD, _PI]
+        f = getattr(lib(), self.prec + "neupd_c")
+        cs = _CF if self.prec == "c" else _CD
+        f.argtypes = [_I, C.c_char_p, _PI, _PD, _PD, _I, cs, _PD, C.c_char_p, _I, C.c_char_p, _I,
+                      C.c_float if self.prec == "c" else C.c_double, _PD, _I, _PD, _I, _PI, _PI,
+                      _PD, _PD, _I, _PD, _PI]
         f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, z.ctypes.data, self.n,
-          _CD(sigma.real, sigma.imag), workev.ctypes.data, self.bmat.encode(), self.n,
+          cs(sigma.real, sigma.imag), workev.ctypes.data, self.bmat.encode(), self.n,
           self.which.encode(), self.nev, self.tol, self.resid.ctypes.data, self.ncv,
           self.v.ctypes.data, self.n, _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
           self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data, _ip(info))
@@ -636,6 +645,11 @@ class ZRci:
 class _CD(C.Structure):
     """C99 double _Complex passed by value (two doubles in SSE registers)."""
     _fields_ = [("re", C.c_double), ("im", C.c_double)]
+
+
+class _CF(C.Structure):
+    """C99 float _Complex passed by value (both floats in one SSE register)."""
+    _fields_ = [("re", C.c_float), ("im", C.c_float)]
 
 
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,

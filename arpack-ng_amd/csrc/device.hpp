@@ -103,11 +103,12 @@ void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int 
 // dlarnv / slarnv(idist=2) continuation: x[m] = 2*u(seed*a^(m+1) mod 2^48) - 1;
 // offset: global index of x[0] in the stream (row-block sharding).  Returns the
 // advanced 48-bit seed (seed*a^n unless slaruv's float redraw rule fired).
+// batch: slaruv draws per call (64 for s/dlarnv, 128 for c/zlarnv: 64 complex)
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,
-                       int64_t offset = 0);
+                       int64_t offset = 0, int batch = 64);
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x,
-                       int64_t offset = 0);
-uint64_t slarnv_host(int64_t n, uint64_t seed48, float* x);
+                       int64_t offset = 0, int batch = 64);
+uint64_t slarnv_host(int64_t n, uint64_t seed48, float* x, int batch = 64);
 template <class R>
 void copy(hipStream_t s, int64_t n, const R* src, R* dst);
 template <class R>

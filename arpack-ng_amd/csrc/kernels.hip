@@ -723,19 +723,20 @@ void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int 
 }
 
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,
-                       int64_t offset) {
+                       int64_t offset, int) {
     hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x);
     return lcg_pow(seed48, (uint64_t)n);
 }
 
-// Sequential slarnv(idist=2, iseed, n, x) with slaruv's 64-draw batches and its
-// redraw rule (LAPACK slarnv.f / slaruv.f); returns the updated 48-bit seed.
-uint64_t slarnv_host(int64_t n, uint64_t seed, float* x) {
+// Sequential slarnv(idist=2, iseed, n, x) with slaruv's batches (64 draws;
+// clarnv draws 128 = 64 complex per slaruv call) and its redraw rule (LAPACK
+// slarnv.f / clarnv.f / slaruv.f); returns the updated 48-bit seed.
+uint64_t slarnv_host(int64_t n, uint64_t seed, float* x, int batch) {
 #pragma clang fp contract(off)
     // every seed digit + 2 (slaruv.f: I1..I4 = I1..I4 + 2 when X(I) = 1)
     const uint64_t bump = 2 * ((1ull << 36) + (1ull << 24) + (1ull << 12) + 1);
-    for (int64_t iv = 0; iv < n; iv += 64) {
-        const int il = (int)((n - iv) < 64 ? (n - iv) : 64);
+    for (int64_t iv = 0; iv < n; iv += batch) {
+        const int il = (int)((n - iv) < batch ? (n - iv) : batch);
         uint64_t s = seed, p = 1, last = seed;
         for (int i = 0; i < il; ++i) {
             p = mulmod48(p, kLcgA);
@@ -755,16 +756,23 @@ uint64_t slarnv_host(int64_t n, uint64_t seed, float* x) {
 }
 
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x,
-                       int64_t offset) {
+                       int64_t offset, int batch) {
     unsigned long long* flag = reinterpret_cast<unsigned long long*>(ws.host_scratch);
-    *flag = ~0ull;  // pinned host memory, visible to the kernel
-    hipLaunchKernelGGL(k_larnv_f, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x,
-                       flag);
-    (void)hipStreamSynchronize(ws.stream);
-    if (*flag == ~0ull) return lcg_pow(seed48, (uint64_t)n);
+    const bool own = (flag == nullptr);
+    if (own && hipHostMalloc(&flag, sizeof(unsigned long long)) != hipSuccess) flag = nullptr;
+    bool redraw = true;  // no flag memory: take the sequential path
+    if (flag) {
+        *flag = ~0ull;  // pinned host memory, visible to the kernel
+        hipLaunchKernelGGL(k_larnv_f, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48,
+                           offset, x, flag);
+        (void)hipStreamSynchronize(ws.stream);
+        redraw = (*flag != ~0ull);
+        if (own) (void)hipHostFree(flag);
+    }
+    if (!redraw) return lcg_pow(seed48, (uint64_t)n);
     // a draw rounded to 1.0: slaruv's redraw shifts the stream from there on
     std::vector<float> h((size_t)n);
-    const uint64_t s = slarnv_host(n, seed48, h.data());
+    const uint64_t s = slarnv_host(n, seed48, h.data(), batch);
     (void)hipMemcpyAsync(x, h.data(), sizeof(float) * n, hipMemcpyHostToDevice, ws.stream);
     (void)hipStreamSynchronize(ws.stream);
     return s;

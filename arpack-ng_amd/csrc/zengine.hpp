@@ -34,26 +34,36 @@ struct ZCsr {
 };
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Ws& ws);
+// Launchers over the component type R of the interleaved complex vectors
+// (double: complex128, z*; float: complex64, c*); arithmetic in complex128.
 // out[c] = V(:,c)^H u for c < j; out[j] = w^H u if w
-void dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
-          const double* w, std::complex<double>* out);
+template <class R>
+void dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, const R* w,
+          std::complex<double>* out);
 // rout = rin - V(:,0:j) h
-void update(const Ws& ws, int64_t n, int j, const double* V, int64_t ld,
-            const std::complex<double>* h, const double* rin, double* rout);
+template <class R>
+void update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld,
+            const std::complex<double>* h, const R* rin, R* rout);
 // Z(:,0:nz) = V(:,0:k) M (k x nz); Z may alias V
-void gemm(const Ws& ws, int64_t n, const double* V, int64_t ld, int k, int nz,
-          const std::complex<double>* M, double* Z, int64_t ldz);
+template <class R>
+void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
+          const std::complex<double>* M, R* Z, int64_t ldz);
 // y = a*y + b*x (x may be null)
-void axpby(const Ws& ws, int64_t n, std::complex<double> a, double* y, std::complex<double> b,
-           const double* x);
+template <class R>
+void axpby(const Ws& ws, int64_t n, std::complex<double> a, R* y, std::complex<double> b,
+           const R* x);
 // Z(:,c) += x * w[c]
-void ger(const Ws& ws, int64_t n, int k, const double* x, const std::complex<double>* w,
-         double* Z, int64_t ldz);
+template <class R>
+void ger(const Ws& ws, int64_t n, int k, const R* x, const std::complex<double>* w, R* Z,
+         int64_t ldz);
 void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
 int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift);
 }  // namespace zdev
 
-class ZSolver {
+// R: component type of the n-length complex data (double: znaupd, float:
+// cnaupd); the ncv-sized host work is complex128 in both (workl shadow for c*).
+template <class R>
+class ZSolverT {
 public:
     using cd = std::complex<double>;
     char bmat = 'I';
@@ -68,15 +78,16 @@ public:
     int ih = 0, iritz = 0, ibounds = 0, iq = 0, iw = 0;
     double rnorm = 0.0;
 
-    Arrays a;  // n complex = 2n doubles; offsets below are in complex units
+    ArraysT<R> a;  // n complex = 2n reals; offsets below are in complex units
+    std::vector<cd> wshadow;  // c*: complex128 shadow of the caller's workl
     zdev::Ws ws;
     RciCtx ctx;
     std::optional<Task> root;
     const zdev::ZCsr* csr = nullptr;  // free-running OP (mode 1)
-    const double* op_x = nullptr;
-    double* op_y = nullptr;
+    const R* op_x = nullptr;
+    R* op_y = nullptr;
 
-    ~ZSolver();
+    ~ZSolverT();
     Task run();  // znaup2
 
 private:
@@ -84,10 +95,11 @@ private:
     Task naitr(int k, int npk, int& iinfo);
     RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
     RciAwait op(int ido, int64_t x, int64_t y, int64_t bx);
-    double* col(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based, doubles
-    double* wd(int64_t off) { return a.d_workd + 2 * off; }           // complex offset
-    int64_t ldc() const { return a.d_ld / 2; }                         // ld in complex units
-    double cnorm(const double* x);                                     // dznrm2 on device
+    R* col(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based, reals
+    R* wd(int64_t off) { return a.d_workd + 2 * off; }           // complex offset
+    int64_t ldc() const { return a.d_ld / 2; }                    // ld in complex units
+    double cnorm(const R* x);                                     // dznrm2 on device
 };
+using ZSolver = ZSolverT<double>;
 
 }  // namespace ahip

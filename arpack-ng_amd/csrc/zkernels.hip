@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/arpack_hip.h"
 #include "zengine.hpp"
@@ -30,21 +31,42 @@ __device__ __forceinline__ double2 cmulc(double2 a, double2 b) {  // conj(a) * b
     return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
 }
 
+// storage of one complex element: double2 (complex128, z*) or float2
+// (complex64, c*); arithmetic is always complex128
+template <class R>
+struct C2;
+template <>
+struct C2<double> {
+    using T = double2;
+};
+template <>
+struct C2<float> {
+    using T = float2;
+};
+__device__ __forceinline__ double2 d2(double2 v) { return v; }
+__device__ __forceinline__ double2 d2(float2 v) { return make_double2(v.x, v.y); }
+template <class R>
+__device__ __forceinline__ typename C2<R>::T st2(double2 v) {
+    if constexpr (std::is_same_v<R, double>) return v;
+    else return make_float2((float)v.x, (float)v.y);
+}
+
 // part layout: part[slot * nblk + block]; slot 2c = Re, 2c+1 = Im of column c0+c
-template <int C>
-__global__ __launch_bounds__(kB) void k_zdots(int64_t n, int c0, int cnt, const double2* __restrict__ V,
-                                              int64_t ld, const double2* __restrict__ u,
+template <class R, int C>
+__global__ __launch_bounds__(kB) void k_zdots(int64_t n, int c0, int cnt,
+                                              const typename C2<R>::T* __restrict__ V, int64_t ld,
+                                              const typename C2<R>::T* __restrict__ u,
                                               double* __restrict__ part, int nblk) {
     double2 acc[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) acc[c] = make_double2(0.0, 0.0);
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        const double2 ui = u[i];
+        const double2 ui = d2(u[i]);
 #pragma unroll
         for (int c = 0; c < C; ++c)
             if (c < cnt) {
-                const double2 p = cmulc(V[i + (int64_t)(c0 + c) * ld], ui);
+                const double2 p = cmulc(d2(V[i + (int64_t)(c0 + c) * ld]), ui);
                 acc[c].x += p.x;
                 acc[c].y += p.y;
             }
@@ -81,32 +103,36 @@ __global__ __launch_bounds__(kB) void k_sum_slots(const double* __restrict__ par
     if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(kB) void k_zupdate(int64_t n, int j, const double2* __restrict__ V,
-                                                int64_t ld, const double2* __restrict__ h,
-                                                const double2* rin, double2* rout) {
+template <class R>
+__global__ __launch_bounds__(kB) void k_zupdate(int64_t n, int j,
+                                                const typename C2<R>::T* __restrict__ V, int64_t ld,
+                                                const double2* __restrict__ h,
+                                                const typename C2<R>::T* rin,
+                                                typename C2<R>::T* rout) {
     __shared__ double2 sh[256];
     for (int c = threadIdx.x; c < j; c += kB) sh[c] = h[c];
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        double2 r = rin[i];
+        double2 r = d2(rin[i]);
         for (int c = 0; c < j; ++c) {
-            const double2 p = cmul(V[i + (int64_t)c * ld], sh[c]);
+            const double2 p = cmul(d2(V[i + (int64_t)c * ld]), sh[c]);
             r.x -= p.x;
             r.y -= p.y;
         }
-        rout[i] = r;
+        rout[i] = st2<R>(r);
     }
 }
 
-template <int MAXK>
-__global__ __launch_bounds__(kB) void k_zgemm(int64_t n, const double2* V, int64_t ld, int k, int nz,
-                                              const double2* __restrict__ M, double2* Z, int64_t ldz) {
+template <class R, int MAXK>
+__global__ __launch_bounds__(kB) void k_zgemm(int64_t n, const typename C2<R>::T* V, int64_t ld,
+                                              int k, int nz, const double2* __restrict__ M,
+                                              typename C2<R>::T* Z, int64_t ldz) {
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
         double2 v[MAXK];
 #pragma unroll
-        for (int t = 0; t < MAXK; ++t) v[t] = (t < k) ? V[i + (int64_t)t * ld] : make_double2(0.0, 0.0);
+        for (int t = 0; t < MAXK; ++t) v[t] = (t < k) ? d2(V[i + (int64_t)t * ld]) : make_double2(0.0, 0.0);
         for (int l = 0; l < nz; ++l) {
             double2 o = make_double2(0.0, 0.0);
 #pragma unroll
@@ -116,33 +142,38 @@ __global__ __launch_bounds__(kB) void k_zgemm(int64_t n, const double2* V, int64
                     o.x += p.x;
                     o.y += p.y;
                 }
-            Z[i + (int64_t)l * ldz] = o;
+            Z[i + (int64_t)l * ldz] = st2<R>(o);
         }
     }
 }
 
-__global__ void k_zaxpby(int64_t n, double2 a, double2* y, double2 b, const double2* x) {
+template <class R>
+__global__ void k_zaxpby(int64_t n, double2 a, typename C2<R>::T* y, double2 b,
+                         const typename C2<R>::T* x) {
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        double2 r = cmul(a, y[i]);
+        double2 r = cmul(a, d2(y[i]));
         if (x) {
-            const double2 p = cmul(b, x[i]);
+            const double2 p = cmul(b, d2(x[i]));
             r.x += p.x;
             r.y += p.y;
         }
-        y[i] = r;
+        y[i] = st2<R>(r);
     }
 }
 
-__global__ void k_zger(int64_t n, int k, const double2* __restrict__ x, const double2* __restrict__ w,
-                       double2* Z, int64_t ldz) {
+template <class R>
+__global__ void k_zger(int64_t n, int k, const typename C2<R>::T* __restrict__ x,
+                       const double2* __restrict__ w, typename C2<R>::T* Z, int64_t ldz) {
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        const double2 xi = x[i];
+        const double2 xi = d2(x[i]);
         for (int c = 0; c < k; ++c) {
             const double2 p = cmul(xi, w[c]);
-            Z[i + (int64_t)c * ldz].x += p.x;
-            Z[i + (int64_t)c * ldz].y += p.y;
+            double2 z = d2(Z[i + (int64_t)c * ldz]);
+            z.x += p.x;
+            z.y += p.y;
+            Z[i + (int64_t)c * ldz] = st2<R>(z);
         }
     }
 }
@@ -262,19 +293,21 @@ inline int grid(int64_t n, int cap = 8192) {
 }
 }  // namespace
 
-void dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* u,
-          const double* w, std::complex<double>* out) {
-    const double2* V2 = reinterpret_cast<const double2*>(V);
-    const double2* u2 = reinterpret_cast<const double2*>(u);
+template <class R>
+void dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, const R* w,
+          std::complex<double>* out) {
+    using T = typename C2<R>::T;
+    const T* V2 = reinterpret_cast<const T*>(V);
+    const T* u2 = reinterpret_cast<const T*>(u);
     for (int c0 = 0; c0 < j; c0 += 8) {
         const int cnt = j - c0 < 8 ? j - c0 : 8;
-        hipLaunchKernelGGL(k_zdots<8>, dim3(ws.nblk), dim3(kB), 0, ws.stream, n, c0, cnt, V2, ld, u2,
-                           ws.part, ws.nblk);
+        hipLaunchKernelGGL((k_zdots<R, 8>), dim3(ws.nblk), dim3(kB), 0, ws.stream, n, c0, cnt, V2, ld,
+                           u2, ws.part, ws.nblk);
     }
     // slot j: w^H u (a "column" at w with ld irrelevant)
     if (w) {
-        hipLaunchKernelGGL(k_zdots<1>, dim3(ws.nblk), dim3(kB), 0, ws.stream, n, 0, 1,
-                           reinterpret_cast<const double2*>(w), 0, u2, ws.part + (int64_t)2 * j * ws.nblk,
+        hipLaunchKernelGGL((k_zdots<R, 1>), dim3(ws.nblk), dim3(kB), 0, ws.stream, n, 0, 1,
+                           reinterpret_cast<const T*>(w), 0, u2, ws.part + (int64_t)2 * j * ws.nblk,
                            ws.nblk);
     }
     const int m = 2 * (j + (w ? 1 : 0));
@@ -284,45 +317,71 @@ void dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const dou
     for (int c = 0; c < m / 2; ++c) out[c] = std::complex<double>(ws.host[2 * c], ws.host[2 * c + 1]);
 }
 
-void update(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const std::complex<double>* h,
-            const double* rin, double* rout) {
+template <class R>
+void update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const std::complex<double>* h,
+            const R* rin, R* rout) {
+    using T = typename C2<R>::T;
     if (j > 0) (void)hipMemcpyAsync(ws.coef, h, sizeof(double) * 2 * j, hipMemcpyHostToDevice, ws.stream);
-    hipLaunchKernelGGL(k_zupdate, dim3(grid(n)), dim3(kB), 0, ws.stream, n, j,
-                       reinterpret_cast<const double2*>(V), ld, reinterpret_cast<const double2*>(ws.coef),
-                       reinterpret_cast<const double2*>(rin), reinterpret_cast<double2*>(rout));
+    hipLaunchKernelGGL(k_zupdate<R>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, j,
+                       reinterpret_cast<const T*>(V), ld, reinterpret_cast<const double2*>(ws.coef),
+                       reinterpret_cast<const T*>(rin), reinterpret_cast<T*>(rout));
     (void)hipStreamSynchronize(ws.stream);  // h is host memory
 }
 
-void gemm(const Ws& ws, int64_t n, const double* V, int64_t ld, int k, int nz, const std::complex<double>* M,
-          double* Z, int64_t ldz) {
+template <class R>
+void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
+          const std::complex<double>* M, R* Z, int64_t ldz) {
+    using T = typename C2<R>::T;
     (void)hipMemcpyAsync(ws.q, M, sizeof(double) * 2 * (size_t)k * nz, hipMemcpyHostToDevice, ws.stream);
-    auto V2 = reinterpret_cast<const double2*>(V);
+    auto V2 = reinterpret_cast<const T*>(V);
     auto M2 = reinterpret_cast<const double2*>(ws.q);
-    auto Z2 = reinterpret_cast<double2*>(Z);
+    auto Z2 = reinterpret_cast<T*>(Z);
     if (k <= 16)
-        hipLaunchKernelGGL(k_zgemm<16>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+        hipLaunchKernelGGL((k_zgemm<R, 16>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
+                           Z2, ldz);
     else if (k <= 32)
-        hipLaunchKernelGGL(k_zgemm<32>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+        hipLaunchKernelGGL((k_zgemm<R, 32>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
+                           Z2, ldz);
     else
-        hipLaunchKernelGGL(k_zgemm<64>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2, Z2, ldz);
+        hipLaunchKernelGGL((k_zgemm<R, 64>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
+                           Z2, ldz);
     (void)hipStreamSynchronize(ws.stream);
 }
 
-void axpby(const Ws& ws, int64_t n, std::complex<double> a, double* y, std::complex<double> b,
-           const double* x) {
-    hipLaunchKernelGGL(k_zaxpby, dim3(grid(n)), dim3(kB), 0, ws.stream, n, make_double2(a.real(), a.imag()),
-                       reinterpret_cast<double2*>(y), make_double2(b.real(), b.imag()),
-                       reinterpret_cast<const double2*>(x));
+template <class R>
+void axpby(const Ws& ws, int64_t n, std::complex<double> a, R* y, std::complex<double> b,
+           const R* x) {
+    using T = typename C2<R>::T;
+    hipLaunchKernelGGL(k_zaxpby<R>, dim3(grid(n)), dim3(kB), 0, ws.stream, n,
+                       make_double2(a.real(), a.imag()), reinterpret_cast<T*>(y),
+                       make_double2(b.real(), b.imag()), reinterpret_cast<const T*>(x));
 }
 
-void ger(const Ws& ws, int64_t n, int k, const double* x, const std::complex<double>* w, double* Z,
+template <class R>
+void ger(const Ws& ws, int64_t n, int k, const R* x, const std::complex<double>* w, R* Z,
          int64_t ldz) {
+    using T = typename C2<R>::T;
     (void)hipMemcpyAsync(ws.coef, w, sizeof(double) * 2 * k, hipMemcpyHostToDevice, ws.stream);
-    hipLaunchKernelGGL(k_zger, dim3(grid(n)), dim3(kB), 0, ws.stream, n, k,
-                       reinterpret_cast<const double2*>(x), reinterpret_cast<const double2*>(ws.coef),
-                       reinterpret_cast<double2*>(Z), ldz);
+    hipLaunchKernelGGL(k_zger<R>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, k,
+                       reinterpret_cast<const T*>(x), reinterpret_cast<const double2*>(ws.coef),
+                       reinterpret_cast<T*>(Z), ldz);
     (void)hipStreamSynchronize(ws.stream);
 }
+
+#define AHIP_ZINST(R)                                                                              \
+    template void dots<R>(const Ws&, int64_t, int, const R*, int64_t, const R*, const R*,          \
+                          std::complex<double>*);                                                  \
+    template void update<R>(const Ws&, int64_t, int, const R*, int64_t,                            \
+                            const std::complex<double>*, const R*, R*);                            \
+    template void gemm<R>(const Ws&, int64_t, const R*, int64_t, int, int,                         \
+                          const std::complex<double>*, R*, int64_t);                               \
+    template void axpby<R>(const Ws&, int64_t, std::complex<double>, R*, std::complex<double>,     \
+                           const R*);                                                              \
+    template void ger<R>(const Ws&, int64_t, int, const R*, const std::complex<double>*, R*,       \
+                         int64_t);
+AHIP_ZINST(double)
+AHIP_ZINST(float)
+#undef AHIP_ZINST
 
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s) {
     ws.stream = s;

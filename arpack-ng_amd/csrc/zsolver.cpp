@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "../../include/arpack_hip.h"
@@ -21,39 +22,43 @@ namespace ahip {
 
 using cd = std::complex<double>;
 
-ZSolver::~ZSolver() {
+template <class R>
+ZSolverT<R>::~ZSolverT() {
     root.reset();
     zdev::ws_destroy(ws);
     a.release();
 }
 
-RciAwait ZSolver::rci(int ido, int64_t x, int64_t y, int64_t bx) {
+template <class R>
+RciAwait ZSolverT<R>::rci(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = nullptr;
     op_y = nullptr;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
-RciAwait ZSolver::op(int ido, int64_t x, int64_t y, int64_t bx) {
+template <class R>
+RciAwait ZSolverT<R>::op(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = wd(x);
     op_y = wd(y);
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
 }
 
-double ZSolver::cnorm(const double* x) {
+template <class R>
+double ZSolverT<R>::cnorm(const R* x) {
     cd s;
     zdev::dots(ws, n, 0, a.d_v, ldc(), x, x, &s);
     return std::sqrt(std::fabs(s.real()));
 }
 
 // zgetv0 (SRC/zgetv0.f): start vector in range(OP), B-orthogonal to V(:,1:j-1)
-Task ZSolver::getv0(bool initv, int j, int itry, int& ierr) {
+template <class R>
+Task ZSolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
     const int64_t nn = n;
     ierr = 0;
     if (!initv) {  // zlarnv(idist=2): re/im pairs of one dlaruv stream
         dev::Workspace tmp;
         tmp.stream = a.stream;
-        dev::larnv_uniform(tmp, 2 * nn, g_dseed, a.d_resid);
-        g_dseed = lcg_advance(g_dseed, (uint64_t)(2 * nn));
+        g_dseed = dev::larnv_uniform(tmp, 2 * nn, g_dseed, a.d_resid, 0, 128);
     }
     if (itry == 1) {
         g_stats.nopx += 1;
@@ -79,7 +84,7 @@ Task ZSolver::getv0(bool initv, int j, int itry, int& ierr) {
     if (j == 1) co_return;
     std::vector<cd> c(j);
     for (int iter = 0;;) {
-        zdev::dots(ws, nn, j - 1, a.d_v, ldc(), wd(0), nullptr, c.data());
+        zdev::dots<R>(ws, nn, j - 1, a.d_v, ldc(), wd(0), nullptr, c.data());
         zdev::update(ws, nn, j - 1, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
         if (bmat == 'G') {
             g_stats.nbx += 1;
@@ -107,12 +112,13 @@ Task ZSolver::getv0(bool initv, int j, int itry, int& ierr) {
 }
 
 // znaitr: extend a k-step Arnoldi factorization to k+npk steps (host-driven).
-Task ZSolver::naitr(int k, int npk, int& iinfo) {
+template <class R>
+Task ZSolverT<R>::naitr(int k, int npk, int& iinfo) {
     const int64_t nn = n;
     const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
     const int ldh = ncv;
     cd* h = workl + ih;
-    const double unfl = la::kSafmin;
+    const double unfl = Prec<R>::safmin;
     iinfo = 0;
     std::vector<cd> c(ncv + 1);
     for (int j = k + 1; j <= k + npk; ++j) {
@@ -159,7 +165,7 @@ Task ZSolver::naitr(int k, int npk, int& iinfo) {
             wnorm = cnorm(a.d_resid);
         }
         // CGS: h(1:j,j) = V' B r ; r -= V h (SRC/znaitr.f:567-590)
-        zdev::dots(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
+        zdev::dots<R>(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
         for (int i = 0; i < j; ++i) h[i + (size_t)(j - 1) * ldh] = c[i];
         zdev::update(ws, nn, j, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
         if (j > 1) h[(j - 1) + (size_t)(j - 2) * ldh] = cd(betaj, 0.0);
@@ -181,7 +187,7 @@ Task ZSolver::naitr(int k, int npk, int& iinfo) {
             g_stats.nrorth += 1;
             for (int iter = 0;;) {
                 const double rprev = rnorm;
-                zdev::dots(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
+                zdev::dots<R>(ws, nn, j, a.d_v, ldc(), wd(ipj), nullptr, c.data());
                 zdev::update(ws, nn, j, a.d_v, ldc(), c.data(), a.d_resid, a.d_resid);
                 for (int i = 0; i < j; ++i) h[i + (size_t)(j - 1) * ldh] += c[i];
                 co_await bnorm();
@@ -196,7 +202,7 @@ Task ZSolver::naitr(int k, int npk, int& iinfo) {
         }
     }
     // negligible subdiagonals (SRC/znaitr.f:812-830)
-    const double ulp = 2.0 * la::kEps, smlnum = la::kSafmin * ((double)n / ulp);
+    const double ulp = 2.0 * Prec<R>::eps, smlnum = Prec<R>::safmin * ((double)n / ulp);
     const int kp = k + npk;
     for (int i = std::max(1, k); i <= kp - 1; ++i) {
         double tst1 = zla::cabs1(h[(i - 1) + (size_t)(i - 1) * ldh]) + zla::cabs1(h[i + (size_t)i * ldh]);
@@ -207,9 +213,10 @@ Task ZSolver::naitr(int k, int npk, int& iinfo) {
     co_return;
 }
 
-Task ZSolver::run() {
+template <class R>
+Task ZSolverT<R>::run() {
     using la::Which;
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(Prec<R>::eps, 2.0 / 3.0);
     int nev = nev0;
     const int np0 = np, kplusp = nev0 + np0;
     int nconv = 0, iter = 0;
@@ -335,14 +342,37 @@ fail:
 }
 
 // ---------------------------------------------------------------- drivers ---
-static std::mutex g_zmu;
-static std::unordered_map<const void*, std::unique_ptr<ZSolver>> g_z;
+template class ZSolverT<double>;
+template class ZSolverT<float>;
 
+static std::mutex g_zmu;
+template <class R>
+static std::unordered_map<const void*, std::unique_ptr<ZSolverT<R>>>& zregistry() {
+    static std::unordered_map<const void*, std::unique_ptr<ZSolverT<R>>> m;
+    return m;
+}
+
+// znaupd (R = double) and cnaupd (R = float: complex64 n-length data, complex128
+// host work on a shadow of workl rounded into the caller's at every return).
+template <class R>
 static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
-                   cd* resid, int ncv, cd* v, int ldv, int* iparam, int* ipntr, cd* workd,
-                   cd* workl, int lworkl, double* rwork, int* info, const zdev::ZCsr* csr) {
+                   std::complex<R>* resid, int ncv, std::complex<R>* v, int ldv, int* iparam,
+                   int* ipntr, std::complex<R>* workd, std::complex<R>* workl, int lworkl,
+                   R* rwork, int* info, const zdev::ZCsr* csr) {
+    constexpr bool kShadow = !std::is_same_v<R, double>;
+    if (kShadow && csr) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
     std::lock_guard<std::mutex> lk(g_zmu);
-    ZSolver* S = nullptr;
+    auto& g_z = zregistry<R>();
+    ZSolverT<R>* S = nullptr;
+    const int wlen = 3 * ncv * ncv + 5 * ncv;
+    auto wl_out = [&]() {
+        if constexpr (kShadow)
+            for (int t = 0; t < wlen; ++t) workl[t] = std::complex<R>(S->wshadow[t]);
+    };
     if (*ido == 0) {
         ahip_ensure_seed();
         g_stats = Stats{};
@@ -366,8 +396,8 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             *ido = 99;
             return;
         }
-        if (*tol <= 0.0) *tol = la::kEps;
-        auto up = std::make_unique<ZSolver>();
+        if (*tol <= 0.0) *tol = Prec<R>::eps;
+        auto up = std::make_unique<ZSolverT<R>>();
         S = up.get();
         S->bmat = bmat[0];
         S->which = w;
@@ -380,7 +410,12 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         S->np = ncv - nev;
         S->lworkl = lworkl;
         S->info = *info;
-        std::memset(static_cast<void*>(workl), 0, sizeof(cd) * (size_t)(3 * ncv * ncv + 5 * ncv));
+        std::memset(static_cast<void*>(workl), 0, sizeof(std::complex<R>) * (size_t)wlen);
+        cd* wl = reinterpret_cast<cd*>(workl);
+        if constexpr (kShadow) {
+            S->wshadow.assign((size_t)wlen, cd(0.0));
+            wl = S->wshadow.data();
+        }
         S->ih = 0;  // SRC/znaupd.f:541-555
         S->iritz = S->ih + ncv * ncv;
         S->ibounds = S->iritz + ncv;
@@ -393,8 +428,8 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         ipntr[6] = S->iq + 1;
         ipntr[7] = S->ibounds + 1;
         ipntr[13] = S->iw + 1;
-        if (S->a.attach(2 * (int64_t)n, ncv, reinterpret_cast<double*>(resid),
-                        reinterpret_cast<double*>(v), 2 * ldv, reinterpret_cast<double*>(workd)) != 0 ||
+        if (S->a.attach(2 * (int64_t)n, ncv, reinterpret_cast<R*>(resid), reinterpret_cast<R*>(v),
+                        2 * ldv, reinterpret_cast<R*>(workd)) != 0 ||
             zdev::ws_create(S->ws, n, ncv, S->a.stream) != hipSuccess) {
             *info = -9999;
             *ido = 99;
@@ -404,8 +439,9 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
-        S->workl = workl;
-        S->rwork = rwork;
+        S->workl = wl;
+        S->rwork = nullptr;  // the engine needs no real workspace (zneigh's is internal)
+        (void)rwork;
         S->root.emplace(S->run());
         start_root(*S->root, S->ctx);
         g_z[v] = std::move(up);
@@ -420,9 +456,13 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
-        S->workl = workl;
-        S->rwork = rwork;
         const RciReq& r = S->ctx.req;
+        if constexpr (kShadow) {
+            if (r.ido == 3)  // the caller's shifts at workl(ipntr(14))
+                for (int t = 0; t < iparam[7]; ++t) S->wshadow[S->iw + t] = cd(workl[S->iw + t]);
+        } else {
+            S->workl = reinterpret_cast<cd*>(workl);
+        }
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) S->a.h2d_workd(2 * r.y, 2 * (int64_t)n);
     }
     for (;;) {
@@ -430,7 +470,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
         if (S->csr && (r.ido == -1 || r.ido == 1)) {
-            zdev::zcsr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            if constexpr (!kShadow) zdev::zcsr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
             continue;
         }
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
@@ -441,6 +481,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             if (r.bx >= 0) ipntr[2] = (int)(r.bx + 1);
         }
         S->a.sync();
+        wl_out();
         *ido = r.ido;
         return;
     }
@@ -455,18 +496,46 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
     *info = inf;
     S->a.download_all();
     S->a.sync();
+    wl_out();
     g_z.erase(v);
 }
 
 // zneupd (SRC/zneupd.f): Schur form of H, ztrsen reordering, V <- V*Qh and
 // Z = V(:,1:nconv) * X (ztrevc eigenvectors of T) on the device.
-static int z_eupd(bool rvec, char howmny, cd* d, cd* z, int ldz, cd sigma, cd* workev, char bmat,
-                  int n, const char* which_s, int nev, double tol, cd* resid, int ncv, cd* v,
-                  int ldv, int* iparam, int* ipntr, cd* workd, cd* workl, int lworkl) {
+// R = float (cneupd): complex128 host work on shadows of workl, d and workev.
+template <class R>
+static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R>* z, int ldz,
+                  cd sigma, std::complex<R>* workev_out, char bmat, int n, const char* which_s,
+                  int nev, double tol, std::complex<R>* resid, int ncv, std::complex<R>* v,
+                  int ldv, int* iparam, int* ipntr, std::complex<R>* workd,
+                  std::complex<R>* workl_in, int lworkl) {
     using la::Which;
+    using CT = std::complex<R>;
+    constexpr bool kShadow = !std::is_same_v<R, double>;
+    cd* workl = reinterpret_cast<cd*>(workl_in);
+    cd* d = reinterpret_cast<cd*>(d_out);
+    cd* workev = reinterpret_cast<cd*>(workev_out);
+    std::vector<cd> sh[3];  // workl, d, workev
+    if constexpr (kShadow) {
+        sh[0].assign(workl_in, workl_in + (lworkl > 0 ? lworkl : 0));
+        sh[1].assign((size_t)(nev > 0 ? nev : 0), cd(0.0));
+        sh[2].assign(2 * (size_t)(ncv > 0 ? ncv : 0), cd(0.0));
+        workl = sh[0].data();
+        d = sh[1].data();
+        workev = sh[2].data();
+    }
+    struct Back {
+        std::vector<cd>* sh;
+        CT* out[3];
+        ~Back() {
+            if constexpr (kShadow)
+                for (int k = 0; k < 3; ++k)
+                    for (size_t t = 0; t < sh[k].size(); ++t) out[k][t] = CT(sh[k][t]);
+        }
+    } back{sh, {workl_in, d_out, workev_out}};
     const int mode = iparam[6];
     int nconv = iparam[4];
-    const double eps23 = std::pow(la::kEps, 2.0 / 3.0);
+    const double eps23 = std::pow(Prec<R>::eps, 2.0 / 3.0);
     const Which which = la::parse_which(which_s);
     int ierr = 0;
     if (nconv <= 0) ierr = -14;
@@ -580,9 +649,9 @@ static int z_eupd(bool rvec, char howmny, cd* d, cd* z, int ldz, cd sigma, cd* w
         std::memcpy(static_cast<void*>(workev), wpur.data(), sizeof(cd) * nconv);
     }
     // ---- device: V <- V*Qh ; Z = V(:,1:nconv) * X (+ resid w^T)
-    Arrays a;
-    if (a.attach(2 * (int64_t)n, ncv, reinterpret_cast<double*>(resid), reinterpret_cast<double*>(v),
-                 2 * ldv, reinterpret_cast<double*>(workd)) != 0)
+    ArraysT<R> a;
+    if (a.attach(2 * (int64_t)n, ncv, reinterpret_cast<R*>(resid), reinterpret_cast<R*>(v), 2 * ldv,
+                 reinterpret_cast<R*>(workd)) != 0)
         return -9999;
     zdev::Ws ws;
     if (zdev::ws_create(ws, n, ncv, a.stream) != hipSuccess) {
@@ -590,34 +659,34 @@ static int z_eupd(bool rvec, char howmny, cd* d, cd* z, int ldz, cd sigma, cd* w
         return -9999;
     }
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(double) * a.d_ld, v, sizeof(cd) * ldv, sizeof(cd) * n, ncv,
+        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(CT) * ldv, sizeof(CT) * n, ncv,
                                hipMemcpyHostToDevice, a.stream);
         a.upload_resid();
     }
     const int64_t ldc = a.d_ld / 2;
     zdev::gemm(ws, n, a.d_v, ldc, ncv, ncv, Qh.data(), a.d_v, ldc);
     const bool zdevp = is_device_pointer(z);
-    double* zd = nullptr;
+    R* zd = nullptr;
     int64_t ldzd = ldc;
     if (zdevp) {
-        zd = reinterpret_cast<double*>(z);
+        zd = reinterpret_cast<R*>(z);
         ldzd = ldz;
     } else {
-        (void)hipMalloc(&zd, sizeof(cd) * (size_t)ldc * nconv);
+        (void)hipMalloc(&zd, sizeof(CT) * (size_t)ldc * nconv);
     }
     if (howmny == 'A') {
         zdev::gemm(ws, n, a.d_v, ldc, nconv, nconv, X.data(), zd, ldzd);
         if (type == SHIFTI) zdev::ger(ws, n, nconv, a.d_resid, wpur.data(), zd, ldzd);
     } else if (zd != a.d_v) {
-        (void)hipMemcpy2DAsync(zd, sizeof(cd) * ldzd, a.d_v, sizeof(double) * a.d_ld, sizeof(cd) * n, nconv,
+        (void)hipMemcpy2DAsync(zd, sizeof(CT) * ldzd, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, nconv,
                                hipMemcpyDeviceToDevice, a.stream);
     }
     if (!zdevp) {
-        (void)hipMemcpy2DAsync(z, sizeof(cd) * ldz, zd, sizeof(cd) * ldc, sizeof(cd) * n, nconv,
+        (void)hipMemcpy2DAsync(z, sizeof(CT) * ldz, zd, sizeof(CT) * ldc, sizeof(CT) * n, nconv,
                                hipMemcpyDeviceToHost, a.stream);
     }
     if (a.host_mode)
-        (void)hipMemcpy2DAsync(v, sizeof(cd) * ldv, a.d_v, sizeof(double) * a.d_ld, sizeof(cd) * n, ncv,
+        (void)hipMemcpy2DAsync(v, sizeof(CT) * ldv, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, ncv,
                                hipMemcpyDeviceToHost, a.stream);
     a.sync();
     if (!zdevp) (void)hipFree(zd);
@@ -672,6 +741,53 @@ void zneupd_(int* rvec, char const* howmny, int* select, a_dcomplex* d, a_dcompl
     *info = ahip::z_eupd(*rvec != 0, howmny[0], (cd*)d, (cd*)z, *ldz, s, (cd*)workev, bmat[0], *n, which,
                          *nev, *tol, (cd*)resid, *ncv, (cd*)v, *ldv, iparam, ipntr, (cd*)workd, (cd*)workl,
                          *lworkl);
+}
+
+// ---- complex64 family (ICB/arpack.h:10-11; SRC/cnaupd.f, SRC/cneupd.f) ----
+typedef std::complex<float> cf;
+
+void cnaupd_c(int* ido, char const* bmat, int n, char const* which, int nev, float tol,
+              a_fcomplex* resid, int ncv, a_fcomplex* v, int ldv, int* iparam, int* ipntr,
+              a_fcomplex* workd, a_fcomplex* workl, int lworkl, float* rwork, int* info) {
+    double t = tol;
+    ahip::z_aupd<float>(ido, bmat, n, which, nev, &t, (cf*)resid, ncv, (cf*)v, ldv, iparam, ipntr,
+                        (cf*)workd, (cf*)workl, lworkl, rwork, info, nullptr);
+}
+
+void cnaupd_(int* ido, char const* bmat, int* n, char const* which, int* nev, float* tol,
+             a_fcomplex* resid, int* ncv, a_fcomplex* v, int* ldv, int* iparam, int* ipntr,
+             a_fcomplex* workd, a_fcomplex* workl, int* lworkl, float* rwork, int* info, size_t,
+             size_t) {
+    double t = *tol;
+    ahip::z_aupd<float>(ido, bmat, *n, which, *nev, &t, (cf*)resid, *ncv, (cf*)v, *ldv, iparam,
+                        ipntr, (cf*)workd, (cf*)workl, *lworkl, rwork, info, nullptr);
+    *tol = (float)t;
+}
+
+void cneupd_c(int rvec, char const* howmny, int const* select, a_fcomplex* d, a_fcomplex* z,
+              int ldz, a_fcomplex sigma, a_fcomplex* workev, char const* bmat, int n,
+              char const* which, int nev, float tol, a_fcomplex* resid, int ncv, a_fcomplex* v,
+              int ldv, int* iparam, int* ipntr, a_fcomplex* workd, a_fcomplex* workl, int lworkl,
+              float* rwork, int* info) {
+    (void)select;
+    (void)rwork;
+    const cd s(__real__ sigma, __imag__ sigma);
+    *info = ahip::z_eupd<float>(rvec != 0, howmny[0], (cf*)d, (cf*)z, ldz, s, (cf*)workev, bmat[0],
+                                n, which, nev, tol, (cf*)resid, ncv, (cf*)v, ldv, iparam, ipntr,
+                                (cf*)workd, (cf*)workl, lworkl);
+}
+
+void cneupd_(int* rvec, char const* howmny, int* select, a_fcomplex* d, a_fcomplex* z, int* ldz,
+             a_fcomplex* sigma, a_fcomplex* workev, char const* bmat, int* n, char const* which,
+             int* nev, float* tol, a_fcomplex* resid, int* ncv, a_fcomplex* v, int* ldv,
+             int* iparam, int* ipntr, a_fcomplex* workd, a_fcomplex* workl, int* lworkl,
+             float* rwork, int* info, size_t, size_t, size_t) {
+    (void)select;
+    (void)rwork;
+    const cf sg = *reinterpret_cast<const cf*>(sigma);
+    *info = ahip::z_eupd<float>(*rvec != 0, howmny[0], (cf*)d, (cf*)z, *ldz, cd(sg), (cf*)workev,
+                                bmat[0], *n, which, *nev, *tol, (cf*)resid, *ncv, (cf*)v, *ldv,
+                                iparam, ipntr, (cf*)workd, (cf*)workl, *lworkl);
 }
 
 // ---- complex host kit exports (CPU-testable; tests/test_kit_z.py) ----

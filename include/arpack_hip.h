@@ -34,6 +34,10 @@
 #ifndef a_dcomplex
 #define a_dcomplex _Complex double
 #endif
+/* complex64 (arpackdef.h.in:39): C99 float _Complex */
+#ifndef a_fcomplex
+#define a_fcomplex _Complex float
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -114,6 +118,29 @@ void sneupd_(a_int* rvec, char const* howmny, a_int* select, float* dr, float* d
              char const* which, a_int* nev, float* tol, float* resid, a_int* ncv, float* v,
              a_int* ldv, a_int* iparam, a_int* ipntr, float* workd, float* workl, a_int* lworkl,
              a_int* info, size_t howmny_len, size_t bmat_len, size_t which_len);
+
+/* ---- complex64 (ICB/arpack.h:10-11; SRC/cnaupd.f, SRC/cneupd.f): complex64
+ *      n-length data and kernels, complex128 reductions and host work (workl
+ *      shadow), tol <= 0 -> slamch('EpsMach'); reverse communication on one GPU. */
+void cnaupd_c(a_int* ido, char const* bmat, a_int n, char const* which, a_int nev, float tol,
+              a_fcomplex* resid, a_int ncv, a_fcomplex* v, a_int ldv, a_int* iparam,
+              a_int* ipntr, a_fcomplex* workd, a_fcomplex* workl, a_int lworkl, float* rwork,
+              a_int* info);
+void cneupd_c(a_int rvec, char const* howmny, a_int const* select, a_fcomplex* d,
+              a_fcomplex* z, a_int ldz, a_fcomplex sigma, a_fcomplex* workev, char const* bmat,
+              a_int n, char const* which, a_int nev, float tol, a_fcomplex* resid, a_int ncv,
+              a_fcomplex* v, a_int ldv, a_int* iparam, a_int* ipntr, a_fcomplex* workd,
+              a_fcomplex* workl, a_int lworkl, float* rwork, a_int* info);
+void cnaupd_(a_int* ido, char const* bmat, a_int* n, char const* which, a_int* nev, float* tol,
+             a_fcomplex* resid, a_int* ncv, a_fcomplex* v, a_int* ldv, a_int* iparam,
+             a_int* ipntr, a_fcomplex* workd, a_fcomplex* workl, a_int* lworkl, float* rwork,
+             a_int* info, size_t bmat_len, size_t which_len);
+void cneupd_(a_int* rvec, char const* howmny, a_int* select, a_fcomplex* d, a_fcomplex* z,
+             a_int* ldz, a_fcomplex* sigma, a_fcomplex* workev, char const* bmat, a_int* n,
+             char const* which, a_int* nev, float* tol, a_fcomplex* resid, a_int* ncv,
+             a_fcomplex* v, a_int* ldv, a_int* iparam, a_int* ipntr, a_fcomplex* workd,
+             a_fcomplex* workl, a_int* lworkl, float* rwork, a_int* info, size_t howmny_len,
+             size_t bmat_len, size_t which_len);
 
 /* ---- Fortran symbols (SRC/dsaupd.f:182-186, SRC/dseupd.f:218-223): every
  *      argument by reference + hidden trailing CHARACTER lengths ---------------- */

@@ -225,30 +225,33 @@ def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
 
 
 def znaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode=1,
-                 bmat="I", bop=None, rvec=True, sigma=0.0 + 0.0j, return_state=False):
-    """Run znaupd_/zneupd_ (SRC/znaupd.f, SRC/zneupd.f) to completion."""
+                 bmat="I", bop=None, rvec=True, sigma=0.0 + 0.0j, return_state=False,
+                 prec="z"):
+    """Run znaupd_/zneupd_ (SRC/znaupd.f, SRC/zneupd.f) to completion
+    (prec="c": cnaupd_/cneupd_ on complex64 arrays)."""
     L = lib()
+    ct = np.complex64 if prec == "c" else np.complex128
+    rt = np.float32 if prec == "c" else np.float64
     ido = np.zeros(1, np.int32)
     info = np.zeros(1, np.int32)
-    resid = np.zeros(n, np.complex128) if v0 is None else np.array(v0, dtype=np.complex128,
-                                                                     copy=True)
+    resid = np.zeros(n, ct) if v0 is None else np.array(v0, dtype=ct, copy=True)
     info[0] = 0 if v0 is None else 1
     ldv = n
-    v = np.asfortranarray(np.zeros((ldv, ncv), np.complex128))
+    v = np.asfortranarray(np.zeros((ldv, ncv), ct))
     iparam = np.zeros(11, np.int32)
     ipntr = np.zeros(14, np.int32)
     iparam[0] = 1
     iparam[2] = mxiter
     iparam[6] = mode
-    workd = np.zeros(3 * n, np.complex128)
+    workd = np.zeros(3 * n, ct)
     lworkl = 3 * ncv * ncv + 5 * ncv
-    workl = np.zeros(lworkl, np.complex128)
-    rwork = np.zeros(ncv)
-    tolc = C.c_double(tol)
+    workl = np.zeros(lworkl, ct)
+    rwork = np.zeros(ncv, rt)
+    tolc = (C.c_float if prec == "c" else C.c_double)(tol)
     bm = bmat.encode()
     wh = which.encode()
     while True:
-        L.znaupd_(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
+        getattr(L, prec + "naupd_")(_pi(ido), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev), C.byref(tolc),
                   _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
                   _pd(workd), _pd(workl), _ci(lworkl), _pd(rwork), _pi(info),
                   C.c_size_t(1), C.c_size_t(2))
@@ -269,13 +272,13 @@ def znaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
     if info[0] < 0:
         return out
     nconv = int(iparam[4])
-    d = np.zeros(nev + 1, np.complex128)
-    z = np.asfortranarray(np.zeros((n, nev), np.complex128))
+    d = np.zeros(nev + 1, ct)
+    z = np.asfortranarray(np.zeros((n, nev), ct))
     select = np.zeros(ncv, np.int32)
-    workev = np.zeros(2 * ncv, np.complex128)
+    workev = np.zeros(2 * ncv, ct)
     ierr = np.zeros(1, np.int32)
-    sg = np.array([sigma], np.complex128)
-    L.zneupd_(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(d), _pd(z), _ci(n),
+    sg = np.array([sigma], ct)
+    getattr(L, prec + "neupd_")(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(d), _pd(z), _ci(n),
               _pd(sg), _pd(workev), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev),
               C.byref(tolc), _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
               _pd(workd), _pd(workl), _ci(lworkl), _pd(rwork), _pi(ierr),

@@ -4,7 +4,9 @@
  * beyond the header name.  Exit code 0 = all three solves correct.
  *   ds: dsaupd_c/dseupd_c on diag(1..N), nev 9, LM -> d = N-8 .. N
  *   dn: dnaupd_c/dneupd_c on the same diagonal
- *   zn: znaupd_c/zneupd_c on diag((k+1)(1+i)) -> d = (N-8 .. N)(1+i) */
+ *   zn: znaupd_c/zneupd_c on diag((k+1)(1+i)) -> d = (N-8 .. N)(1+i)
+ *   ss, sn, cn: the single-precision twins (sn is TESTS/bug_1315_single.c's
+ *   case, tol = 0, acceptance 0.1) */
 #include <complex.h>
 #include <math.h>
 #include <stdio.h>
@@ -19,6 +21,87 @@ static void dop(const double* x, double* y) {
 }
 static void zop(const double _Complex* x, double _Complex* y) {
     for (int i = 0; i < N; ++i) y[i] = x[i] * ((i + 1.0) + (i + 1.0) * I);
+}
+
+static void sop(const float* x, float* y) {
+    for (int i = 0; i < N; ++i) y[i] = (float)(i + 1) * x[i];
+}
+static void cop(const float _Complex* x, float _Complex* y) {
+    for (int i = 0; i < N; ++i) y[i] = x[i] * ((float)(i + 1) + (float)(i + 1) * I);
+}
+
+static int ss(void) {
+    const int nev = 9, ncv = 2 * nev + 1, lworkl = ncv * (ncv + 8);
+    float *resid = calloc(N, sizeof(float)), *v = calloc(N * ncv, sizeof(float));
+    float *workd = calloc(3 * N, sizeof(float)), *workl = calloc(lworkl, sizeof(float));
+    float d[9], *z = calloc(N * nev, sizeof(float));
+    int iparam[11] = {1, 0, 10 * N, 1, 0, 0, 1, 0, 0, 0, 0}, ipntr[11], select[19];
+    int ido = 0, info = 0;
+    do {
+        ssaupd_c(&ido, "I", N, "LM", nev, 1e-4f, resid, ncv, v, N, iparam, ipntr, workd, workl,
+                 lworkl, &info);
+        if (ido == -1 || ido == 1) sop(workd + ipntr[0] - 1, workd + ipntr[1] - 1);
+    } while (ido == -1 || ido == 1);
+    if (info < 0 || iparam[4] < nev) return printf("ss: info %d nconv %d\n", info, iparam[4]), 1;
+    sseupd_c(1, "A", select, d, z, N, 0.0f, "I", N, "LM", nev, 1e-4f, resid, ncv, v, N, iparam,
+             ipntr, workd, workl, lworkl, &info);
+    if (info < 0) return printf("ss: eupd info %d\n", info), 1;
+    for (int i = 0; i < nev; ++i)
+        if (fabsf(d[i] - (float)(N - (nev - 1) + i)) > 1e-2f)
+            return printf("ss: d[%d] = %f\n", i, d[i]), 1;
+    free(resid), free(v), free(workd), free(workl), free(z);
+    return 0;
+}
+
+static int sn(void) {
+    const int nev = 9, ncv = 2 * nev + 1, lworkl = 3 * ncv * ncv + 6 * ncv;
+    float *resid = calloc(N, sizeof(float)), *v = calloc(N * ncv, sizeof(float));
+    float *workd = calloc(3 * N, sizeof(float)), *workl = calloc(lworkl, sizeof(float));
+    float dr[10], di[10], *z = calloc((N + 1) * (nev + 1), sizeof(float)), workev[3 * 19];
+    int iparam[11] = {1, 0, 10 * N, 1, 0, 0, 1, 0, 0, 0, 0}, ipntr[14], select[3 * 19];
+    int ido = 0, info = 0;
+    do {
+        snaupd_c(&ido, "I", N, "LM", nev, 0.0f, resid, ncv, v, N, iparam, ipntr, workd, workl,
+                 lworkl, &info);
+        if (ido == -1 || ido == 1) sop(workd + ipntr[0] - 1, workd + ipntr[1] - 1);
+    } while (ido == -1 || ido == 1);
+    if (info < 0) return printf("sn: info %d\n", info), 1;
+    sneupd_c(1, "A", select, dr, di, z, N + 1, 0.0f, 0.0f, workev, "I", N, "LM", nev, 0.0f, resid,
+             ncv, v, N, iparam, ipntr, workd, workl, lworkl, &info);
+    for (int i = 0; i < nev; ++i)  /* TESTS/bug_1315_single.c acceptance */
+        if (fabsf(dr[i] - (float)(N - i)) > 1e-1f) return printf("sn: dr[%d] = %f\n", i, dr[i]), 1;
+    free(resid), free(v), free(workd), free(workl), free(z);
+    return 0;
+}
+
+static int cn(void) {
+    const int nev = 9, ncv = 2 * nev + 1, lworkl = ncv * (3 * ncv + 5);
+    float _Complex *resid = calloc(N, sizeof(float _Complex));
+    float _Complex *v = calloc(N * ncv, sizeof(float _Complex));
+    float _Complex *workd = calloc(3 * N, sizeof(float _Complex));
+    float _Complex *workl = calloc(lworkl, sizeof(float _Complex));
+    float _Complex d[10], *z = calloc(N * nev, sizeof(float _Complex)), workev[2 * 19];
+    float rwork[19];
+    int iparam[11] = {1, 0, 10 * N, 1, 0, 0, 1, 0, 0, 0, 0}, ipntr[14], select[19];
+    int ido = 0, info = 0;
+    do {
+        cnaupd_c(&ido, "I", N, "LM", nev, 1e-4f, resid, ncv, v, N, iparam, ipntr, workd, workl,
+                 lworkl, rwork, &info);
+        if (ido == -1 || ido == 1) cop(workd + ipntr[0] - 1, workd + ipntr[1] - 1);
+    } while (ido == -1 || ido == 1);
+    if (info < 0 || iparam[4] < nev) return printf("cn: info %d nconv %d\n", info, iparam[4]), 1;
+    cneupd_c(1, "A", select, d, z, N, 0.0f, workev, "I", N, "LM", nev, 1e-4f, resid, ncv, v, N,
+             iparam, ipntr, workd, workl, lworkl, rwork, &info);
+    if (info < 0) return printf("cn: eupd info %d\n", info), 1;
+    for (int i = 0; i < nev; ++i) {
+        int hit = 0;
+        for (int k = 0; k < nev; ++k)
+            hit |= fabsf(crealf(d[k]) - (float)(N - i)) < 1e-2f &&
+                   fabsf(cimagf(d[k]) - (float)(N - i)) < 1e-2f;
+        if (!hit) return printf("cn: %d missing\n", N - i), 1;
+    }
+    free(resid), free(v), free(workd), free(workl), free(z);
+    return 0;
 }
 
 static int ds(void) {
@@ -97,12 +180,12 @@ static int zn(void) {
 }
 
 int main(void) {
-    const int a = ds(), b = dn(), c = zn();
+    const int a = ds(), b = dn(), c = zn(), e = ss(), f = sn(), g = cn();
     int nopx, nbx, nrorth, nitref, nrstrt;
     float t[26];
     stat_c(&nopx, &nbx, &nrorth, &nitref, &nrstrt, t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6,
            t + 7, t + 8, t + 9, t + 10, t + 11, t + 12, t + 13, t + 14, t + 15, t + 16, t + 17,
            t + 18, t + 19, t + 20, t + 21, t + 22, t + 23, t + 24, t + 25);
-    printf("ds %d dn %d zn %d (last solve: nopx %d)\n", a, b, c, nopx);
-    return a | b | c;
+    printf("ds %d dn %d zn %d ss %d sn %d cn %d (last solve: nopx %d)\n", a, b, c, e, f, g, nopx);
+    return a | b | c | e | f | g;
 }

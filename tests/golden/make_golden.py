@@ -100,7 +100,7 @@ def nonsym_fixtures():
 
 
 def run_z(name, mat, spec, nev, ncv, which, tol, mxiter=300, mode=1, sigma=0j, keep_z=True,
-          **extra):
+          prec="z", **extra):
     """znaupd/zneupd fixture (SRC/znaupd.f, SRC/zneupd.f).  Mode 3 applies
     OP = inv(A - sigma I) with a sparse LU on the host, as a caller would."""
     import scipy.sparse as sp
@@ -109,13 +109,16 @@ def run_z(name, mat, spec, nev, ncv, which, tol, mxiter=300, mode=1, sigma=0j, k
     n = len(rowptr) - 1
     A = sp.csr_matrix((val, col, rowptr), shape=(n, n))
     v0 = M.dlarnv_uniform(2 * n)[0].view(np.complex128)
+    if prec == "c":
+        v0 = v0.astype(np.complex64)
+        extra["prec"] = "c"
     if mode == 1:
         op = lambda x, *_: A @ x  # noqa: E731
     else:
         lu = spl.splu((A - sigma * sp.identity(n, format="csr")).tocsc())
         op = lambda x, *_: lu.solve(x)  # noqa: E731
     r = ref.znaupd_solve(op, n, nev, ncv, which, tol, v0=v0, mxiter=mxiter, mode=mode,
-                         sigma=sigma, return_state=True)
+                         sigma=sigma, return_state=True, prec=prec)
     assert r["info"] >= 0, r
     o = ncv * ncv
     out = dict(spec=np.array(spec), nev=nev, ncv=ncv, which=np.array(which), tol=tol,
@@ -225,6 +228,13 @@ def single_fixtures():
            keep_z=True, prec="s")
     run_ns("s7_convdiff_lr", M.convdiff2d(30, 10.0), ["convdiff2d", 30, 10.0], 6, 30, "LR", 1e-5,
            keep_z=True, mxiter=3000, prec="s")
+    # complex64 (cnaupd/cneupd; EXAMPLES/SIMPLE/cnsimp.f family)
+    run_z("c1_icb_cn", M.zdiag_icb(1000), ["zdiag_icb", 1000], 9, 19, "LM", 1e-4, mxiter=10000,
+          prec="c")
+    zr = M.zrandom(2000, 20, 5, 100.0)
+    run_z("c2_zrandom_lm", zr, ["zrandom", 2000, 20, 5, 100.0], 6, 20, "LM", 1e-5, prec="c")
+    run_z("c3_zrandom_si", zr, ["zrandom", 2000, 20, 5, 100.0], 6, 20, "LM", 1e-5, mode=3,
+          sigma=0j, prec="c")
 
 
 if __name__ == "__main__":

@@ -22,9 +22,10 @@ def test_header_symbols_exported(pkg):
 def test_reference_icb_names_covered():
     """Every ICB symbol of the implemented families is declared (ICB/arpack.h:10-21)."""
     names = _declared()
-    for s in ("dsaupd_c", "dseupd_c", "dsaupd_", "dseupd_", "dnaupd_c", "dneupd_c", "dnaupd_",
-              "dneupd_", "znaupd_c", "zneupd_c", "znaupd_", "zneupd_", "stat_c", "debug_c",
-              "sstats_c"):
+    for fam in ("ds", "dn", "zn", "ss", "sn", "cn"):  # all twelve ICB entry points
+        for s in (fam + "aupd_c", fam + "eupd_c", fam + "aupd_", fam + "eupd_"):
+            assert s in names, s
+    for s in ("stat_c", "debug_c", "sstats_c"):
         assert s in names
 
 

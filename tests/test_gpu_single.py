@@ -160,3 +160,52 @@ def test_device_slarnv_bitwise(pkg, seed):
                                      xd.ptr) == 0
     y, s_out = M.dlarnv_uniform(1000)
     assert np.array_equal(xd.numpy(), y) and tuple(isd) == tuple(s_out)
+
+
+def _zmat(spec):
+    if str(spec[0]) == "zdiag_icb":
+        return M.zdiag_icb(int(spec[1]))
+    return M.zrandom(int(spec[1]), int(spec[2]), int(spec[3]), float(spec[4]))
+
+
+@pytest.mark.parametrize("name", ["c1_icb_cn", "c2_zrandom_lm", "c3_zrandom_si"])
+def test_cnaupd(pkg, golden, name):
+    """complex64 family (cnaupd_c / cneupd_c) against the reference's cnaupd_/cneupd_."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+    g = golden(name)
+    rp, col, val = _zmat(g["spec"])
+    n = len(rp) - 1
+    A = sp.csr_matrix((val, col, rp), shape=(n, n))
+    mode = int(g["mode"])
+    sigma = complex(g["sigma"])
+    lu = spl.splu((A - sigma * sp.identity(n, format="csr")).tocsc()) if mode == 3 else None
+    s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=mode,
+                 mxiter=int(g["mxiter"]), v0=g["v0"], prec="c")
+    while True:
+        ido = s.aupd()
+        if ido in (-1, 1):
+            x = s.slice(0).astype(np.complex128)
+            s.slice(1)[:] = A @ x if mode == 1 else lu.solve(x)
+        elif ido == 99:
+            break
+        else:
+            raise AssertionError(ido)
+    _counts(g, s)
+    d, z, nconv = s.eupd(sigma=sigma)
+    assert d.dtype == np.complex64
+    dref = g["d"].astype(np.complex128)
+    scale = np.abs(A).sum(axis=0).max()
+    for x in dref:
+        assert np.abs(d.astype(np.complex128) - x).min() <= _tol(g) * scale, (x, d)
+    zz = z.astype(np.complex128)
+    dd = d.astype(np.complex128)
+    ours = max(np.linalg.norm(A @ zz[:, k] - dd[k] * zz[:, k]) / (scale * np.linalg.norm(zz[:, k]))
+               for k in range(nconv))
+    zr = g["z"].astype(np.complex128)
+    theirs = max(np.linalg.norm(A @ zr[:, k] - dref[k] * zr[:, k]) /
+                 (scale * np.linalg.norm(zr[:, k])) for k in range(len(dref)))
+    assert ours <= max(10 * theirs, 1e-6), (ours, theirs)
+    if name == "c1_icb_cn":  # TESTS/icb_arpack_c.c's zn acceptance, at float level
+        for x in np.arange(1000 - 8, 1001) * (1 + 1j):
+            assert np.abs(dd - x).min() <= 1e-2
