@@ -26,8 +26,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* a_int: int (LP64, libarpack_hip.so) or int64_t (ILP64, libarpack_hip64.so: define
+ * a_int as int64_t before including, as arpackdef.h.in:6-14 does with INTERFACE64=1) */
 #ifndef a_int
-#define a_int int /* LP64, arpackdef.h.in:6-14 with INTERFACE64=0 */
+#define a_int int
 #endif
 
 /* complex128 as the ICB passes it (arpackdef.h.in:40-41): C99 double _Complex */
@@ -188,7 +190,8 @@ void debug_c(a_int logfil, a_int ndigit, a_int mgetv0, a_int msaupd, a_int msaup
              a_int mngets, a_int mneupd, a_int mcaupd, a_int mcaup2, a_int mcaitr,
              a_int mceigh, a_int mcapps, a_int mcgets, a_int mceupd);
 
-/* ---- native extension ---------------------------------------------------------- */
+/* ---- native extension ---------------------------------------------------------- *
+ * LP64 (plain int) in both builds: only the reference ABI above follows a_int. */
 typedef struct arpack_hip_csr arpack_hip_csr;
 
 /* Version / capability probe: returns a static string. */
@@ -221,28 +224,28 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y);
 /* dsaupd_c with OP = A served on the GPU: same arguments and results as
  * dsaupd_c (mode 1, bmat 'I'), but returns only with ido = 99 (or ido = 3 when
  * iparam[0] = 0 asks for user shifts). */
-void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, a_int* ido, char const* bmat, a_int n,
-                           char const* which, a_int nev, double tol, double* resid, a_int ncv,
-                           double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
-                           double* workl, a_int lworkl, a_int* info);
+void arpack_hip_dsaupd_csr(const arpack_hip_csr* A, int* ido, char const* bmat, int n,
+                           char const* which, int nev, double tol, double* resid, int ncv,
+                           double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                           double* workl, int lworkl, int* info);
 
 /* Same, but parks after at most `max_cycles` further restart cycles with
  * ido = 98 (tol by reference, as dsaupd_).  Call again with ido = 98 to
  * continue; ido = 99 when the solve is complete.  Used to time exactly K
  * restart cycles (bench.py); max_cycles < 0 never parks. */
-void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_int* ido,
-                                  char const* bmat, a_int n, char const* which, a_int nev,
-                                  double* tol, double* resid, a_int ncv, double* v, a_int ldv,
-                                  a_int* iparam, a_int* ipntr, double* workd, double* workl,
-                                  a_int lworkl, a_int* info);
+void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* ido,
+                                  char const* bmat, int n, char const* which, int nev,
+                                  double* tol, double* resid, int ncv, double* v, int ldv,
+                                  int* iparam, int* ipntr, double* workd, double* workl,
+                                  int lworkl, int* info);
 
 /* dnaupd with OP = A served on the GPU (mode 1), cycle-parked like
  * arpack_hip_dsaupd_csr_cycles (SRC/dnaupd.f semantics, ipntr[14]). */
-void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, a_int max_cycles, a_int* ido,
-                                  char const* bmat, a_int n, char const* which, a_int nev,
-                                  double* tol, double* resid, a_int ncv, double* v, a_int ldv,
-                                  a_int* iparam, a_int* ipntr, double* workd, double* workl,
-                                  a_int lworkl, a_int* info);
+void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* ido,
+                                  char const* bmat, int n, char const* which, int nev,
+                                  double* tol, double* resid, int ncv, double* v, int ldv,
+                                  int* iparam, int* ipntr, double* workd, double* workl,
+                                  int lworkl, int* info);
 
 /* Complex CSR operator (rowptr int64[n+1], col int32[nnz], val complex128[nnz]
  * interleaved) and the complex random operator of BASELINE config 5 (SURVEY.md
@@ -259,11 +262,11 @@ int arpack_hip_zcsr_download(const arpack_hip_zcsr* A, int64_t* rowptr, int32_t*
                              double* val);
 int arpack_hip_zcsr_spmv(const arpack_hip_zcsr* A, const double* x, double* y);
 /* znaupd (mode 1) with OP = A served on the GPU; returns with ido = 99. */
-void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* A, a_int* ido, char const* bmat, a_int n,
-                            char const* which, a_int nev, double* tol, a_dcomplex* resid,
-                            a_int ncv, a_dcomplex* v, a_int ldv, a_int* iparam, a_int* ipntr,
-                            a_dcomplex* workd, a_dcomplex* workl, a_int lworkl, double* rwork,
-                            a_int* info);
+void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* A, int* ido, char const* bmat, int n,
+                            char const* which, int nev, double* tol, a_dcomplex* resid,
+                            int ncv, a_dcomplex* v, int ldv, int* iparam, int* ipntr,
+                            a_dcomplex* workd, a_dcomplex* workl, int lworkl, double* rwork,
+                            int* info);
 
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
@@ -307,41 +310,41 @@ int arpack_hip_dist_rows(arpack_hip_dist** D, int64_t nloc, int64_t row0, int64_
  * PARPACK/EXAMPLES/MPI/pdsdrv1.f.  Post-processing: arpack_hip_pdseupd_c
  * (ICB/parpack.h:21; collective B-norm for bmat = 'G', PARPACK/SRC/MPI/pdseupd.f:456)
  * and arpack_hip_pdneupd_c (ICB/parpack.h:27; no collective). */
-void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
-                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
-                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
-                          double* workl, a_int lworkl, a_int* info);
-void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, a_int* ido, char const* bmat, a_int n,
-                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
-                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
-                          double* workl, a_int lworkl, a_int* info);
-void arpack_hip_pdseupd_c(const arpack_hip_dist* D, a_int rvec, char const* howmny,
-                          a_int const* select, double* d, double* z, a_int ldz, double sigma,
-                          char const* bmat, a_int n, char const* which, a_int nev, double tol,
-                          double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
-                          a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info);
-void arpack_hip_pdneupd_c(const arpack_hip_dist* D, a_int rvec, char const* howmny,
-                          a_int const* select, double* dr, double* di, double* z, a_int ldz,
-                          double sigmar, double sigmai, double* workev, char const* bmat, a_int n,
-                          char const* which, a_int nev, double tol, double* resid, a_int ncv,
-                          double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
-                          double* workl, a_int lworkl, a_int* info);
+void arpack_hip_pdsaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info);
+void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info);
+void arpack_hip_pdseupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, double* d, double* z, int ldz, double sigma,
+                          char const* bmat, int n, char const* which, int nev, double tol,
+                          double* resid, int ncv, double* v, int ldv, int* iparam,
+                          int* ipntr, double* workd, double* workl, int lworkl, int* info);
+void arpack_hip_pdneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, double* dr, double* di, double* z, int ldz,
+                          double sigmar, double sigmai, double* workev, char const* bmat, int n,
+                          char const* which, int nev, double tol, double* resid, int ncv,
+                          double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                          double* workl, int lworkl, int* info);
 /* Halo plan (host only, CPU-testable): tab = [row0, nloc, min col, max col] per
  * rank (4*P doubles, global indices); out = {halo_lo, halo_hi, send_lo, send_hi}
  * of rank r.  Returns 0, -3 (blocks not contiguous) or -4 (halo too wide). */
 int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out);
 /* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
  * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
-void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
-                                   char const* bmat, a_int n, char const* which, a_int nev,
-                                   double* tol, double* resid, a_int ncv, double* v, a_int ldv,
-                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
-                                   a_int lworkl, a_int* info);
-void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, a_int max_cycles, a_int* ido,
-                                   char const* bmat, a_int n, char const* which, a_int nev,
-                                   double* tol, double* resid, a_int ncv, double* v, a_int ldv,
-                                   a_int* iparam, a_int* ipntr, double* workd, double* workl,
-                                   a_int lworkl, a_int* info);
+void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,
+                                   char const* bmat, int n, char const* which, int nev,
+                                   double* tol, double* resid, int ncv, double* v, int ldv,
+                                   int* iparam, int* ipntr, double* workd, double* workl,
+                                   int lworkl, int* info);
+void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,
+                                   char const* bmat, int n, char const* which, int nev,
+                                   double* tol, double* resid, int ncv, double* v, int ldv,
+                                   int* iparam, int* ipntr, double* workd, double* workl,
+                                   int lworkl, int* info);
 
 /* Per-kernel-class device timing with hipEvents on the launch stream.
  * Classes: 0 SpMV, 1 CGS dots, 2 update(+fused DGKS dots), 3 V*Q, 4 place,
