@@ -192,6 +192,17 @@ int64_t scan_counts(int64_t rows, int64_t* counts_then_rowptr_tmp, int64_t* rowp
     return nnz;
 }
 
+// LDS x-window tables, then the SELL-64 layout over them (default kernel);
+// matrices whose rows span more than a window keep the CSR-stream kernel.
+void analyse_window_sell(arpack_hip_csr* A, int64_t ncols) {
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) != 0) return;
+    A->A.kernel = ahip::dev::kCsrWVecX;
+    if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
+        A->A.kernel = ahip::dev::kCsrSell;
+        A->A.s_unroll = 4;
+    }
+}
+
 arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, int32_t* col, double* val) {
     auto* A = new arpack_hip_csr;
     A->rowptr = rp;
@@ -205,7 +216,7 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
     if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVecX;
+    analyse_window_sell(A, ncols);
     return A;
 }
 
@@ -237,9 +248,17 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     (void)hipFree(A->val);
     if (A->rblk) (void)hipFree(A->rblk);
     if (A->win) (void)hipFree(A->win);
+    if (A->sell) (void)hipFree(A->sell);
     if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
     A->A.w_colw = nullptr;
     delete A;
+}
+
+// SELL-64 layout statistics (0 slices if it was never built)
+int arpack_hip_csr_sell_info(const arpack_hip_csr* A, int64_t* nslices, int64_t* padded) {
+    *nslices = A->A.s_nslices;
+    *padded = A->A.s_padded;
+    return A->sell ? 0 : -1;
 }
 
 int arpack_hip_csr_info(const arpack_hip_csr* A, int64_t* n, int64_t* nnz) {
@@ -263,6 +282,12 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
     if (kernel == ahip::dev::kCsrVector) {
         A->A.kernel = kernel;
+        return 0;
+    }
+    if (kernel == ahip::dev::kCsrSell) {  // tile selects the unroll (4, 8, 16)
+        if (!A->sell && ahip::dev::csr_build_sell(A->A, &A->sell) != 0) return -1;
+        A->A.kernel = kernel;
+        A->A.s_unroll = (tile >= 2 && tile <= 8) ? tile : 4;  // 5, 7: two slices per wave
         return 0;
     }
     if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVecP4) {
@@ -408,11 +433,14 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     (void)hipDeviceSynchronize();
     A->ncols = ncols;
     if (A->win) (void)hipFree(A->win);
+    if (A->sell) (void)hipFree(A->sell);
     if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
     A->A.w_colw = nullptr;
     A->win = nullptr;
+    A->sell = nullptr;
+    A->A.s_val = nullptr;
     A->A.w_nsb = 0;
     A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) == 0) A->A.kernel = ahip::dev::kCsrWVecX;
+    analyse_window_sell(A, ncols);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

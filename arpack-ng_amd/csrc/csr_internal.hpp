@@ -13,6 +13,7 @@ struct arpack_hip_csr {
     int64_t ncols = 0;
     int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
     void* win = nullptr;      // LDS-window superblock tables (owned)
+    void* sell = nullptr;     // SELL-64 slices + values (owned, built on demand)
 };
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV

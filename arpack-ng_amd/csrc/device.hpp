@@ -142,6 +142,16 @@ struct Csr {
     const int32_t* w_sb_span = nullptr;   // window length
     int64_t w_nsb = 0;
     const uint16_t* w_colw = nullptr;     // col - c0(superblock), 16 bit (owned separately)
+    // SELL-64 slices inside each window superblock (kCsrSell, csr_build_sell):
+    // the superblock's rows sorted by length, 64 per slice (one per lane),
+    // entries stored column-step-major so a wave reads 64 consecutive values
+    const int64_t* s_sb_slice0 = nullptr;  // first slice of each superblock (+ end)
+    const int64_t* s_ptr = nullptr;        // slice start in s_val / s_colw (+ end)
+    const int32_t* s_row = nullptr;        // 64 per slice: global row, -1 = padding lane
+    const double* s_val = nullptr;
+    const uint16_t* s_colw = nullptr;
+    int64_t s_nslices = 0, s_padded = 0;
+    int s_unroll = 8;                      // column steps per chunk (4, 8 or 16)
 };
 enum CsrKernel : int {
     kCsrVector = 0,
@@ -155,7 +165,11 @@ enum CsrKernel : int {
     kCsrWVecX = 8,  // wvec with the XCD-contiguous superblock order
     kCsrWVecP3 = 9,  // XCD order, 3 row passes in flight
     kCsrWVecP4 = 10, // XCD order, 4 row passes in flight
+    kCsrSell = 11,   // SELL-64 slices (length-sorted rows) over the x windows
 };
+// Build the SELL-64 layout from a matrix with window tables; *owned receives the
+// single device allocation.  0 on success.
+int csr_build_sell(Csr& A, void** owned);
 // Superblock analysis for the LDS x-window kernel; -1 if some row's column
 // span exceeds the window (then the stream kernel is used).  *owned receives
 // the single device allocation holding the tables.

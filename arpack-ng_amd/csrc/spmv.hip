@@ -371,6 +371,183 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvecp(
     }
 }
 
+// SELL-64 over the LDS x window: one workgroup per superblock, each wave takes
+// whole slices (lane = row); a column step is one coalesced 512-B val load and
+// one 128-B colw load per wave.  Each row is summed sequentially in its CSR
+// (column) order.
+template <int U, bool XCD>
+__global__ __launch_bounds__(kWinThreads) void k_csr_sell(
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
+    const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y) {
+    // unfused multiply-add: each row is summed exactly as a sequential CSR loop
+    // (y_i = ((0 + a_i1 x_1) + a_i2 x_2) + ...) -- SciPy's csr_matvec, the OP
+    // the reference's RCI callers use -- so y is bitwise the CPU result
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xw = lds;
+    constexpr int NW = kWinThreads / 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t sb = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t c0 = sb_c0[sb];
+    const int span = sb_span[sb];
+    const int64_t s0 = sb_slice0[sb], s1 = sb_slice0[sb + 1];
+    // double-buffered column steps: chunk k+U (or the next slice's first chunk)
+    // is in flight while chunk k is consumed; the first chunk is issued before
+    // the x window is staged so the HBM stream starts with the x loads
+    struct Chunk {
+        double v[U];
+        int c[U];
+    };
+    auto load = [&](Chunk& ch, int64_t base, int w, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < w;
+            ch.v[u] = in ? sval[base + (int64_t)(k0 + u) * 64 + lane] : 0.0;
+            ch.c[u] = in ? (int)scolw[base + (int64_t)(k0 + u) * 64 + lane] : 0;
+        }
+    };
+    int64_t s = s0 + wave;
+    int64_t base = 0;
+    int w = 0;
+    Chunk cur, nxt;
+    if (s < s1) {
+        base = sptr[s];
+        w = (int)((sptr[s + 1] - base) >> 6);
+        load(cur, base, w, 0);
+    }
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    __syncthreads();
+    for (; s < s1; s += NW) {
+        const int row = srow[s * 64 + lane];
+        const int64_t sn = s + NW;
+        int64_t nbase = 0;
+        int nw = 0;
+        if (sn < s1) {
+            nbase = sptr[sn];
+            nw = (int)((sptr[sn + 1] - nbase) >> 6);
+        }
+        double acc = 0.0;
+        int k = 0;
+        do {
+            if (k + U < w) load(nxt, base, w, k + U);
+            else if (sn < s1) load(nxt, nbase, nw, 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += cur.v[u] * xw[cur.c[u]];
+            cur = nxt;
+            k += U;
+        } while (k < w);
+        if (row >= 0) y[row] = acc;
+        base = nbase;
+        w = nw;
+    }
+}
+
+// Two slices per wave at once (s and s + NW): twice the independent column
+// streams per wave, each double-buffered.
+template <int U, bool XCD>
+__global__ __launch_bounds__(kWinThreads) void k_csr_sell2(
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
+    const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xw = lds;
+    constexpr int NW = kWinThreads / 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t sb = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t c0 = sb_c0[sb];
+    const int span = sb_span[sb];
+    const int64_t s0 = sb_slice0[sb], s1 = sb_slice0[sb + 1];
+    struct Chunk {
+        double v[U];
+        int c[U];
+    };
+    auto load = [&](Chunk& ch, int64_t base, int w, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < w;
+            ch.v[u] = in ? sval[base + (int64_t)(k0 + u) * 64 + lane] : 0.0;
+            ch.c[u] = in ? (int)scolw[base + (int64_t)(k0 + u) * 64 + lane] : 0;
+        }
+    };
+    auto geom = [&](int64_t sl, int64_t& base, int& w) {
+        base = 0;
+        w = 0;
+        if (sl < s1) {
+            base = sptr[sl];
+            w = (int)((sptr[sl + 1] - base) >> 6);
+        }
+    };
+    int64_t s = s0 + wave;
+    int64_t ba, bb;
+    int wa, wb;
+    geom(s, ba, wa);
+    geom(s + NW, bb, wb);
+    Chunk ca, cb, na, nb;
+    load(ca, ba, wa, 0);
+    load(cb, bb, wb, 0);
+    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    __syncthreads();
+    for (; s < s1; s += 2 * NW) {
+        const int ra = srow[s * 64 + lane];
+        const int rb = s + NW < s1 ? srow[(s + NW) * 64 + lane] : -1;
+        int64_t nba, nbb;
+        int nwa, nwb;
+        geom(s + 2 * NW, nba, nwa);
+        geom(s + 3 * NW, nbb, nwb);
+        double acc_a = 0.0, acc_b = 0.0;
+        const int w = wa > wb ? wa : wb;
+        int k = 0;
+        do {
+            const bool last = k + U >= w;
+            if (k + U < wa) load(na, ba, wa, k + U);
+            else if (last) load(na, nba, nwa, 0);
+            if (k + U < wb) load(nb, bb, wb, k + U);
+            else if (last) load(nb, nbb, nwb, 0);
+            if (k < wa) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc_a += ca.v[u] * xw[ca.c[u]];
+            }
+            if (k < wb) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc_b += cb.v[u] * xw[cb.c[u]];
+            }
+            if (k + U < wa) ca = na;
+            if (k + U < wb) cb = nb;
+            k += U;
+        } while (k < w);
+        // the chunks left in na / nb are the next pair's first chunks
+        ca = na;
+        cb = nb;
+        if (ra >= 0) y[ra] = acc_a;
+        if (rb >= 0) y[rb] = acc_b;
+        ba = nba;
+        wa = nwa;
+        bb = nbb;
+        wb = nwb;
+    }
+}
+
+// fill the SELL arrays: one 64-thread block per slice, lane = row of the slice
+__global__ void k_sell_fill(const int64_t* __restrict__ sptr, const int32_t* __restrict__ srow,
+                            const int64_t* __restrict__ rp, const uint16_t* __restrict__ colw,
+                            const double* __restrict__ val, uint16_t* __restrict__ scolw,
+                            double* __restrict__ sval) {
+    const int64_t s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t base = sptr[s];
+    const int w = (int)((sptr[s + 1] - base) >> 6);
+    const int row = srow[s * 64 + lane];
+    const int64_t b = row >= 0 ? rp[row] : 0, len = row >= 0 ? rp[row + 1] - rp[row] : 0;
+    for (int k = 0; k < w; ++k) {
+        const bool in = k < len;
+        sval[base + (int64_t)k * 64 + lane] = in ? val[b + k] : 0.0;
+        scolw[base + (int64_t)k * 64 + lane] = in ? colw[b + k] : (uint16_t)0;
+    }
+}
+
 __global__ void k_colw(const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
                        const int64_t* __restrict__ sb_c0, const int64_t* __restrict__ rp,
                        const int32_t* __restrict__ col, uint16_t* __restrict__ colw) {
@@ -478,6 +655,71 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     return 0;
 }
 
+int csr_build_sell(Csr& A, void** owned) {
+    if (!A.w_colw || A.w_nsb <= 0 || A.n >= (int64_t)INT32_MAX) return -1;
+    const int64_t n = A.n, nsb = A.w_nsb;
+    std::vector<int64_t> rp(n + 1), sb_tile0(nsb + 1);
+    (void)hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(sb_tile0.data(), A.w_sb_tile0, sizeof(int64_t) * (nsb + 1), hipMemcpyDeviceToHost);
+    std::vector<int64_t> tiles((size_t)sb_tile0[nsb] + 1);
+    (void)hipMemcpy(tiles.data(), A.w_tiles, sizeof(int64_t) * tiles.size(), hipMemcpyDeviceToHost);
+    std::vector<int64_t> sb_slice0{0}, sptr{0};
+    std::vector<int32_t> srow;
+    std::vector<int32_t> order;
+    for (int64_t b = 0; b < nsb; ++b) {
+        const int64_t R0 = tiles[sb_tile0[b]], R1 = tiles[sb_tile0[b + 1]];
+        order.resize((size_t)(R1 - R0));
+        for (int64_t r = R0; r < R1; ++r) order[r - R0] = (int32_t)r;
+        // longest rows first (stable): a slice's width is its first row's length
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t c) {
+            return rp[a + 1] - rp[a] > rp[c + 1] - rp[c];
+        });
+        for (size_t q = 0; q < order.size(); q += 64) {
+            const int64_t w = rp[order[q] + 1] - rp[order[q]];
+            for (size_t l = 0; l < 64; ++l) srow.push_back(q + l < order.size() ? order[q + l] : -1);
+            sptr.push_back(sptr.back() + 64 * w);
+        }
+        sb_slice0.push_back((int64_t)sptr.size() - 1);
+    }
+    const int64_t ns = (int64_t)sptr.size() - 1, padded = sptr.back();
+    const size_t b0 = sizeof(int64_t) * sb_slice0.size(), b1 = sizeof(int64_t) * sptr.size(),
+                 b2 = sizeof(int32_t) * srow.size(), bv = sizeof(double) * (size_t)(padded ? padded : 1),
+                 bc = sizeof(uint16_t) * (size_t)(padded ? padded : 1);
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char* d = nullptr;
+    if (hipMalloc(&d, up(b0) + up(b1) + up(b2) + up(bv) + up(bc))) return -2;
+    char* p = d;
+    auto take = [&](size_t bytes) {
+        char* r = p;
+        p += up(bytes);
+        return r;
+    };
+    auto* d0 = (int64_t*)take(b0);
+    auto* d1 = (int64_t*)take(b1);
+    auto* d2 = (int32_t*)take(b2);
+    auto* dv = (double*)take(bv);
+    auto* dc = (uint16_t*)take(bc);
+    (void)hipMemcpy(d0, sb_slice0.data(), b0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d1, sptr.data(), b1, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d2, srow.data(), b2, hipMemcpyHostToDevice);
+    if (ns > 0)
+        hipLaunchKernelGGL(k_sell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d1, d2, A.rowptr,
+                           A.w_colw, A.val, dc, dv);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(d);
+        return -2;
+    }
+    A.s_sb_slice0 = d0;
+    A.s_ptr = d1;
+    A.s_row = d2;
+    A.s_val = dv;
+    A.s_colw = dc;
+    A.s_nslices = ns;
+    A.s_padded = padded;
+    *owned = d;
+    return 0;
+}
+
 int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
     std::vector<int64_t> rp(A.n + 1);
     if (hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost) !=
@@ -508,7 +750,10 @@ int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
 }
 
 double csr_bytes(const Csr& A) {
-    // bytes the selected kernel must move: val + column index (+ rowptr, x, y)
+    // bytes the selected kernel must move: val + column index (+ rowptr, x, y);
+    // SELL: 10 B per stored nonzero + the 4-B row map (padding not counted)
+    if (A.kernel == kCsrSell && A.s_val)
+        return 10.0 * (double)A.nnz + 4.0 * (double)A.n + 16.0 * (double)A.n;
     const bool cw = A.w_colw != nullptr && (A.kernel == kCsrWVec || A.kernel == kCsrWVec8 ||
                                           A.kernel == kCsrWVecX || A.kernel == kCsrWVecP3 ||
                                           A.kernel == kCsrWVecP4);
@@ -539,6 +784,23 @@ static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y,
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if (A.kernel == kCsrSell && A.s_val) {
+        const size_t lds = sizeof(double) * kWinX;
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
+                               A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y);
+        };
+        if (A.s_unroll == 4) go(k_csr_sell<4, true>);
+        else if (A.s_unroll == 2) go(k_csr_sell<2, true>);
+        else if (A.s_unroll == 3) go(k_csr_sell<3, true>);
+        else if (A.s_unroll == 6) go(k_csr_sell<6, true>);
+        else if (A.s_unroll == 5) go(k_csr_sell2<4, true>);  // two slices per wave
+        else if (A.s_unroll == 7) go(k_csr_sell2<2, true>);
+        else go(k_csr_sell<8, true>);
+        return;
+    }
     if ((A.kernel == kCsrWVec || A.kernel == kCsrWVecNT || A.kernel == kCsrWVecX) && A.w_nsb > 0) {
         const bool nt = A.kernel == kCsrWVecNT;
         const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;

@@ -363,6 +363,8 @@ int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disor
 int arpack_hip_gen_banded_sym(arpack_hip_csr** A, int64_t n, int64_t row_begin,
                               int64_t row_end, uint32_t seed, int bandwidth, int per_row);
 /* Copy a registered CSR back to host buffers (sizes from arpack_hip_csr_info). */
+/* SELL-64 layout statistics (slices, stored entries incl. padding); -1 if not built */
+int arpack_hip_csr_sell_info(const arpack_hip_csr* A, int64_t* nslices, int64_t* padded);
 int arpack_hip_csr_info(const arpack_hip_csr* A, int64_t* n, int64_t* nnz);
 int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* col, double* val);
 
