@@ -77,6 +77,7 @@ def _declare(L):
     L.arpack_hip_csr_destroy.argtypes = [C.c_void_p]
     L.arpack_hip_csr_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_csr_set_kernel.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.arpack_hip_csr_set_symmetric.argtypes = [C.c_void_p, C.c_int]
     L.arpack_hip_csr_time.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     L.arpack_hip_csr_time.restype = C.c_double
     L.arpack_hip_csr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
@@ -325,6 +326,15 @@ class CSR:
         """0 vector, 1 CSR-stream, 2 CSR-stream non-temporal."""
         if lib().arpack_hip_csr_set_kernel(self.h, kernel, tile) != 0:
             raise RuntimeError("kernel not applicable to this matrix")
+
+    def set_symmetric(self, on: bool = True):
+        """Declare the matrix symmetric: the SpMV streams only the upper
+        triangle (arpack_hip_csr_set_symmetric; entries below the diagonal are
+        ignored).  Raises if the band structure does not fit the LDS windows."""
+        rc = lib().arpack_hip_csr_set_symmetric(self.h, 1 if on else 0)
+        if rc != 0:
+            raise RuntimeError("symmetric storage not applicable to this matrix (rc=%d)" % rc)
+        self.symmetric = bool(on)
 
     def time_spmv(self, reps=20):
         x = DeviceBuffer(self.n)

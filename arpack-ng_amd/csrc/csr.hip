@@ -249,6 +249,7 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     if (A->rblk) (void)hipFree(A->rblk);
     if (A->win) (void)hipFree(A->win);
     if (A->sell) (void)hipFree(A->sell);
+    if (A->symsell) (void)hipFree(A->symsell);
     if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
     A->A.w_colw = nullptr;
     delete A;
@@ -279,7 +280,23 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
+    if (!on) {
+        if (A->A.kernel == ahip::dev::kCsrSymSell)
+            A->A.kernel = A->sell ? ahip::dev::kCsrSell
+                                  : (A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector);
+        return 0;
+    }
+    if (!A->symsell) {
+        const int rc = ahip::dev::csr_build_symsell(A->A, A->ncols, &A->symsell);
+        if (rc != 0) return rc;
+    }
+    A->A.kernel = ahip::dev::kCsrSymSell;
+    return 0;
+}
+
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
+    if (kernel == ahip::dev::kCsrSymSell) return arpack_hip_csr_set_symmetric(A, 1);
     if (kernel == ahip::dev::kCsrVector) {
         A->A.kernel = kernel;
         return 0;
@@ -434,6 +451,9 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     A->ncols = ncols;
     if (A->win) (void)hipFree(A->win);
     if (A->sell) (void)hipFree(A->sell);
+    if (A->symsell) (void)hipFree(A->symsell);
+    A->symsell = nullptr;
+    A->A.ss_val = nullptr;
     if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
     A->A.w_colw = nullptr;
     A->win = nullptr;

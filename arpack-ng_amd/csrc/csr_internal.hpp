@@ -14,6 +14,7 @@ struct arpack_hip_csr {
     int64_t* rblk = nullptr;  // CSR-stream row blocks (owned)
     void* win = nullptr;      // LDS-window superblock tables (owned)
     void* sell = nullptr;     // SELL-64 slices + values (owned, built on demand)
+    void* symsell = nullptr;  // symmetric-storage layout (owned, arpack_hip_csr_set_symmetric)
 };
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV

@@ -20,6 +20,15 @@ namespace ahip::dev {
 constexpr int kBlock = 256;
 constexpr int kMaxRedBlocks = 2048;
 
+// XCD-contiguous block order: the hardware deals workgroups round-robin over
+// the 8 XCDs, so logical block xcd_block(b) makes each XCD walk one contiguous
+// range of superblocks (its 4 MB L2 then serves overlapping window loads).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    constexpr int64_t X = 8;
+    const int64_t q = nb / X, r = nb % X, x = b % X, i = b / X;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 // Scalar state of the current step j (device memory).
 struct LzState {
     double rnorm;   // B-norm of the current residual (beta of the next step)
@@ -152,6 +161,21 @@ struct Csr {
     const uint16_t* s_colw = nullptr;
     int64_t s_nslices = 0, s_padded = 0;
     int s_unroll = 8;                      // column steps per chunk (4, 8 or 16)
+    // symmetric storage (kCsrSymSell, csr_build_symsell, spmv_sym.hip): upper
+    // triangle only, symmetric superblocks [r0, r1) with x/y windows of span
+    // columns, `pre` leading rows combined with the previous superblock's spill
+    const int64_t* ss_sb_r0 = nullptr;     // nsb + 1 row bounds
+    const int32_t* ss_sb_span = nullptr;
+    const int32_t* ss_sb_pre = nullptr;
+    const int64_t* ss_sb_off = nullptr;    // nsb + 1 offsets into the combine slots
+    const int64_t* ss_slice0 = nullptr;    // first slice of each superblock (+ end)
+    const int64_t* ss_ptr = nullptr;       // slice start (+ end)
+    const int32_t* ss_row = nullptr;       // 64 per slice, -1 = padding lane
+    const double* ss_val = nullptr;
+    const uint16_t* ss_colw = nullptr;     // col - r0 (16 bit)
+    double* ss_lo = nullptr;               // spill partials (written by superblock b-1)
+    double* ss_hi = nullptr;               // prefix partials (written by superblock b)
+    int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;
 };
 enum CsrKernel : int {
     kCsrVector = 0,
@@ -166,7 +190,13 @@ enum CsrKernel : int {
     kCsrWVecP3 = 9,  // XCD order, 3 row passes in flight
     kCsrWVecP4 = 10, // XCD order, 4 row passes in flight
     kCsrSell = 11,   // SELL-64 slices (length-sorted rows) over the x windows
+    kCsrSymSell = 12,  // symmetric storage: upper-triangle SELL-64, LDS x and y windows
 };
+// Build the symmetric-storage layout (upper triangle of a square matrix the
+// caller declares symmetric); -1 if the matrix does not fit the superblock
+// scheme, -2 on allocation failure.  *owned receives the device allocation.
+int csr_build_symsell(Csr& A, int64_t ncols, void** owned);
+void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y);
 // Build the SELL-64 layout from a matrix with window tables; *owned receives the
 // single device allocation.  0 on success.
 int csr_build_sell(Csr& A, void** owned);

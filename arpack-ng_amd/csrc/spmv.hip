@@ -217,16 +217,9 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_window(
 // CW: read the 16-bit window-relative column indices (colw = col - c0 of the
 // superblock, built by the analysis) instead of int32 col: 10 instead of 12
 // bytes per nonzero.
-// XCD-aware superblock order: the hardware deals workgroup b to XCD b % 8, so
-// consecutive superblocks (whose x windows overlap by ~80%) would land on
-// different XCDs and fetch their windows from HBM eight times over.  Remap so
-// each XCD walks one contiguous range of superblocks: its 4 MB L2 then serves
-// the overlapping window loads.
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
-    constexpr int64_t X = 8;
-    const int64_t q = nb / X, r = nb % X, x = b % X, i = b / X;
-    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-}
+// XCD-aware superblock order (xcd_block, device.hpp): consecutive superblocks
+// (whose x windows overlap by ~80%) would otherwise land on different XCDs and
+// fetch their windows from HBM eight times over.
 
 template <int L, int U, bool NT, bool CW, bool XCD = false>
 __global__ __launch_bounds__(kWinThreads) void k_csr_wvec(
@@ -754,6 +747,9 @@ double csr_bytes(const Csr& A) {
     // SELL: 10 B per stored nonzero + the 4-B row map (padding not counted)
     if (A.kernel == kCsrSell && A.s_val)
         return 10.0 * (double)A.nnz + 4.0 * (double)A.n + 16.0 * (double)A.n;
+    // symmetric storage: 10 B per stored upper-triangle entry + row map + x + y
+    if (A.kernel == kCsrSymSell && A.ss_val)
+        return 10.0 * (double)A.ss_nnz + 4.0 * (double)A.n + 16.0 * (double)A.n;
     const bool cw = A.w_colw != nullptr && (A.kernel == kCsrWVec || A.kernel == kCsrWVec8 ||
                                           A.kernel == kCsrWVecX || A.kernel == kCsrWVecP3 ||
                                           A.kernel == kCsrWVecP4);
@@ -784,6 +780,10 @@ static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y,
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if (A.kernel == kCsrSymSell && A.ss_val) {
+        csr_spmv_sym(s, A, x, y);
+        return;
+    }
     if (A.kernel == kCsrSell && A.s_val) {
         const size_t lds = sizeof(double) * kWinX;
         auto go = [&](auto kern) {

@@ -1,0 +1,375 @@
+// Symmetric-storage SpMV y = A x for dsaupd's OP (A = A', declared by the
+// caller through arpack_hip_csr_set_symmetric; MKL's SPARSE_MATRIX_TYPE_SYMMETRIC
+// with the upper fill mode is the same contract).  Only the upper triangle
+// (col >= row, diagonal included) is streamed from HBM: at the north-star
+// operator that halves the val/col bytes of the dominant kernel of the cycle
+// (SpMV ~50% of the cycle's bytes).
+//
+// y_i = sum_{j >= i} a_ij x_j  (row part, lane registers)
+//     + sum_{k <  i} a_ki x_k  (transposed part: scattered from row k)
+//
+// Layout: SYMMETRIC SUPERBLOCKS.  Superblock b owns rows [r0, r1); the upper
+// entries of those rows touch columns [r0, r0 + span) with span <= kSymWin.
+// One 1024-thread workgroup per superblock stages x[r0, r0+span) in LDS,
+// zeroes an LDS y window of the same range, and streams the superblock's
+// upper entries as SELL-64 slices (rows sorted by upper length, one row per
+// lane, column-step-major: one 512-B val load + one 128-B 16-bit column load
+// per wave and step).  Each entry feeds the row sum (x gathered from LDS) and,
+// off the diagonal, one LDS atomic add a_ij x_i into y_lds[j].
+// The y window then holds three ranges:
+//   [0, pre)     rows that the previous superblock's window also reaches
+//                (its spill): written to slot_hi, combined below
+//   [pre, R)     complete rows: stored to y
+//   [R, span)    this superblock's spill into the next one: slot_lo
+// The analysis guarantees every spill lies inside the NEXT superblock's rows,
+// so each combined row has exactly two partial sums; a second small kernel
+// stores y = lo + hi (a two-term sum is commutative, so the combine adds no
+// order dependence of its own).
+//
+// Rounding: the transposed contributions arrive in LDS in wave-schedule order,
+// so y is not bitwise reproducible run to run (|dy| ~ 1 ulp of the row's
+// terms).  The full-storage kernel (spmv.hip, bitwise SciPy's csr_matvec) stays
+// the default; this one is opt-in for operators the caller declares symmetric.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <vector>
+
+#include "device.hpp"
+
+namespace ahip::dev {
+
+namespace {
+
+constexpr int kSymThreads = 1024;
+constexpr int kSymWin = 8192;  // doubles per LDS window (x and y: 2 x 64 KB)
+
+// per row: number of upper entries (col >= row) and their largest column
+// (at least the row itself, so every row's y slot is inside its window)
+__global__ void k_upper_stats(int64_t n, const int64_t* __restrict__ rp,
+                              const int32_t* __restrict__ col, int32_t* __restrict__ cnt,
+                              int32_t* __restrict__ cmax) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int32_t c = 0, m = (int32_t)i;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            const int32_t j = col[k];
+            if (j >= i) {
+                ++c;
+                m = max(m, j);
+            }
+        }
+        cnt[i] = c;
+        cmax[i] = m;
+    }
+}
+
+// one 64-thread block per slice, lane = row: the row's upper entries in CSR
+// order; padding steps carry value 0 and the row's own (diagonal) column, so
+// the kernel's off-diagonal test drops them without a length check
+__global__ void k_symsell_fill(const int64_t* __restrict__ sptr, const int32_t* __restrict__ srow,
+                               const int64_t* __restrict__ slice_r0, const int64_t* __restrict__ rp,
+                               const int32_t* __restrict__ col, const double* __restrict__ val,
+                               uint16_t* __restrict__ scolw, double* __restrict__ sval) {
+    const int64_t s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t base = sptr[s];
+    const int w = (int)((sptr[s + 1] - base) >> 6);
+    const int row = srow[s * 64 + lane];
+    const int64_t r0 = slice_r0[s];
+    const uint16_t pad = row >= 0 ? (uint16_t)(row - r0) : (uint16_t)0;
+    int k = 0;
+    if (row >= 0) {
+        for (int64_t e = rp[row]; e < rp[row + 1]; ++e) {
+            const int32_t j = col[e];
+            if (j < row) continue;
+            sval[base + (int64_t)k * 64 + lane] = val[e];
+            scolw[base + (int64_t)k * 64 + lane] = (uint16_t)(j - r0);
+            ++k;
+        }
+    }
+    for (; k < w; ++k) {
+        sval[base + (int64_t)k * 64 + lane] = 0.0;
+        scolw[base + (int64_t)k * 64 + lane] = pad;
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
+    const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
+    const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
+    double* __restrict__ slot_lo, double* __restrict__ slot_hi) {
+    __shared__ double xw[kSymWin];
+    __shared__ double yw[kSymWin];
+    constexpr int NW = kSymThreads / 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t sb = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t r0 = sb_r0[sb];
+    const int R = (int)(sb_r0[sb + 1] - r0);
+    const int span = sb_span[sb];
+    const int64_t s0 = sb_slice0[sb], s1 = sb_slice0[sb + 1];
+    struct Chunk {
+        double v[U];
+        int c[U];
+    };
+    auto load = [&](Chunk& ch, int64_t base, int w, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < w;
+            ch.v[u] = in ? sval[base + (int64_t)(k0 + u) * 64 + lane] : 0.0;
+            ch.c[u] = in ? (int)scolw[base + (int64_t)(k0 + u) * 64 + lane] : -1;
+        }
+    };
+    int64_t s = s0 + wave;
+    int64_t base = 0;
+    int w = 0;
+    Chunk cur, nxt;
+    if (s < s1) {
+        base = sptr[s];
+        w = (int)((sptr[s + 1] - base) >> 6);
+        load(cur, base, w, 0);
+    }
+    for (int i = t; i < span; i += kSymThreads) {
+        xw[i] = x[r0 + i];
+        yw[i] = 0.0;
+    }
+    __syncthreads();
+    for (; s < s1; s += NW) {
+        const int row = srow[s * 64 + lane];
+        const int rl = row >= 0 ? row - (int)r0 : 0;
+        const double xi = xw[rl];
+        const int64_t sn = s + NW;
+        int64_t nbase = 0;
+        int nw = 0;
+        if (sn < s1) {
+            nbase = sptr[sn];
+            nw = (int)((sptr[sn + 1] - nbase) >> 6);
+        }
+        double acc = 0.0;
+        int k = 0;
+        do {
+            if (k + U < w) load(nxt, base, w, k + U);
+            else if (sn < s1) load(nxt, nbase, nw, 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = cur.c[u];
+                if (c >= 0) {
+                    acc += cur.v[u] * xw[c];
+                    if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+                }
+            }
+            cur = nxt;
+            k += U;
+        } while (k < w);
+        if (row >= 0) atomicAdd(&yw[rl], acc);
+        base = nbase;
+        w = nw;
+    }
+    __syncthreads();
+    const int pre = sb_pre[sb];
+    const int64_t off = sb_off[sb], offn = sb_off[sb + 1];
+    for (int i = t; i < span; i += kSymThreads) {
+        const double v = yw[i];
+        if (i < pre) slot_hi[off + i] = v;
+        else if (i < R) y[r0 + i] = v;
+        else slot_lo[offn + (i - R)] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ssell_combine(const int64_t* __restrict__ sb_r0,
+                                                       const int32_t* __restrict__ sb_pre,
+                                                       const int64_t* __restrict__ sb_off,
+                                                       const double* __restrict__ lo,
+                                                       const double* __restrict__ hi,
+                                                       double* __restrict__ y) {
+    const int64_t b = blockIdx.x;
+    const int pre = sb_pre[b];
+    const int64_t off = sb_off[b], r0 = sb_r0[b];
+    for (int i = threadIdx.x; i < pre; i += 256) y[r0 + i] = lo[off + i] + hi[off + i];
+}
+
+}  // namespace
+
+// Superblock plan from the per-row largest upper column cmax[i] (>= i):
+// greedy superblocks whose window [r0, max cmax] holds <= win columns; pre[b]
+// = rows at the head of superblock b reached by b-1's window (its spill);
+// off = prefix sums of pre (the combine slots).  -1 if a single row is wider
+// than the window or a spill would reach past the next superblock.
+int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& r0s,
+                 std::vector<int32_t>& spans, std::vector<int32_t>& pre, std::vector<int64_t>& off) {
+    r0s.assign(1, 0);
+    spans.clear();
+    int64_t start = 0, run = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c = std::max<int64_t>(cmax[i], i);
+        if (c >= n || c - i + 1 > win) return -1;
+        const int64_t nrun = std::max(run, c);
+        if (i > start && nrun - start + 1 > win) {
+            spans.push_back((int32_t)(run - start + 1));
+            r0s.push_back(i);
+            start = i;
+            run = c;
+        } else {
+            run = nrun;
+        }
+    }
+    spans.push_back((int32_t)(run - start + 1));
+    r0s.push_back(n);
+    const int64_t nsb = (int64_t)spans.size();
+    pre.assign(nsb, 0);
+    off.assign(nsb + 1, 0);
+    for (int64_t b = 1; b < nsb; ++b) {
+        const int64_t Rp = r0s[b] - r0s[b - 1], Rb = r0s[b + 1] - r0s[b];
+        pre[b] = (int32_t)(spans[b - 1] - Rp);
+        if (pre[b] > Rb) return -1;  // the spill would reach two superblocks ahead
+    }
+    if (spans[nsb - 1] != (int32_t)(n - r0s[nsb - 1])) return -1;
+    for (int64_t b = 0; b < nsb; ++b) off[b + 1] = off[b] + pre[b];
+    return 0;
+}
+
+// Host analysis (once per matrix): greedy superblocks under the window, the
+// spill-inside-the-next-superblock rule, SELL slices of the upper rows.
+// -1 when the matrix does not fit the scheme (rectangular / distributed, a row
+// wider than the window, or a spill reaching past the next superblock).
+int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
+    const int64_t n = A.n;
+    if (ncols != n || n <= 0 || n >= (int64_t)INT32_MAX) return -1;
+    int32_t *dcnt = nullptr, *dcm = nullptr;
+    if (hipMalloc(&dcnt, sizeof(int32_t) * n) || hipMalloc(&dcm, sizeof(int32_t) * n)) return -2;
+    int64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dcnt,
+                       dcm);
+    std::vector<int32_t> cnt(n), cm(n);
+    (void)hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(dcnt);
+    (void)hipFree(dcm);
+    std::vector<int64_t> r0s, off;
+    std::vector<int32_t> spans, pre;
+    if (symsell_plan(n, cm.data(), kSymWin, r0s, spans, pre, off) != 0) return -1;
+    const int64_t nsb = (int64_t)spans.size();
+    // SELL-64 slices of the upper rows, longest first (stable)
+    std::vector<int64_t> slice0{0}, sptr{0}, slice_r0;
+    std::vector<int32_t> srow, order;
+    int64_t nnz_u = 0;
+    for (int64_t b = 0; b < nsb; ++b) {
+        const int64_t R0 = r0s[b], R1 = r0s[b + 1];
+        order.resize((size_t)(R1 - R0));
+        for (int64_t r = R0; r < R1; ++r) {
+            order[r - R0] = (int32_t)r;
+            nnz_u += cnt[r];
+        }
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int32_t a, int32_t c) { return cnt[a] > cnt[c]; });
+        for (size_t q = 0; q < order.size(); q += 64) {
+            const int64_t w = cnt[order[q]];
+            for (size_t l = 0; l < 64; ++l) srow.push_back(q + l < order.size() ? order[q + l] : -1);
+            sptr.push_back(sptr.back() + 64 * w);
+            slice_r0.push_back(R0);
+        }
+        slice0.push_back((int64_t)sptr.size() - 1);
+    }
+    const int64_t ns = (int64_t)sptr.size() - 1, padded = sptr.back(), ncomb = off[nsb];
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t b_r0 = sizeof(int64_t) * (nsb + 1), b_sp = sizeof(int32_t) * nsb,
+                 b_pre = sizeof(int32_t) * nsb, b_off = sizeof(int64_t) * (nsb + 1),
+                 b_s0 = sizeof(int64_t) * (nsb + 1), b_ptr = sizeof(int64_t) * (ns + 1),
+                 b_row = sizeof(int32_t) * srow.size(),
+                 b_val = sizeof(double) * (size_t)std::max<int64_t>(padded, 1),
+                 b_cw = sizeof(uint16_t) * (size_t)std::max<int64_t>(padded, 1),
+                 b_slot = sizeof(double) * (size_t)std::max<int64_t>(ncomb, 1);
+    char* d = nullptr;
+    if (hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) + up(b_row) +
+                          up(b_val) + up(b_cw) + 2 * up(b_slot)))
+        return -2;
+    char* p = d;
+    auto take = [&](size_t bytes) {
+        char* r = p;
+        p += up(bytes);
+        return r;
+    };
+    auto* d_r0 = (int64_t*)take(b_r0);
+    auto* d_sp = (int32_t*)take(b_sp);
+    auto* d_pre = (int32_t*)take(b_pre);
+    auto* d_off = (int64_t*)take(b_off);
+    auto* d_s0 = (int64_t*)take(b_s0);
+    auto* d_ptr = (int64_t*)take(b_ptr);
+    auto* d_row = (int32_t*)take(b_row);
+    auto* d_val = (double*)take(b_val);
+    auto* d_cw = (uint16_t*)take(b_cw);
+    auto* d_lo = (double*)take(b_slot);
+    auto* d_hi = (double*)take(b_slot);
+    (void)hipMemcpy(d_r0, r0s.data(), b_r0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_sp, spans.data(), b_sp, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_pre, pre.data(), b_pre, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_off, off.data(), b_off, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_s0, slice0.data(), b_s0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_ptr, sptr.data(), b_ptr, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_row, srow.data(), b_row, hipMemcpyHostToDevice);
+    int64_t* d_sr0 = nullptr;
+    if (ns > 0) {
+        if (hipMalloc(&d_sr0, sizeof(int64_t) * ns)) {
+            (void)hipFree(d);
+            return -2;
+        }
+        (void)hipMemcpy(d_sr0, slice_r0.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d_ptr, d_row, d_sr0,
+                           A.rowptr, A.col, A.val, d_cw, d_val);
+    }
+    const bool ok = hipDeviceSynchronize() == hipSuccess;
+    if (d_sr0) (void)hipFree(d_sr0);
+    if (!ok) {
+        (void)hipFree(d);
+        return -2;
+    }
+    A.ss_sb_r0 = d_r0;
+    A.ss_sb_span = d_sp;
+    A.ss_sb_pre = d_pre;
+    A.ss_sb_off = d_off;
+    A.ss_slice0 = d_s0;
+    A.ss_ptr = d_ptr;
+    A.ss_row = d_row;
+    A.ss_val = d_val;
+    A.ss_colw = d_cw;
+    A.ss_lo = d_lo;
+    A.ss_hi = d_hi;
+    A.ss_nsb = nsb;
+    A.ss_nnz = nnz_u;
+    A.ss_padded = padded;
+    A.ss_ncomb = ncomb;
+    *owned = d;
+    return 0;
+}
+
+void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
+    hipLaunchKernelGGL(k_csr_ssell<4>, dim3((unsigned)A.ss_nsb), dim3(kSymThreads), 0, s, A.ss_sb_r0,
+                       A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row, A.ss_colw,
+                       A.ss_val, x, y, A.ss_lo, A.ss_hi);
+    if (A.ss_ncomb > 0)
+        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)A.ss_nsb), dim3(256), 0, s, A.ss_sb_r0,
+                           A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y);
+}
+
+}  // namespace ahip::dev
+
+// Host-only view of the plan (CPU-tested, tests/test_symsell_plan.py): writes
+// nsb, then r0s[0..nsb], spans[0..nsb), pre[0..nsb) (caller sizes them n + 1).
+extern "C" int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t* nsb,
+                                           int64_t* r0s, int32_t* spans, int32_t* pre) {
+    std::vector<int64_t> r, o;
+    std::vector<int32_t> sp, pr;
+    const int rc = ahip::dev::symsell_plan(n, cmax, win, r, sp, pr, o);
+    *nsb = rc == 0 ? (int64_t)sp.size() : 0;
+    if (rc != 0) return rc;
+    std::copy(r.begin(), r.end(), r0s);
+    std::copy(sp.begin(), sp.end(), spans);
+    std::copy(pr.begin(), pr.end(), pre);
+    return 0;
+}

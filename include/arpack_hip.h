@@ -216,6 +216,15 @@ void arpack_hip_csr_destroy(arpack_hip_csr* A);
 /* SpMV kernel choice: 0 vector (G lanes/row), 1 CSR-stream, 2 CSR-stream with
  * non-temporal val/col loads; tile = nonzeros per workgroup (2048 or 4096). */
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
+/* Declare A symmetric (on != 0): the SpMV then streams only the upper
+ * triangle (col >= row, diagonal included); stored entries below the diagonal
+ * are ignored, as with MKL's symmetric/upper matrix descriptor.  Square,
+ * unsharded matrices whose upper rows reach at most ~4096 columns past the
+ * superblock fit the LDS windows; otherwise returns -1 and A keeps its
+ * full-storage kernel.  y is then not bitwise reproducible run to run
+ * (transposed terms are summed in LDS in schedule order).  on == 0 restores
+ * the full-storage kernel. */
+int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
 /* y = A x on device (x, y device pointers). */
@@ -333,6 +342,15 @@ void arpack_hip_pdneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny
  * rank (4*P doubles, global indices); out = {halo_lo, halo_hi, send_lo, send_hi}
  * of rank r.  Returns 0, -3 (blocks not contiguous) or -4 (halo too wide). */
 int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out);
+/* Host half of arpack_hip_csr_set_symmetric's analysis (no GPU): the symmetric
+ * superblock plan from each row's largest upper column cmax[i] for an LDS
+ * window of `win` columns.  Writes *nsb, r0s[0..nsb] (row bounds), spans[0..nsb)
+ * (window lengths) and pre[0..nsb) (leading rows combined with the previous
+ * superblock's spill); the caller sizes the arrays n + 1.  -1 if the matrix
+ * does not fit (a row wider than the window, or a spill past the next
+ * superblock). */
+int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t* nsb, int64_t* r0s,
+                                int32_t* spans, int32_t* pre);
 /* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
  * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
 void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,

@@ -1,0 +1,112 @@
+"""GPU: symmetric-storage SpMV (arpack_hip_csr_set_symmetric, spmv_sym.hip).
+
+The kernel streams only the upper triangle and scatters the transposed terms
+through LDS atomics, so y is NOT bitwise SciPy's (the full-storage default is,
+tests/test_gpu_parity.py::test_spmv_bitwise_equals_scipy).  Bar here: every
+row within 64 ulp of its absolute-value row sum, |y - A@x| <= 64 eps (|A| |x|),
+and whole solves on the reference's golden fixtures with the SAME restart and
+OP*x counts and Ritz values within the parity tolerance of test_gpu_parity.
+"""
+import numpy as np
+import pytest
+
+from oracle import matrices as M
+from tests.test_gpu_parity import _check, _mat
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+def _spmv_sym(pkg, rp, col, val, x):
+    Ad = pkg.CSR.from_arrays(rp, col, val)
+    Ad.set_symmetric(True)
+    xd = pkg.DeviceBuffer.from_numpy(x)
+    yd = pkg.DeviceBuffer(len(rp) - 1)
+    Ad.matvec_device(xd.at(0), yd.at(0))
+    return yd.numpy(), Ad
+
+
+def _close(rp, col, val, x, y):
+    yref = M.to_scipy(rp, col, val) @ x
+    scale = M.to_scipy(rp, col, np.abs(val)) @ np.abs(x)
+    err = np.abs(y - yref)
+    assert np.all(err <= 64 * EPS * scale), (err / np.maximum(scale, 1e-300)).max()
+
+
+@pytest.mark.parametrize("spec", [("banded_sym", 20000, 1234, 512, 25),
+                                  ("banded_sym", 40000, 99, 4096, 25),   # NS band: spills
+                                  ("banded_sym", 3000, 5, 64, 3),
+                                  ("laplace2d", 37, 3.0), ("laplace3d", 21, 1.0),
+                                  ("anderson", 13, 3, 16.0, 1234), ("diag", 1000), ("diag", 1)])
+def test_symmetric_spmv_matches_full(pkg, spec):
+    rp, col, val = _mat(spec)
+    x = np.random.default_rng(3).standard_normal(len(rp) - 1)
+    y, _ = _spmv_sym(pkg, rp, col, val, x)
+    _close(rp, col, val, x, y)
+
+
+def test_symmetric_spmv_ns_shape_property(pkg):
+    """North-star operator family at 2e5 rows (band 4096, ~51 nnz/row), generated
+    on device: symmetric storage agrees with the full-storage (bitwise-SciPy)
+    kernel row by row."""
+    n = 200_000
+    A = pkg.CSR.banded_sym(n, 1234, 4096, 25)
+    B = pkg.CSR.banded_sym(n, 1234, 4096, 25)
+    B.set_symmetric(True)
+    x = np.random.default_rng(11).standard_normal(n)
+    xd = pkg.DeviceBuffer.from_numpy(x)
+    ya = pkg.DeviceBuffer(n)
+    yb = pkg.DeviceBuffer(n)
+    A.matvec_device(xd.at(0), ya.at(0))
+    B.matvec_device(xd.at(0), yb.at(0))
+    rp, col, val = A.download()
+    scale = M.to_scipy(rp, col, np.abs(val)) @ np.abs(x)
+    assert np.all(np.abs(ya.numpy() - yb.numpy()) <= 64 * EPS * scale)
+
+
+def test_symmetric_ignores_lower_triangle(pkg):
+    """Entries below the diagonal are not read (upper fill mode): corrupting them
+    leaves y unchanged."""
+    rp, col, val = _mat(("banded_sym", 5000, 7, 300, 9))
+    rows = np.repeat(np.arange(len(rp) - 1), np.diff(rp))
+    bad = val.copy()
+    bad[col < rows] = 1e300
+    x = np.random.default_rng(1).standard_normal(len(rp) - 1)
+    y, _ = _spmv_sym(pkg, rp, col, bad, x)
+    _close(rp, col, val, x, y)
+
+
+def test_symmetric_refused_for_wide_band(pkg):
+    """A band wider than the LDS window keeps the full-storage kernel."""
+    import scipy.sparse as sp
+    n = 20000
+    A = (sp.eye(n, format="lil") * 4.0)
+    A[0, 9500] = A[9500, 0] = -1.0
+    A = A.tocsr()
+    A.sort_indices()
+    rp, col, val = A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data
+    Ad = pkg.CSR.from_arrays(rp, col, val)
+    with pytest.raises(RuntimeError):
+        Ad.set_symmetric(True)
+    x = np.random.default_rng(2).standard_normal(len(rp) - 1)
+    xd = pkg.DeviceBuffer.from_numpy(x)
+    yd = pkg.DeviceBuffer(len(rp) - 1)
+    Ad.matvec_device(xd.at(0), yd.at(0))
+    assert np.array_equal(yd.numpy(), M.to_scipy(rp, col, val) @ x)
+
+
+@pytest.mark.parametrize("name", ["g2_icb_ds", "g3_anderson3d", "g4_banded", "g5_anderson2d_sa",
+                                  "g6_anderson2d_be", "g10_anderson2d_sm"])
+def test_solve_with_symmetric_storage(pkg, golden, name):
+    """Whole dsaupd/dseupd solve on the GPU with the symmetric-storage OP: same
+    restart cycles and OP*x count as the reference, Ritz values and residuals
+    within the parity tolerance."""
+    g = golden(name)
+    rp, col, val = _mat(g["spec"])
+    A = M.to_scipy(rp, col, val)
+    Ad = pkg.CSR.from_arrays(rp, col, val)
+    Ad.set_symmetric(True)
+    d, z, res = pkg.eigsh(Ad, A.shape[0], int(g["nev"]), int(g["ncv"]), str(g["which"]),
+                          float(g["tol"]), v0=g["v0"], mxiter=int(g["mxiter"]), device=True)
+    _check(g, d, res, z, A)

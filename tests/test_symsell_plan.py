@@ -1,0 +1,126 @@
+"""CPU: the symmetric-storage SpMV plan (host half of arpack_hip_csr_set_symmetric,
+spmv_sym.hip) -- no GPU needed.
+
+* invariants of arpack_hip_kit_symsell_plan: superblocks tile the rows, every
+  window holds its rows' upper columns within `win`, every spill lies inside the
+  NEXT superblock (so each row has at most two partial sums);
+* the plan's semantics: per-superblock windows of upper-triangle products,
+  spill/prefix slots and the two-term combine reproduce A @ x (the arithmetic
+  that k_csr_ssell + k_ssell_combine perform on the device);
+* matrices that do not fit (band wider than the window) are refused.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import matrices as M
+
+
+def _plan(pkg, cmax, win):
+    L = pkg.lib()
+    L.arpack_hip_kit_symsell_plan.argtypes = [C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_void_p]
+    n = len(cmax)
+    cm = np.ascontiguousarray(cmax, np.int32)
+    nsb = np.zeros(1, np.int64)
+    r0s = np.zeros(n + 1, np.int64)
+    spans = np.zeros(n + 1, np.int32)
+    pre = np.zeros(n + 1, np.int32)
+    rc = L.arpack_hip_kit_symsell_plan(n, cm.ctypes.data, win, nsb.ctypes.data, r0s.ctypes.data,
+                                       spans.ctypes.data, pre.ctypes.data)
+    k = int(nsb[0])
+    return rc, r0s[:k + 1], spans[:k], pre[:k]
+
+
+def _upper_cmax(rp, col):
+    n = len(rp) - 1
+    cmax = np.arange(n, dtype=np.int64)
+    rows = np.repeat(np.arange(n), np.diff(rp))
+    up = col >= rows
+    np.maximum.at(cmax, rows[up], col[up])
+    return cmax
+
+
+def _simulate(rp, col, val, x, r0s, spans, pre):
+    """y from the plan exactly as the device computes it (up to summation order)."""
+    n = len(rp) - 1
+    y = np.zeros(n)
+    nsb = len(spans)
+    lo = {}
+    hi = {}
+    for b in range(nsb):
+        r0, r1, span = r0s[b], r0s[b + 1], spans[b]
+        yw = np.zeros(span)
+        for i in range(r0, r1):
+            for k in range(rp[i], rp[i + 1]):
+                j = col[k]
+                if j < i:
+                    continue
+                assert j - r0 < span          # the window holds every upper column
+                yw[i - r0] += val[k] * x[j]
+                if j != i:
+                    yw[j - r0] += val[k] * x[i]
+        R = r1 - r0
+        hi[b] = yw[:pre[b]].copy()
+        y[r0 + pre[b]:r1] = yw[pre[b]:R]
+        if b + 1 < nsb:
+            lo[b + 1] = yw[R:span].copy()
+            assert len(lo[b + 1]) == pre[b + 1]
+        else:
+            assert span == R
+    for b in range(1, nsb):
+        y[r0s[b]:r0s[b] + pre[b]] = lo[b] + hi[b]
+    return y
+
+
+@pytest.mark.parametrize("spec,win", [(("banded", 3000, 1234, 200, 9), 512),
+                                      (("banded", 3000, 7, 256, 5), 512),
+                                      (("lap2d", 40), 128),
+                                      (("anderson", 9), 256),
+                                      (("diag", 500), 64)])
+def test_symsell_plan_reproduces_spmv(pkg, spec, win):
+    if spec[0] == "banded":
+        rp, col, val = M.banded_sym(spec[1], spec[2], spec[3], spec[4])
+    elif spec[0] == "lap2d":
+        rp, col, val = M.laplace2d(spec[1], 1.0)
+    elif spec[0] == "anderson":
+        rp, col, val = M.anderson(spec[1], 3, 16.0, 1234)
+    else:
+        rp, col, val = M.diag(spec[1])
+    n = len(rp) - 1
+    rc, r0s, spans, pre = _plan(pkg, _upper_cmax(rp, col), win)
+    assert rc == 0
+    # invariants: tiling, windows, spill inside the next superblock
+    assert r0s[0] == 0 and r0s[-1] == n and np.all(np.diff(r0s) > 0)
+    R = np.diff(r0s)
+    assert np.all(spans <= win) and np.all(spans >= R)
+    assert pre[0] == 0
+    assert np.all(pre[1:] == spans[:-1] - R[:-1]) and np.all(pre[1:] <= R[1:])
+    assert spans[-1] == R[-1]
+    x = np.random.default_rng(5).standard_normal(n)
+    y = _simulate(rp, col, val, x, r0s, spans, pre)
+    yref = M.to_scipy(rp, col, val) @ x
+    scale = M.to_scipy(rp, col, np.abs(val)) @ np.abs(x)
+    assert np.all(np.abs(y - yref) <= 1e-13 * scale + 1e-300)
+
+
+def test_symsell_plan_refuses_wide_band(pkg):
+    rp, col, val = M.banded_sym(2000, 1234, 600, 5)
+    rc, *_ = _plan(pkg, _upper_cmax(rp, col), 512)   # a row reaches ~600 columns ahead
+    assert rc == -1
+
+
+def test_symsell_plan_edge_sizes(pkg):
+    # one row, rows with no upper entries (cmax = i), one superblock
+    for n in (1, 2, 63, 64, 65):
+        rc, r0s, spans, pre = _plan(pkg, np.arange(n), 64)
+        assert rc == 0 and r0s[-1] == n and np.all(pre == 0)
+    # a spill that would reach two superblocks ahead is refused
+    cmax = np.arange(100)
+    cmax[0] = 60            # superblock [0, k) must stop by column 63
+    cmax[70] = 99
+    rc, r0s, spans, pre = _plan(pkg, cmax, 64)
+    assert rc in (0, -1)
+    if rc == 0:
+        assert np.all(pre[1:] <= np.diff(r0s)[1:])
