@@ -296,7 +296,11 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
 }
 
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
-    if (kernel == ahip::dev::kCsrSymSell) return arpack_hip_csr_set_symmetric(A, 1);
+    if (kernel == ahip::dev::kCsrSymSell) {  // tile selects the variant
+        const int rc = arpack_hip_csr_set_symmetric(A, 1);
+        if (rc == 0) A->A.ss_variant = tile >= 0 && tile <= 16 ? tile : 0;
+        return rc;
+    }
     if (kernel == ahip::dev::kCsrVector) {
         A->A.kernel = kernel;
         return 0;

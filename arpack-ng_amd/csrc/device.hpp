@@ -176,6 +176,7 @@ struct Csr {
     double* ss_lo = nullptr;               // spill partials (written by superblock b-1)
     double* ss_hi = nullptr;               // prefix partials (written by superblock b)
     int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;
+    int ss_variant = 0;                    // kernel variant (tools/spmv_sym_time.py)
 };
 enum CsrKernel : int {
     kCsrVector = 0,

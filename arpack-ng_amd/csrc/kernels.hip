@@ -18,6 +18,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -158,7 +159,11 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
 // ----------------------------------------------------------------- update ---
 // rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
 // same pass (the V row stays in registers: one HBM read of V serves both).
-template <class R, int J, bool SPEC>
+// REV: sweep the rows last-to-first.  The preceding V pass (the CGS dots)
+// ended on the last rows, which the 256 MB Infinity Cache still holds, so a
+// reversed sweep starts on cache hits (and the next forward pass on this one's
+// last rows).
+template <class R, int J, bool SPEC, bool REV = false>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
     int64_t n, const R* __restrict__ V, int64_t ld, const double* __restrict__ c,
     const R* rin, R* rout, double* __restrict__ part, int pstride,
@@ -169,7 +174,8 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
     for (int k = 0; k < J; ++k) acc[k] = 0.0;
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n; it += stride) {
+        const int64_t i = REV ? n - 1 - it : it;
         double vrow[J];
 #pragma unroll
         for (int k = 0; k < J; ++k) vrow[k] = V[i + (int64_t)k * ld];
@@ -640,11 +646,22 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
     ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
                  gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 2));
     const dim3 g(ws.nblk), b(kBlock);
+    // alternate the sweep direction with the Gram-Schmidt sweep (which = 0:
+    // CGS update after the forward dots pass -> reversed; 1: first DGKS ->
+    // forward; 2: second DGKS -> reversed); AHIP_UPDATE_REV=0 disables
+    static const bool rev_on = [] {
+        const char* e = getenv("AHIP_UPDATE_REV");
+        return !(e && e[0] == '0');
+    }();
+    const bool rev = rev_on && (which % 2 == 0);
     if (j >= 1 && j <= 32) {
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
     case J:                                                                                        \
-        if (spec)                                                                                  \
+        if (spec && rev)                                                                           \
+            hipLaunchKernelGGL((k_update_fused<R, J, true, true>), g, b, 0, ws.stream, n, V, ld, c,\
+                               rin, rout, ws.part, ws.stride, ws.st, gate);                        \
+        else if (spec)                                                                             \
             hipLaunchKernelGGL((k_update_fused<R, J, true>), g, b, 0, ws.stream, n, V, ld, c, rin, \
                                rout, ws.part, ws.stride, ws.st, gate);                             \
         else                                                                                       \

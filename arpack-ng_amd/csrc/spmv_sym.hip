@@ -96,7 +96,13 @@ __global__ void k_symsell_fill(const int64_t* __restrict__ sptr, const int32_t* 
     }
 }
 
-template <int U>
+template <class T, bool NT>
+__device__ __forceinline__ T ldg(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int U, int MODE, bool NT = false>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
     const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
@@ -121,8 +127,8 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = k0 + u < w;
-            ch.v[u] = in ? sval[base + (int64_t)(k0 + u) * 64 + lane] : 0.0;
-            ch.c[u] = in ? (int)scolw[base + (int64_t)(k0 + u) * 64 + lane] : -1;
+            ch.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
+            ch.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
         }
     };
     int64_t s = s0 + wave;
@@ -159,8 +165,10 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
             for (int u = 0; u < U; ++u) {
                 const int c = cur.c[u];
                 if (c >= 0) {
-                    acc += cur.v[u] * xw[c];
-                    if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+                    if constexpr (MODE == 2) acc += cur.v[u] * (double)c;
+                    else acc += cur.v[u] * xw[c];
+                    if constexpr (MODE == 0)
+                        if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
                 }
             }
             cur = nxt;
@@ -349,9 +357,25 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
 }
 
 void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
-    hipLaunchKernelGGL(k_csr_ssell<4>, dim3((unsigned)A.ss_nsb), dim3(kSymThreads), 0, s, A.ss_sb_r0,
-                       A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row, A.ss_colw,
-                       A.ss_val, x, y, A.ss_lo, A.ss_hi);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)A.ss_nsb), dim3(kSymThreads), 0, s, A.ss_sb_r0,
+                           A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
+                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi);
+    };
+    // measured on the NS operator (tools/spmv_sym_time.py, one process): U = 8
+    // with non-temporal val/col loads 0.594 ms incl. the combine; U = 8 plain
+    // 0.611, U = 12 0.611, U = 6 0.626, U = 4 0.652, U = 2 0.671, U = 16 spills.
+    // Diagnostics: without the transposed LDS adds 0.611 (U = 4), without any
+    // LDS traffic 0.559 -- the slice stream itself, not the atomics, bounds it.
+    switch (A.ss_variant) {  // 1, 2: diagnostic (wrong y): no transposed adds / no LDS at all
+        case 1: go(k_csr_ssell<4, 1>); break;
+        case 2: go(k_csr_ssell<4, 2>); break;
+        case 3: go(k_csr_ssell<8, 0>); break;
+        case 4: go(k_csr_ssell<4, 0>); break;
+        case 5: go(k_csr_ssell<6, 0, true>); break;
+        case 6: go(k_csr_ssell<12, 0, true>); break;
+        default: go(k_csr_ssell<8, 0, true>); break;
+    }
     if (A.ss_ncomb > 0)
         hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)A.ss_nsb), dim3(256), 0, s, A.ss_sb_r0,
                            A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y);

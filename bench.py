@@ -12,6 +12,11 @@ the host shift selection and the on-device V*Q update (dsapps).  The whole loop
 runs on the GPU through arpack_hip_dsaupd_csr_cycles (the engine parks every K
 cycles so exactly K cycles sit inside the timed region).
 
+OP: the operator is symmetric (dsaupd's contract), so by default the CSR is
+declared symmetric and the SpMV streams only its upper triangle
+(arpack_hip_csr_set_symmetric); the full-storage SpMV (bitwise SciPy's
+csr_matvec) runs the same K cycles beside it and is reported as `full_storage`.
+
 Also reported: Lanczos steps/s (OP*x/s), time-to-converge at tol=1e-6, the
 roofline of the dominant kernel (SpMV) from live hipEvent timing, and the
 reference CPU path (oracle/_ref: arpack-ng Fortran + OpenBLAS, OpenMP SpMV)
@@ -94,9 +99,15 @@ def main():
     ap.add_argument("--ncv", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttc", action="store_true")
+    ap.add_argument("--no-full-storage", action="store_true",
+                    help="skip the secondary full-storage measurement of --storage sym")
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: engine collectives over gloo instead of RCCL, so N ranks "
                          "can share one GPU (every rank uses device 0)")
+    ap.add_argument("--storage", choices=("sym", "full"), default="sym",
+                    help="sym: the operator is declared symmetric (dsaupd's contract) and the "
+                         "SpMV streams its upper triangle (arpack_hip_csr_set_symmetric); full: "
+                         "full CSR, bitwise SciPy's csr_matvec.  Multi-GPU row blocks use full.")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
     args = ap.parse_args()
@@ -126,6 +137,10 @@ def main():
     A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row, r0, r1)
     if world > 1:
         D = pkg.DistOp(A, n, r0)
+    storage = "full"
+    if world == 1 and args.storage == "sym":
+        A.set_symmetric(True)
+        storage = "sym"
     gen_s = time.time() - t
     nnz = A.nnz
     if dist:
@@ -142,21 +157,34 @@ def main():
         return pkg.pdsaupd_cycles(s, D, k) if D is not None else s.aupd_cycles(A, k)
 
     # ---- restart-cycle throughput: W untimed cycles, then exactly K timed ones
-    mx = args.warmup + 2 * args.steps + 5
-    s = solver(0.0, mx)
-    assert cycles(s, 0) == 98                    # getv0 + initial nev-step factorization
-    cycles(s, args.warmup)                       # warmup cycles
-    pkg.synchronize()
-    if dist:
-        dist.barrier()
-    it0 = pkg.stats()["nopx"]
-    t0 = time.perf_counter()
-    ido = cycles(s, args.steps)                  # the timed region: nothing but the solve
-    pkg.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    nopx = pkg.stats()["nopx"] - it0
+    def timed_run():
+        mx = args.warmup + 2 * args.steps + 5
+        s = solver(0.0, mx)
+        assert cycles(s, 0) == 98                # getv0 + initial nev-step factorization
+        cycles(s, args.warmup)                   # warmup cycles
+        pkg.synchronize()
+        if dist:
+            dist.barrier()
+        it0 = pkg.stats()["nopx"]
+        t0 = time.perf_counter()
+        ido = cycles(s, args.steps)              # the timed region: nothing but the solve
+        pkg.synchronize()
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        return s, ido, t1 - t0, pkg.stats()["nopx"] - it0
+
+    full_storage = None
+    if storage == "sym" and not args.no_full_storage:
+        # the same K cycles with the full-storage (bitwise csr_matvec) SpMV, reported beside
+        A.set_symmetric(False)
+        s_f, ido_f, el_f, nopx_f = timed_run()
+        nc_f = args.steps if ido_f == 98 else int(s_f.iparam[2]) - args.warmup
+        full_storage = dict(value=nc_f / el_f, ms_per_step=1e3 * el_f / nc_f,
+                            lanczos_steps_per_s=nopx_f / el_f)
+        del s_f
+        A.set_symmetric(True)
+    s, ido, elapsed, nopx = timed_run()
     # Per-kernel roofline: the next K cycles of the same solve with a hipEvent
     # pair around every launch on its stream (the events cost ~7% of the cycle,
     # so they are kept out of the timed region above).
@@ -167,7 +195,6 @@ def main():
         cycles(s, args.steps)
         prof = pkg.profile_read()
         pkg.profile(False)
-    elapsed = t1 - t0
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -211,7 +238,8 @@ def main():
     step_gbs = (by + orth_bytes) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
 
     # PMC traffic is collected on the default single-GPU workload only
-    traffic, traffic_src = (pmc_traffic("k_csr_sell") if world == 1 and n == 10_000_000
+    spmv_kernel = "k_csr_ssell" if storage == "sym" else "k_csr_sell"
+    traffic, traffic_src = (pmc_traffic(spmv_kernel) if world == 1 and n == 10_000_000
                             else (None, None))
     out = {
         "metric": "Arnoldi iters/sec + time-to-converge (nev=10), n=10M CSR; %HBM roofline",
@@ -229,6 +257,7 @@ def main():
         "config": {"workload": "dsaupd LA on NS symmetric CSR (BASELINE north star)",
                    "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
                    "which": "LA", "tol": "eps (cycles never converge in the timed window)",
+                   "spmv_storage": "symmetric (upper triangle)" if storage == "sym" else "full CSR",
                    "parallelism": "single GPU" if world == 1 else
                    f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
                    f"REHEARSAL row-block x{world} on one GPU, host-staged gloo transport"},
@@ -237,8 +266,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS x "
-                               "windows, 16-bit window-relative cols, XCD-contiguous superblocks)",
+                     "kernel": ("csr_spmv symmetric storage (k_csr_ssell + k_ssell_combine: "
+                                "upper-triangle SELL-64 slices over LDS x/y windows, LDS atomic "
+                                "transposed terms, 16-bit window-relative cols)") if storage == "sym"
+                               else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "
+                                     "x windows, 16-bit window-relative cols, XCD-contiguous "
+                                     "superblocks)"),
                      "measured_on": "hipEvents around each launch over a second run of the same "
                                     "K cycles (events kept out of the timed region)",
                      "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
@@ -246,6 +279,8 @@ def main():
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
         "kernels": kernels,
         "gen_s": gen_s,
+        "storage": storage,
+        "full_storage": full_storage,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del A

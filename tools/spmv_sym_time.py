@@ -32,6 +32,10 @@ def main():
     A.set_symmetric(True)
     out["sym_ms"] = A.time_spmv(a.reps)
     A.matvec_device(x.at(0), y2.at(0))
+    for v in (1, 2, 3, 4, 5, 6):
+        A.set_kernel(12, v)
+        out["sym_v%d_ms" % v] = A.time_spmv(a.reps)
+    A.set_kernel(12, 0)
     d = np.abs(y1.numpy() - y2.numpy())
     out["max_abs_diff"] = float(d.max())
     out["max_rel_diff"] = float((d / np.maximum(np.abs(y1.numpy()), 1e-300)).max())
