@@ -807,6 +807,15 @@ class DistOp:
         self.A = A  # keeps the local CSR alive
         self.n_global, self.row0, self.nloc = n_global, row0, A.n
 
+    def matvec_device(self, x, y):
+        """y = A x on this rank's rows (collective; DeviceBuffers or addresses)."""
+        xp = x if isinstance(x, int) else _ptr(x)
+        yp = y if isinstance(y, int) else _ptr(y)
+        L = lib()
+        L.arpack_hip_dist_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        if L.arpack_hip_dist_spmv(self.h, xp, yp) != 0:
+            raise RuntimeError("distributed spmv failed")
+
     def info(self):
         v = [C.c_int64() for _ in range(4)]
         lib().arpack_hip_dist_info(self.h, *[C.byref(x) for x in v])

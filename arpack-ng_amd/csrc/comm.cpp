@@ -128,6 +128,28 @@ static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s) {
     (void)hipStreamSynchronize(s);
 }
 
+// Forward "spill" of the symmetric-storage SpMV: send nsend doubles to rank+1,
+// receive nrecv from rank-1 (the reverse of the x halo's hi side).
+void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
+                hipStream_t s) {
+    if (!c || c->nranks == 1) return;
+    const int r = c->rank, P = c->nranks;
+    const int64_t ns = r < P - 1 ? nsend : 0, nr = r > 0 ? nrecv : 0;
+    if (c->h_halo) {
+        std::vector<double> b((size_t)(ns + nr));
+        if (ns) (void)hipMemcpyAsync(b.data(), send, 8 * ns, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        c->h_halo(nullptr, 0, b.data() + ns, nr, b.data(), ns, nullptr, 0, c->h_ctx);
+        if (nr) (void)hipMemcpyAsync(recv, b.data() + ns, 8 * nr, hipMemcpyHostToDevice, s);
+        (void)hipStreamSynchronize(s);
+        return;
+    }
+    (void)ncclGroupStart();
+    if (ns) (void)ncclSend(send, (size_t)ns, ncclDouble, r + 1, c->nccl, s);
+    if (nr) (void)ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, c->nccl, s);
+    (void)ncclGroupEnd();
+}
+
 void comm_halo(const Comm* c, const DistOp& D, hipStream_t s) {
     if (!c || c->nranks == 1) return;
     if (c->h_halo) return comm_halo_host(c, D, s);

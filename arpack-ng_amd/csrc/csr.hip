@@ -288,7 +288,8 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
         return 0;
     }
     if (!A->symsell) {
-        const int rc = ahip::dev::csr_build_symsell(A->A, A->ncols, &A->symsell);
+        const int rc = ahip::dev::csr_build_symsell(A->A, A->ncols, A->sym_coff, A->sym_spill_in,
+                                                    A->sym_spill_out, &A->symsell);
         if (rc != 0) return rc;
     }
     A->A.kernel = ahip::dev::kCsrSymSell;

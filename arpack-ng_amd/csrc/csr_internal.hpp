@@ -15,6 +15,10 @@ struct arpack_hip_csr {
     void* win = nullptr;      // LDS-window superblock tables (owned)
     void* sell = nullptr;     // SELL-64 slices + values (owned, built on demand)
     void* symsell = nullptr;  // symmetric-storage layout (owned, arpack_hip_csr_set_symmetric)
+    // row distribution seen by the symmetric layout (arpack_hip_dist_create):
+    // x = [sym_coff | local rows | sym_spill_out], sym_spill_in leading rows
+    // receive the previous rank's transposed terms
+    int64_t sym_coff = 0, sym_spill_in = 0, sym_spill_out = 0;
 };
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV

@@ -177,6 +177,8 @@ struct Csr {
     double* ss_hi = nullptr;               // prefix partials (written by superblock b)
     int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;
     int ss_variant = 0;                    // kernel variant (tools/spmv_sym_time.py)
+    int64_t ss_coff = 0;                   // x index of local row 0's diagonal (halo_lo)
+    int64_t ss_spill_out = 0;              // rows of the next rank reached by the last window
 };
 enum CsrKernel : int {
     kCsrVector = 0,
@@ -196,8 +198,17 @@ enum CsrKernel : int {
 // Build the symmetric-storage layout (upper triangle of a square matrix the
 // caller declares symmetric); -1 if the matrix does not fit the superblock
 // scheme, -2 on allocation failure.  *owned receives the device allocation.
-int csr_build_symsell(Csr& A, int64_t ncols, void** owned);
+// ncols = coff + n + spill_out: x is [coff | n local | spill_out] (a rank's
+// extended x; coff = spill_out = 0 on one GPU); spill_in = leading local rows
+// that the previous rank's transposed terms reach (its spill_out).
+int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int64_t spill_out,
+                      void** owned);
 void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y);
+// the two halves (the row-distributed SpMV exchanges the spills in between):
+// main kernel, then y(prefix rows) = lo + hi.  The outgoing spill is
+// ss_lo + ss_ncomb (ss_spill_out doubles); the incoming one lands in ss_lo[0, spill_in).
+void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y);
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y);
 // Build the SELL-64 layout from a matrix with window tables; *owned receives the
 // single device allocation.  0 on success.
 int csr_build_sell(Csr& A, void** owned);

@@ -10,11 +10,23 @@
 
 namespace ahip {
 void comm_halo(const Comm* c, const DistOp& D, hipStream_t s);
+void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
+                hipStream_t s);
 
 void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
     if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
     comm_halo(D.comm, D, s);
-    dev::csr_spmv(s, *D.A, D.x_ext, y);
+    const dev::Csr& A = *D.A;
+    if (A.kernel == dev::kCsrSymSell && A.ss_val) {
+        // symmetric storage: my rows' upper entries reach the next rank's first
+        // rows -- those transposed terms (the spill) travel forward and are
+        // combined into the receiver's leading rows (a reverse halo)
+        dev::csr_spmv_sym_main(s, A, D.x_ext, y);
+        comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s);
+        dev::csr_spmv_sym_combine(s, A, y);
+        return;
+    }
+    dev::csr_spmv(s, A, D.x_ext, y);
 }
 }  // namespace ahip
 
@@ -91,11 +103,16 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     }
     (void)hipMemset(o.x_ext, 0, sizeof(double) * (next > 0 ? next : 1));
     // local column indices relative to x_ext
+    const bool was_sym = A->A.kernel == ahip::dev::kCsrSymSell;
+    A->sym_coff = o.halo_lo;
+    A->sym_spill_in = o.send_lo;
+    A->sym_spill_out = o.halo_hi;
     if (ahip_csr_remap_cols(A, row0 - o.halo_lo, next) != 0) {
         (void)hipFree(o.x_ext);
         delete D;
         return -1;
     }
+    if (was_sym) (void)arpack_hip_csr_set_symmetric(A, 1);
     o.A = &A->A;
     *out = D;
     return 0;
@@ -114,6 +131,15 @@ int arpack_hip_dist_rows(arpack_hip_dist** out, int64_t nloc, int64_t row0, int6
     D->D.comm = c;
     *out = D;
     return 0;
+}
+
+// y = A x over the row distribution (collective): x, y are this rank's rows
+// in device memory.  The halo (and, for symmetric storage, the spill) exchange
+// runs on the null stream.
+int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y) {
+    if (!D || !D->D.A) return -1;
+    ahip::dist_spmv(D->D, nullptr, x, y);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
 void arpack_hip_dist_destroy(arpack_hip_dist* D) {

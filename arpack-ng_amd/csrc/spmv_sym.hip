@@ -9,7 +9,7 @@
 //     + sum_{k <  i} a_ki x_k  (transposed part: scattered from row k)
 //
 // Layout: SYMMETRIC SUPERBLOCKS.  Superblock b owns rows [r0, r1); the upper
-// entries of those rows touch columns [r0, r0 + span) with span <= kSymWin.
+// entries of those rows touch columns [r0, r0 + span) with span <= kSymWin (10240).
 // One 1024-thread workgroup per superblock stages x[r0, r0+span) in LDS,
 // zeroes an LDS y window of the same range, and streams the superblock's
 // upper entries as SELL-64 slices (rows sorted by upper length, one row per
@@ -44,18 +44,20 @@ namespace ahip::dev {
 namespace {
 
 constexpr int kSymThreads = 1024;
-constexpr int kSymWin = 8192;  // doubles per LDS window (x and y: 2 x 64 KB)
+constexpr int kSymWin = 10240;  // doubles per LDS window (x and y: 2 x 80 KB = all 160 KB)
 
 // per row: number of upper entries (col >= row) and their largest column
 // (at least the row itself, so every row's y slot is inside its window)
-__global__ void k_upper_stats(int64_t n, const int64_t* __restrict__ rp,
+// (columns relative to the diagonal's: j - coff, coff = halo_lo for a rank's
+// block of a row-distributed operator whose x is [halo_lo | local | halo_hi])
+__global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict__ rp,
                               const int32_t* __restrict__ col, int32_t* __restrict__ cnt,
                               int32_t* __restrict__ cmax) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         int32_t c = 0, m = (int32_t)i;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-            const int32_t j = col[k];
+            const int32_t j = (int32_t)(col[k] - coff);
             if (j >= i) {
                 ++c;
                 m = max(m, j);
@@ -69,7 +71,8 @@ __global__ void k_upper_stats(int64_t n, const int64_t* __restrict__ rp,
 // one 64-thread block per slice, lane = row: the row's upper entries in CSR
 // order; padding steps carry value 0 and the row's own (diagonal) column, so
 // the kernel's off-diagonal test drops them without a length check
-__global__ void k_symsell_fill(const int64_t* __restrict__ sptr, const int32_t* __restrict__ srow,
+__global__ void k_symsell_fill(int64_t coff, const int64_t* __restrict__ sptr,
+                               const int32_t* __restrict__ srow,
                                const int64_t* __restrict__ slice_r0, const int64_t* __restrict__ rp,
                                const int32_t* __restrict__ col, const double* __restrict__ val,
                                uint16_t* __restrict__ scolw, double* __restrict__ sval) {
@@ -83,7 +86,7 @@ __global__ void k_symsell_fill(const int64_t* __restrict__ sptr, const int32_t* 
     int k = 0;
     if (row >= 0) {
         for (int64_t e = rp[row]; e < rp[row + 1]; ++e) {
-            const int32_t j = col[e];
+            const int32_t j = (int32_t)(col[e] - coff);
             if (j < row) continue;
             sval[base + (int64_t)k * 64 + lane] = val[e];
             scolw[base + (int64_t)k * 64 + lane] = (uint16_t)(j - r0);
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
     const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
     const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
-    double* __restrict__ slot_lo, double* __restrict__ slot_hi) {
+    double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff) {
     __shared__ double xw[kSymWin];
     __shared__ double yw[kSymWin];
     constexpr int NW = kSymThreads / 64;
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         load(cur, base, w, 0);
     }
     for (int i = t; i < span; i += kSymThreads) {
-        xw[i] = x[r0 + i];
+        xw[i] = x[coff + r0 + i];
         yw[i] = 0.0;
     }
     __syncthreads();
@@ -203,22 +206,73 @@ __global__ __launch_bounds__(256) void k_ssell_combine(const int64_t* __restrict
 
 }  // namespace
 
-// Superblock plan from the per-row largest upper column cmax[i] (>= i):
-// greedy superblocks whose window [r0, max cmax] holds <= win columns; pre[b]
-// = rows at the head of superblock b reached by b-1's window (its spill);
-// off = prefix sums of pre (the combine slots).  -1 if a single row is wider
-// than the window or a spill would reach past the next superblock.
+// Superblock plan from the per-row largest upper column cmax[i] (>= i).
+// Superblock b owns rows [r0s[b], r0s[b+1]); its window [r0, r0 + spans[b])
+// covers every upper column of its rows (<= win columns); pre[b] = leading rows
+// reached by superblock b-1's window (its spill), which must lie inside b, so
+// every row has at most two partial sums; pre[0] = spill_in (the previous
+// rank's spill); the last window may reach spill_out rows past the block.
+// off = prefix sums of pre (the combine slots).
+//
+// Balanced first: with the largest reach m = max(cmax[i] - i), any block of
+// <= win - m rows fits a window, and blocks of >= m rows hold the previous
+// block's spill, so k equal blocks work whenever n/k lies in [m, win - m].
+// k is rounded up to a multiple of kQuantum (the CU count: whole rounds of
+// one workgroup per CU, no tail) when the rows allow.  Otherwise greedy
+// blocks (widest windows), which suit the end of a matrix where reaches
+// shrink.  -1 if neither satisfies the rules.
+static bool plan_check(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& r0s,
+                       std::vector<int32_t>& spans, std::vector<int32_t>& pre,
+                       std::vector<int64_t>& off, int64_t spill_in, int64_t spill_out) {
+    const int64_t nsb = (int64_t)r0s.size() - 1;
+    spans.assign(nsb, 0);
+    for (int64_t b = 0; b < nsb; ++b) {
+        int64_t run = r0s[b + 1] - 1;
+        for (int64_t i = r0s[b]; i < r0s[b + 1]; ++i) run = std::max<int64_t>(run, cmax[i]);
+        if (run - r0s[b] + 1 > win) return false;
+        spans[b] = (int32_t)(run - r0s[b] + 1);
+    }
+    pre.assign(nsb, 0);
+    off.assign(nsb + 1, 0);
+    pre[0] = (int32_t)spill_in;
+    if (spill_in > r0s[1] - r0s[0]) return false;
+    for (int64_t b = 1; b < nsb; ++b) {
+        pre[b] = (int32_t)(spans[b - 1] - (r0s[b] - r0s[b - 1]));
+        if (pre[b] > r0s[b + 1] - r0s[b]) return false;  // would reach two superblocks ahead
+    }
+    if (spans[nsb - 1] - (r0s[nsb] - r0s[nsb - 1]) > spill_out) return false;
+    for (int64_t b = 0; b < nsb; ++b) off[b + 1] = off[b] + pre[b];
+    return true;
+}
+
 int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& r0s,
-                 std::vector<int32_t>& spans, std::vector<int32_t>& pre, std::vector<int64_t>& off) {
+                 std::vector<int32_t>& spans, std::vector<int32_t>& pre, std::vector<int64_t>& off,
+                 int64_t spill_in, int64_t spill_out) {
+    constexpr int64_t kQuantum = 256;
+    if (n <= 0) return -1;
+    int64_t m = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c = std::max<int64_t>(cmax[i], i);
+        if (c >= n + spill_out || c - i + 1 > win) return -1;
+        m = std::max<int64_t>(m, c - i);
+    }
+    auto balanced = [&](int64_t k) {
+        r0s.resize(k + 1);
+        for (int64_t b = 0; b <= k; ++b) r0s[b] = b * n / k;
+        return plan_check(n, cmax, win, r0s, spans, pre, off, spill_in, spill_out);
+    };
+    const int64_t rmax = win - m;  // >= 1
+    const int64_t k0 = (n + rmax - 1) / rmax;
+    const int64_t kq = (k0 + kQuantum - 1) / kQuantum * kQuantum;
+    if (kq <= n && balanced(kq)) return 0;
+    if (balanced(k0)) return 0;
+    // greedy: extend each superblock while its window fits
     r0s.assign(1, 0);
-    spans.clear();
     int64_t start = 0, run = -1;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t c = std::max<int64_t>(cmax[i], i);
-        if (c >= n || c - i + 1 > win) return -1;
         const int64_t nrun = std::max(run, c);
         if (i > start && nrun - start + 1 > win) {
-            spans.push_back((int32_t)(run - start + 1));
             r0s.push_back(i);
             start = i;
             run = c;
@@ -226,34 +280,24 @@ int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& 
             run = nrun;
         }
     }
-    spans.push_back((int32_t)(run - start + 1));
     r0s.push_back(n);
-    const int64_t nsb = (int64_t)spans.size();
-    pre.assign(nsb, 0);
-    off.assign(nsb + 1, 0);
-    for (int64_t b = 1; b < nsb; ++b) {
-        const int64_t Rp = r0s[b] - r0s[b - 1], Rb = r0s[b + 1] - r0s[b];
-        pre[b] = (int32_t)(spans[b - 1] - Rp);
-        if (pre[b] > Rb) return -1;  // the spill would reach two superblocks ahead
-    }
-    if (spans[nsb - 1] != (int32_t)(n - r0s[nsb - 1])) return -1;
-    for (int64_t b = 0; b < nsb; ++b) off[b + 1] = off[b] + pre[b];
-    return 0;
+    return plan_check(n, cmax, win, r0s, spans, pre, off, spill_in, spill_out) ? 0 : -1;
 }
 
 // Host analysis (once per matrix): greedy superblocks under the window, the
 // spill-inside-the-next-superblock rule, SELL slices of the upper rows.
 // -1 when the matrix does not fit the scheme (rectangular / distributed, a row
 // wider than the window, or a spill reaching past the next superblock).
-int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
+int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int64_t spill_out,
+                      void** owned) {
     const int64_t n = A.n;
-    if (ncols != n || n <= 0 || n >= (int64_t)INT32_MAX) return -1;
+    if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
     int32_t *dcnt = nullptr, *dcm = nullptr;
     if (hipMalloc(&dcnt, sizeof(int32_t) * n) || hipMalloc(&dcm, sizeof(int32_t) * n)) return -2;
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dcnt,
-                       dcm);
+    hipLaunchKernelGGL(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
+                       dcnt, dcm);
     std::vector<int32_t> cnt(n), cm(n);
     (void)hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
     (void)hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
@@ -261,7 +305,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
     (void)hipFree(dcm);
     std::vector<int64_t> r0s, off;
     std::vector<int32_t> spans, pre;
-    if (symsell_plan(n, cm.data(), kSymWin, r0s, spans, pre, off) != 0) return -1;
+    if (symsell_plan(n, cm.data(), kSymWin, r0s, spans, pre, off, spill_in, spill_out) != 0) return -1;
     const int64_t nsb = (int64_t)spans.size();
     // SELL-64 slices of the upper rows, longest first (stable)
     std::vector<int64_t> slice0{0}, sptr{0}, slice_r0;
@@ -284,7 +328,9 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
         }
         slice0.push_back((int64_t)sptr.size() - 1);
     }
+    // slots: off[nsb] combined rows, then the outgoing spill (spill_out)
     const int64_t ns = (int64_t)sptr.size() - 1, padded = sptr.back(), ncomb = off[nsb];
+    const int64_t nslot = ncomb + spill_out;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t b_r0 = sizeof(int64_t) * (nsb + 1), b_sp = sizeof(int32_t) * nsb,
                  b_pre = sizeof(int32_t) * nsb, b_off = sizeof(int64_t) * (nsb + 1),
@@ -292,7 +338,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
                  b_row = sizeof(int32_t) * srow.size(),
                  b_val = sizeof(double) * (size_t)std::max<int64_t>(padded, 1),
                  b_cw = sizeof(uint16_t) * (size_t)std::max<int64_t>(padded, 1),
-                 b_slot = sizeof(double) * (size_t)std::max<int64_t>(ncomb, 1);
+                 b_slot = sizeof(double) * (size_t)std::max<int64_t>(nslot, 1);
     char* d = nullptr;
     if (hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) + up(b_row) +
                           up(b_val) + up(b_cw) + 2 * up(b_slot)))
@@ -328,9 +374,11 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
             return -2;
         }
         (void)hipMemcpy(d_sr0, slice_r0.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d_ptr, d_row, d_sr0,
-                           A.rowptr, A.col, A.val, d_cw, d_val);
+        hipLaunchKernelGGL(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, coff, d_ptr, d_row,
+                           d_sr0, A.rowptr, A.col, A.val, d_cw, d_val);
     }
+    // the outgoing spill's tail past the last window is never written: zero it once
+    (void)hipMemset(d_lo, 0, b_slot);
     const bool ok = hipDeviceSynchronize() == hipSuccess;
     if (d_sr0) (void)hipFree(d_sr0);
     if (!ok) {
@@ -352,15 +400,17 @@ int csr_build_symsell(Csr& A, int64_t ncols, void** owned) {
     A.ss_nnz = nnz_u;
     A.ss_padded = padded;
     A.ss_ncomb = ncomb;
+    A.ss_coff = coff;
+    A.ss_spill_out = spill_out;
     *owned = d;
     return 0;
 }
 
-void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
+void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) {
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((unsigned)A.ss_nsb), dim3(kSymThreads), 0, s, A.ss_sb_r0,
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
-                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi);
+                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff);
     };
     // measured on the NS operator (tools/spmv_sym_time.py, one process): U = 8
     // with non-temporal val/col loads 0.594 ms incl. the combine; U = 8 plain
@@ -376,20 +426,29 @@ void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
         case 6: go(k_csr_ssell<12, 0, true>); break;
         default: go(k_csr_ssell<8, 0, true>); break;
     }
+}
+
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
     if (A.ss_ncomb > 0)
         hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)A.ss_nsb), dim3(256), 0, s, A.ss_sb_r0,
                            A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y);
+}
+
+void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
+    csr_spmv_sym_main(s, A, x, y);
+    csr_spmv_sym_combine(s, A, y);
 }
 
 }  // namespace ahip::dev
 
 // Host-only view of the plan (CPU-tested, tests/test_symsell_plan.py): writes
 // nsb, then r0s[0..nsb], spans[0..nsb), pre[0..nsb) (caller sizes them n + 1).
-extern "C" int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t* nsb,
-                                           int64_t* r0s, int32_t* spans, int32_t* pre) {
+extern "C" int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t spill_in,
+                                           int64_t spill_out, int64_t* nsb, int64_t* r0s, int32_t* spans,
+                                           int32_t* pre) {
     std::vector<int64_t> r, o;
     std::vector<int32_t> sp, pr;
-    const int rc = ahip::dev::symsell_plan(n, cmax, win, r, sp, pr, o);
+    const int rc = ahip::dev::symsell_plan(n, cmax, win, r, sp, pr, o, spill_in, spill_out);
     *nsb = rc == 0 ? (int64_t)sp.size() : 0;
     if (rc != 0) return rc;
     std::copy(r.begin(), r.end(), r0s);

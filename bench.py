@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--storage", choices=("sym", "full"), default="sym",
                     help="sym: the operator is declared symmetric (dsaupd's contract) and the "
                          "SpMV streams its upper triangle (arpack_hip_csr_set_symmetric); full: "
-                         "full CSR, bitwise SciPy's csr_matvec.  Multi-GPU row blocks use full.")
+                         "full CSR, bitwise SciPy's csr_matvec.")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
     args = ap.parse_args()
@@ -138,7 +138,7 @@ def main():
     if world > 1:
         D = pkg.DistOp(A, n, r0)
     storage = "full"
-    if world == 1 and args.storage == "sym":
+    if args.storage == "sym":  # row blocks: upper-triangle SpMV + forward spill exchange
         A.set_symmetric(True)
         storage = "sym"
     gen_s = time.time() - t
@@ -175,7 +175,7 @@ def main():
         return s, ido, t1 - t0, pkg.stats()["nopx"] - it0
 
     full_storage = None
-    if storage == "sym" and not args.no_full_storage:
+    if storage == "sym" and world == 1 and not args.no_full_storage:
         # the same K cycles with the full-storage (bitwise csr_matvec) SpMV, reported beside
         A.set_symmetric(False)
         s_f, ido_f, el_f, nopx_f = timed_run()

@@ -308,6 +308,10 @@ typedef struct arpack_hip_dist arpack_hip_dist;
  * row blocks are not contiguous or a halo reaches beyond the neighbours. */
 int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_global, int64_t row0);
 void arpack_hip_dist_destroy(arpack_hip_dist* D);
+/* y = A x on this rank's rows (device pointers), collective over the ranks:
+ * halo exchange + local SpMV (+ the forward spill exchange when the local CSR
+ * was declared symmetric with arpack_hip_csr_set_symmetric). */
+int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y);
 int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
                          int64_t* send_lo, int64_t* send_hi);
 /* Row-block decomposition without an operator: rank owns rows [row0, row0+nloc)
@@ -344,13 +348,15 @@ void arpack_hip_pdneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny
 int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out);
 /* Host half of arpack_hip_csr_set_symmetric's analysis (no GPU): the symmetric
  * superblock plan from each row's largest upper column cmax[i] for an LDS
- * window of `win` columns.  Writes *nsb, r0s[0..nsb] (row bounds), spans[0..nsb)
+ * window of `win` columns; spill_in / spill_out: rows reached from / into the
+ * neighbouring ranks (0 on one GPU).  Writes *nsb, r0s[0..nsb] (row bounds), spans[0..nsb)
  * (window lengths) and pre[0..nsb) (leading rows combined with the previous
  * superblock's spill); the caller sizes the arrays n + 1.  -1 if the matrix
  * does not fit (a row wider than the window, or a spill past the next
  * superblock). */
-int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t* nsb, int64_t* r0s,
-                                int32_t* spans, int32_t* pre);
+int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int win, int64_t spill_in,
+                                int64_t spill_out, int64_t* nsb, int64_t* r0s, int32_t* spans,
+                                int32_t* pre);
 /* Distributed free-running dsaupd (n = LOCAL rows, device arrays), cycle-parked
  * like arpack_hip_dsaupd_csr_cycles.  All ranks call it collectively. */
 void arpack_hip_pdsaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int* ido,

@@ -9,7 +9,9 @@ logic, halo plan + extended-x SpMV, global-offset start vector, row-local V*Q)
 is the one the 8-GPU job runs.
 
   python tests/dist_worker.py CASE FIXTURE OUTDIR [info0]
-CASE: sym_csr (pdsaupd_csr_cycles), ns_csr (pdnaupd_csr_cycles),
+CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
+      declared symmetric: upper-triangle SpMV + forward spill exchange; also
+      checks one distributed SpMV against SciPy), ns_csr (pdnaupd_csr_cycles),
       sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather).
 Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
 import os
@@ -55,7 +57,7 @@ def main():
     s = cls(nloc, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
             mxiter=int(g["mxiter"]), v0=v0, device=(case != "sym_rci"))
     res = {}
-    if case in ("sym_csr", "ns_csr"):
+    if case in ("sym_csr", "sym_csr_s", "ns_csr"):
         if str(g["spec"][0]) == "banded_sym":  # the device generator's row-range form
             A = pkg.CSR.banded_sym(n, int(g["spec"][2]), int(g["spec"][3]), int(g["spec"][4]),
                                    r0, r1)
@@ -67,6 +69,17 @@ def main():
             A = pkg.CSR.from_arrays(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]])
         D = pkg.DistOp(A, n, r0)
         res["halo"] = np.array(list(D.info().values()))
+        if case == "sym_csr_s":
+            A.set_symmetric(True)
+            x = np.random.default_rng(7).standard_normal(n)
+            xd = pkg.DeviceBuffer.from_numpy(x[r0:r1].copy())
+            yd = pkg.DeviceBuffer(nloc)
+            D.matvec_device(xd, yd)
+            Aloc = M.to_scipy(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]], n)
+            scale = M.to_scipy(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]],
+                               np.abs(val[rp[r0]:rp[r1]]), n) @ np.abs(x)
+            err = np.abs(yd.numpy() - Aloc @ x)
+            res["spmv_ok"] = np.array([bool(np.all(err <= 64 * np.finfo(float).eps * scale))])
         assert pkg.pdsaupd_cycles(s, D, -1) == 99
     else:
         D = pkg.DistRows(nloc, r0, n)

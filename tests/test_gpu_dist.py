@@ -97,6 +97,28 @@ def test_sym_csr_ranks(tmp_path, golden, fixture):
     assert h[1][0] > 0 and h[1][1] > 0 and h[0][0] == 0 and h[2][1] == 0
 
 
+@pytest.mark.parametrize("fixture", ["g4_banded", "g3_anderson3d"])
+def test_sym_csr_symmetric_storage_ranks(tmp_path, golden, fixture):
+    """Local blocks declared symmetric (upper-triangle SpMV, transposed terms for
+    the next rank's rows sent forward as a spill): the distributed SpMV matches
+    SciPy row by row and the solve gives the reference's cycles and values."""
+    g = golden(fixture)
+    spec = g["spec"]
+    rp, col, val = (M.banded_sym(*[int(x) for x in spec[1:]]) if str(spec[0]) == "banded_sym"
+                    else M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4])))
+    A = M.to_scipy(rp, col, val)
+    for P in (1, 2, 3):
+        ranks = _run(tmp_path, "sym_csr_s", fixture, P)
+        for r in ranks:
+            assert bool(r["spmv_ok"][0])
+            assert int(r["info"][0]) == 0
+            assert int(r["iparam"][2]) == int(g["iparam"][2]), (P, r["iparam"][2])
+            assert int(r["iparam"][4]) == int(g["iparam"][4])
+        d = ranks[0]["d"]
+        np.testing.assert_allclose(np.sort(d), np.sort(g["d"]), rtol=1e-10)
+        assert _resid(A, _z(ranks), d) <= 1e-8
+
+
 def test_sym_csr_random_start(tmp_path, golden):
     """info = 0: the dlarnv start vector is drawn at global row offsets, so P
     ranks see the same v0 as one GPU -- same cycles and values."""

@@ -82,7 +82,7 @@ def test_symmetric_refused_for_wide_band(pkg):
     import scipy.sparse as sp
     n = 20000
     A = (sp.eye(n, format="lil") * 4.0)
-    A[0, 9500] = A[9500, 0] = -1.0
+    A[0, 15000] = A[15000, 0] = -1.0   # reach 15000 > the 10240-column window
     A = A.tocsr()
     A.sort_indices()
     rp, col, val = A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data

@@ -17,26 +17,27 @@ import pytest
 from oracle import matrices as M
 
 
-def _plan(pkg, cmax, win):
+def _plan(pkg, cmax, win, spill_in=0, spill_out=0):
     L = pkg.lib()
-    L.arpack_hip_kit_symsell_plan.argtypes = [C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
-                                              C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_kit_symsell_plan.argtypes = [C.c_int64, C.c_void_p, C.c_int, C.c_int64, C.c_int64,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     n = len(cmax)
     cm = np.ascontiguousarray(cmax, np.int32)
     nsb = np.zeros(1, np.int64)
     r0s = np.zeros(n + 1, np.int64)
     spans = np.zeros(n + 1, np.int32)
     pre = np.zeros(n + 1, np.int32)
-    rc = L.arpack_hip_kit_symsell_plan(n, cm.ctypes.data, win, nsb.ctypes.data, r0s.ctypes.data,
-                                       spans.ctypes.data, pre.ctypes.data)
+    rc = L.arpack_hip_kit_symsell_plan(n, cm.ctypes.data, win, spill_in, spill_out, nsb.ctypes.data,
+                                       r0s.ctypes.data, spans.ctypes.data, pre.ctypes.data)
     k = int(nsb[0])
     return rc, r0s[:k + 1], spans[:k], pre[:k]
 
 
-def _upper_cmax(rp, col):
+def _upper_cmax(rp, col, coff=0):
     n = len(rp) - 1
     cmax = np.arange(n, dtype=np.int64)
     rows = np.repeat(np.arange(n), np.diff(rp))
+    col = col.astype(np.int64) - coff
     up = col >= rows
     np.maximum.at(cmax, rows[up], col[up])
     return cmax
@@ -124,3 +125,47 @@ def test_symsell_plan_edge_sizes(pkg):
     assert rc in (0, -1)
     if rc == 0:
         assert np.all(pre[1:] <= np.diff(r0s)[1:])
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_symsell_plan_row_distribution(pkg, P):
+    """Rank blocks of a banded operator (as arpack_hip_dist_create hands them to
+    the symmetric layout): each block's plan with spill_in = the previous
+    rank's reach and spill_out = its own; local windows + the forward spill
+    added into the next rank's first rows reproduce the global A @ x."""
+    n, B = 6000, 300
+    rp, col, val = M.banded_sym(n, 1234, B, 9)
+    x = np.random.default_rng(9).standard_normal(n)
+    yref = M.to_scipy(rp, col, val) @ x
+    scale = M.to_scipy(rp, col, np.abs(val)) @ np.abs(x)
+    bounds = [(q * n // P, (q + 1) * n // P) for q in range(P)]
+    reach = []
+    for a, b in bounds:   # how far each block's upper rows reach past its end
+        c = col[rp[a]:rp[b]]
+        reach.append(max(0, int(c.max()) - (b - 1)))
+    y = np.zeros(n)
+    carry = None
+    for q, (a, b) in enumerate(bounds):
+        lrp = rp[a:b + 1] - rp[a]
+        lcol = col[rp[a]:rp[b]].astype(np.int64) - a          # diagonal at local index
+        lval = val[rp[a]:rp[b]]
+        sin = reach[q - 1] if q > 0 else 0
+        sout = reach[q] if q < P - 1 else 0
+        rc, r0s, spans, pre = _plan(pkg, _upper_cmax(lrp, lcol), 2048, sin, sout)
+        assert rc == 0 and pre[0] == sin
+        m = b - a
+        yl = np.zeros(m + sout)
+        for i in range(m):    # upper rows of the block, transposed terms included
+            for k in range(lrp[i], lrp[i + 1]):
+                j = lcol[k]
+                if j < i:
+                    continue
+                yl[i] += lval[k] * x[a + j]
+                if j != i:
+                    yl[j] += lval[k] * x[a + i]
+        if carry is not None:
+            yl[:len(carry)] += carry
+        y[a:b] = yl[:m]
+        carry = yl[m:]
+        assert spans[-1] - (r0s[-1] - r0s[-2]) <= sout
+    assert np.all(np.abs(y - yref) <= 1e-13 * scale)
