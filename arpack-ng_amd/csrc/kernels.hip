@@ -242,7 +242,18 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
             s = lane == 0 ? sums[k] : 0.0;
         } else {
-            for (int b = lane; b < nblk; b += 64) s += part[(int64_t)k * nblk + b];
+            // four independent chains so the strided loads overlap
+            const double* p = part + (int64_t)k * nblk;
+            double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            int b = lane;
+            for (; b + 192 < nblk; b += 256) {
+                s += p[b];
+                s1 += p[b + 64];
+                s2 += p[b + 128];
+                s3 += p[b + 192];
+            }
+            for (; b < nblk; b += 64) s += p[b];
+            s = (s + s1) + (s2 + s3);
         }
         s = wave_sum(s);
         if (lane == 0) s_sum[k] = s;
@@ -539,8 +550,14 @@ inline int grid_for(int64_t n, int per_block = kBlock, int cap = 8192) {
 // ================================================================ launchers ==
 
 int choose_nblk(int64_t n) {
+    // AHIP_NBLK: tuning knob for the partial-sum grid (default kMaxRedBlocks)
+    static const int64_t cap = [] {
+        const char* e = getenv("AHIP_NBLK");
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v >= 64 && v <= 8192 ? v : kMaxRedBlocks);
+    }();
     int64_t b = (n + kBlock - 1) / kBlock;
-    if (b > kMaxRedBlocks) b = kMaxRedBlocks;
+    if (b > cap) b = cap;
     if (b < 1) b = 1;
     return (int)b;
 }
@@ -681,6 +698,16 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
 
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums) {
     ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * m);
+    // AHIP_FUSED_FIN=0: two launches (per-slot reduction, then the phase logic)
+    static const bool fused = [] {
+        const char* e = getenv("AHIP_FUSED_FIN");
+        return !(e && e[0] == '0');
+    }();
+    if (!from_sums && fused) {  // one launch: the finalize block sums the partials itself
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, 0, m, (int)ph,
+                           j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
+        return;
+    }
     if (!from_sums) {
         // stage 2a: one workgroup per slot sums that slot's nblk partials (coalesced)
         hipLaunchKernelGGL(k_reduce_slots, dim3(m), dim3(256), 0, ws.stream, ws.part, ws.nblk, ws.sums,
