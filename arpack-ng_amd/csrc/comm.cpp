@@ -113,10 +113,10 @@ int arpack_hip_comm_allreduce(double* dev, int count) {
 namespace ahip {
 
 // Halo exchange of the distributed SpMV (grouped point-to-point over xGMI).
-static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s) {
+static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only) {
     const int r = c->rank, P = c->nranks;
-    const int64_t slo = r > 0 ? D.send_lo : 0, shi = r < P - 1 ? D.send_hi : 0;
-    const int64_t hlo = r > 0 ? D.halo_lo : 0, hhi = r < P - 1 ? D.halo_hi : 0;
+    const int64_t slo = r > 0 ? D.send_lo : 0, shi = r < P - 1 && !hi_only ? D.send_hi : 0;
+    const int64_t hlo = r > 0 && !hi_only ? D.halo_lo : 0, hhi = r < P - 1 ? D.halo_hi : 0;
     std::vector<double> b((size_t)(slo + shi + hlo + hhi));
     double *bsl = b.data(), *bsh = bsl + slo, *brl = bsh + shi, *brh = brl + hlo;
     if (slo) (void)hipMemcpyAsync(bsl, D.x_mid(), 8 * slo, hipMemcpyDeviceToHost, s);
@@ -150,17 +150,20 @@ void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, 
     (void)ncclGroupEnd();
 }
 
-void comm_halo(const Comm* c, const DistOp& D, hipStream_t s) {
+// hi_only: the symmetric-storage SpMV reads x only at and above its own rows,
+// so only the hi halo travels (my first rows to rank-1, rank+1's to me).
+void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only) {
     if (!c || c->nranks == 1) return;
-    if (c->h_halo) return comm_halo_host(c, D, s);
+    if (c->h_halo) return comm_halo_host(c, D, s, hi_only);
     const int r = c->rank, P = c->nranks;
     (void)ncclGroupStart();
     if (r > 0) {
         if (D.send_lo) (void)ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, c->nccl, s);
-        if (D.halo_lo) (void)ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, c->nccl, s);
+        if (D.halo_lo && !hi_only)
+            (void)ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, c->nccl, s);
     }
     if (r < P - 1) {
-        if (D.send_hi)
+        if (D.send_hi && !hi_only)
             (void)ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, c->nccl, s);
         if (D.halo_hi) (void)ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, c->nccl, s);
     }

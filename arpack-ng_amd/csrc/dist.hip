@@ -9,15 +9,16 @@
 #include "dist.hpp"
 
 namespace ahip {
-void comm_halo(const Comm* c, const DistOp& D, hipStream_t s);
+void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only);
 void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
                 hipStream_t s);
 
 void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
     if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
-    comm_halo(D.comm, D, s);
     const dev::Csr& A = *D.A;
-    if (A.kernel == dev::kCsrSymSell && A.ss_val) {
+    const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val;
+    comm_halo(D.comm, D, s, sym);
+    if (sym) {
         // symmetric storage: my rows' upper entries reach the next rank's first
         // rows -- those transposed terms (the spill) travel forward and are
         // combined into the receiver's leading rows (a reverse halo)

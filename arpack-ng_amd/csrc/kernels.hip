@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_place(int64_t n, const R* __restrict
 // ------------------------------------------------------------------- dots ---
 // Exact compile-time column count J (branch-free unrolled loads: all J column
 // loads of a row are in flight together).  WM: 0 no w'u, 1 w == u, 2 w != u.
-template <class R, int J, int WM>
+template <class R, int J, int WM, bool REV = false>
 __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __restrict__ V,
                                                  int64_t ld, const R* __restrict__ u,
                                                  const R* __restrict__ w,
@@ -132,7 +132,8 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
     // unchanged.
     constexpr int JL = J > 0 ? J : 1;
     double cur[JL], cu = 0.0, cw = 0.0;
-    auto load = [&](int64_t r, double (&dst)[JL], double& du, double& dw) {
+    auto load = [&](int64_t it, double (&dst)[JL], double& du, double& dw) {
+        const int64_t r = REV ? n - 1 - it : it;  // REV: sweep last-to-first (see k_update_fused)
 #pragma unroll
         for (int k = 0; k < J; ++k) dst[k] = Vb[r + (int64_t)k * ld];
         du = u[r];
@@ -606,6 +607,23 @@ struct ProfScope {  // event pair around one launch when profiling is on
 };
 }  // namespace
 
+// Sweep direction of the V passes.  Each pass starts where the previous one
+// ended, on the rows the 256 MB Infinity Cache still holds: within step j the
+// CGS dots, the CGS update and the first DGKS update alternate, and so do
+// consecutive steps (the SpMV between them streams its matrix with
+// non-temporal loads).  AHIP_SWEEP=0: all forward; 1: only the updates
+// alternate (dots forward); 2 (default): dots alternate per step too.
+static bool dir_rev(int j, int which, bool is_dots) {
+    static const int mode = [] {
+        const char* e = getenv("AHIP_SWEEP");
+        return e ? atoi(e) : 2;
+    }();
+    if (mode == 0) return false;
+    const bool d = mode == 2 && (j & 1);  // the dots pass of step j
+    if (is_dots) return d;
+    return which % 2 == 0 ? !d : d;      // CGS / second DGKS update: opposite; first DGKS: same
+}
+
 template <class R>
 void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc, int j) {
     ProfScope ps(kProfPlace, ws.stream,
@@ -618,7 +636,7 @@ void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc,
     M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16) \
     M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
 
-template <class R, int WM>
+template <class R, int WM, bool REV = false>
 static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R* V, int64_t ld,
                         const R* u, const R* w, int wslot, int gate) {
     const dim3 g(ws.nblk), b(kBlock);
@@ -629,8 +647,8 @@ static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R*
             break;
 #define AHIP_DOTS_CASE(J)                                                                          \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_dots<R, J, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,    \
-                           ws.stride, wslot, ws.st, gate);                                         \
+        hipLaunchKernelGGL((k_dots<R, J, WM, REV>), g, b, 0, ws.stream, n, j0, V, ld, u, w,        \
+                           ws.part, ws.stride, wslot, ws.st, gate);                                \
         break;
         AHIP_CASES_1_32(AHIP_DOTS_CASE)
 #undef AHIP_DOTS_CASE
@@ -648,9 +666,12 @@ void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R
         else launch_dots<R, 2>(ws, n, 0, 0, V, ld, u, w, 0, gate);
         return;
     }
+    // sweep direction alternates per Lanczos step (dir_rev, below)
+    const bool rev = dir_rev(j, 0, true);
     for (int j0 = 0; j0 < j; j0 += 32) {
         const int jc = (j - j0 < 32) ? j - j0 : 32;
         if (j0 > 0) launch_dots<R, 0>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else if (w == u && rev) launch_dots<R, 1, true>(ws, n, j0, jc, V, ld, u, w, j, gate);
         else if (w == u) launch_dots<R, 1>(ws, n, j0, jc, V, ld, u, w, j, gate);
         else launch_dots<R, 2>(ws, n, j0, jc, V, ld, u, w, j, gate);
     }
@@ -663,14 +684,7 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
     ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
                  gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 2));
     const dim3 g(ws.nblk), b(kBlock);
-    // alternate the sweep direction with the Gram-Schmidt sweep (which = 0:
-    // CGS update after the forward dots pass -> reversed; 1: first DGKS ->
-    // forward; 2: second DGKS -> reversed); AHIP_UPDATE_REV=0 disables
-    static const bool rev_on = [] {
-        const char* e = getenv("AHIP_UPDATE_REV");
-        return !(e && e[0] == '0');
-    }();
-    const bool rev = rev_on && (which % 2 == 0);
+    const bool rev = dir_rev(j, which, false);
     if (j >= 1 && j <= 32) {
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
