@@ -177,6 +177,7 @@ struct Csr {
     double* ss_hi = nullptr;               // prefix partials (written by superblock b)
     int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;
     int ss_variant = 0;                    // kernel variant (tools/spmv_sym_time.py)
+    int ss_chain = 1;                      // consecutive superblocks per workgroup
     int64_t ss_coff = 0;                   // x index of local row 0's diagonal (halo_lo)
     int64_t ss_spill_out = 0;              // rows of the next rank reached by the last window
 };

@@ -105,6 +105,14 @@ __device__ __forceinline__ T ldg(const T* p) {
     else return *p;
 }
 
+// One workgroup walks a CHAIN of `chain` consecutive superblocks (grid = the
+// CU count, one resident workgroup per CU: the windows take all 160 KB of
+// LDS).  A superblock's spill is the next one's window head, so inside a chain
+// it stays in LDS: the x and y windows shift down by R and only the new x
+// columns are loaded.  Only a chain's first superblock has head rows combined
+// with another workgroup's (or rank's) spill through the slots, and only its
+// last superblock's spill leaves through a slot.  Each wave streams its slices
+// with the next slice's first chunk in flight, across superblock boundaries.
 template <int U, int MODE, bool NT = false>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
@@ -112,93 +120,138 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
     const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
     const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
-    double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff) {
+    double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff, int chain,
+    int64_t nsb) {
     __shared__ double xw[kSymWin];
     __shared__ double yw[kSymWin];
     constexpr int NW = kSymThreads / 64;
+    constexpr int PT = kSymWin / kSymThreads;  // window elements per thread
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t sb = xcd_block(blockIdx.x, gridDim.x);
-    const int64_t r0 = sb_r0[sb];
-    const int R = (int)(sb_r0[sb + 1] - r0);
-    const int span = sb_span[sb];
-    const int64_t s0 = sb_slice0[sb], s1 = sb_slice0[sb + 1];
+    const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
     struct Chunk {
         double v[U];
         int c[U];
     };
-    auto load = [&](Chunk& ch, int64_t base, int w, int k0) {
+    auto load = [&](Chunk& c, int64_t base, int w, int k0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = k0 + u < w;
-            ch.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
-            ch.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
+            c.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
+            c.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
         }
     };
-    int64_t s = s0 + wave;
-    int64_t base = 0;
-    int w = 0;
+    auto geom = [&](int64_t sl, int64_t& base, int& w) {
+        base = sptr[sl];
+        w = (int)((sptr[sl + 1] - base) >> 6);
+    };
     Chunk cur, nxt;
-    if (s < s1) {
-        base = sptr[s];
-        w = (int)((sptr[s + 1] - base) >> 6);
-        load(cur, base, w, 0);
-    }
-    for (int i = t; i < span; i += kSymThreads) {
-        xw[i] = x[coff + r0 + i];
-        yw[i] = 0.0;
-    }
-    __syncthreads();
-    for (; s < s1; s += NW) {
-        const int row = srow[s * 64 + lane];
-        const int rl = row >= 0 ? row - (int)r0 : 0;
-        const double xi = xw[rl];
-        const int64_t sn = s + NW;
-        int64_t nbase = 0;
-        int nw = 0;
-        if (sn < s1) {
-            nbase = sptr[sn];
-            nw = (int)((sptr[sn + 1] - nbase) >> 6);
+    int64_t cur_s = -1;  // slice whose first chunk is in `cur`
+    {
+        const int64_t s = sb_slice0[b0] + wave;
+        if (s < sb_slice0[b0 + 1]) {
+            int64_t base;
+            int w;
+            geom(s, base, w);
+            load(cur, base, w, 0);
+            cur_s = s;
         }
-        double acc = 0.0;
-        int k = 0;
-        do {
-            if (k + U < w) load(nxt, base, w, k + U);
-            else if (sn < s1) load(nxt, nbase, nw, 0);
+    }
+    int R_prev = 0, span_prev = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+        const int64_t r0 = sb_r0[b];
+        const int R = (int)(sb_r0[b + 1] - r0);
+        const int span = sb_span[b];
+        const int64_t s1 = sb_slice0[b + 1];
+        int carry = 0;
+        if (b > b0) {  // the previous window's tail [R_prev, span_prev) becomes this head
+            carry = span_prev - R_prev;
+            double xs[PT], ys[PT];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = cur.c[u];
-                if (c >= 0) {
-                    if constexpr (MODE == 2) acc += cur.v[u] * (double)c;
-                    else acc += cur.v[u] * xw[c];
-                    if constexpr (MODE == 0)
-                        if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+            for (int q = 0; q < PT; ++q) {
+                const int i = t + q * kSymThreads;
+                if (i < carry) {
+                    xs[q] = xw[R_prev + i];
+                    ys[q] = yw[R_prev + i];
                 }
             }
-            cur = nxt;
-            k += U;
-        } while (k < w);
-        if (row >= 0) atomicAdd(&yw[rl], acc);
-        base = nbase;
-        w = nw;
-    }
-    __syncthreads();
-    const int pre = sb_pre[sb];
-    const int64_t off = sb_off[sb], offn = sb_off[sb + 1];
-    for (int i = t; i < span; i += kSymThreads) {
-        const double v = yw[i];
-        if (i < pre) slot_hi[off + i] = v;
-        else if (i < R) y[r0 + i] = v;
-        else slot_lo[offn + (i - R)] = v;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < PT; ++q) {
+                const int i = t + q * kSymThreads;
+                if (i < carry) {
+                    xw[i] = xs[q];
+                    yw[i] = ys[q];
+                }
+            }
+        }
+        for (int i = carry + t; i < span; i += kSymThreads) {
+            xw[i] = x[coff + r0 + i];
+            yw[i] = 0.0;
+        }
+        __syncthreads();
+        for (int64_t s = sb_slice0[b] + wave; s < s1; s += NW) {
+            int64_t base;
+            int w;
+            geom(s, base, w);
+            if (cur_s != s) load(cur, base, w, 0);
+            const int row = srow[s * 64 + lane];
+            const int rl = row >= 0 ? row - (int)r0 : 0;
+            const double xi = xw[rl];
+            // this wave's next slice: in this superblock, else its first in the next one
+            int64_t sn = s + NW;
+            if (sn >= s1) sn = b + 1 < b1 ? sb_slice0[b + 1] + wave : -1;
+            if (sn >= 0 && b + 1 < b1 && sn >= s1 && sn >= sb_slice0[b + 2]) sn = -1;
+            int64_t nbase = 0;
+            int nw = 0;
+            if (sn >= 0) geom(sn, nbase, nw);
+            double acc = 0.0;
+            int k = 0;
+            do {
+                if (k + U < w) load(nxt, base, w, k + U);
+                else if (sn >= 0) load(nxt, nbase, nw, 0);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = cur.c[u];
+                    if (c >= 0) {
+                        if constexpr (MODE == 2) acc += cur.v[u] * (double)c;
+                        else acc += cur.v[u] * xw[c];
+                        if constexpr (MODE == 0)
+                            if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+                    }
+                }
+                cur = nxt;
+                k += U;
+            } while (k < w);
+            cur_s = sn;
+            if (row >= 0) atomicAdd(&yw[rl], acc);
+        }
+        __syncthreads();
+        // head rows meet another chain's spill through the slots; the rest are final
+        const int head = b == b0 ? sb_pre[b] : 0;
+        const int64_t off = sb_off[b];
+        for (int i = t; i < R; i += kSymThreads) {
+            const double v = yw[i];
+            if (i < head) slot_hi[off + i] = v;
+            else y[r0 + i] = v;
+        }
+        if (b == b1 - 1) {  // the chain's last spill leaves through a slot
+            const int64_t offn = sb_off[b + 1];
+            for (int i = R + t; i < span; i += kSymThreads) slot_lo[offn + (i - R)] = yw[i];
+        }
+        R_prev = R;
+        span_prev = span;
     }
 }
 
+// y(head rows of each chain's first superblock) = lo + hi
 __global__ __launch_bounds__(256) void k_ssell_combine(const int64_t* __restrict__ sb_r0,
                                                        const int32_t* __restrict__ sb_pre,
                                                        const int64_t* __restrict__ sb_off,
                                                        const double* __restrict__ lo,
                                                        const double* __restrict__ hi,
-                                                       double* __restrict__ y) {
-    const int64_t b = blockIdx.x;
+                                                       double* __restrict__ y, int chain) {
+    const int64_t b = (int64_t)blockIdx.x * chain;
     const int pre = sb_pre[b];
     const int64_t off = sb_off[b], r0 = sb_r0[b];
     for (int i = threadIdx.x; i < pre; i += 256) y[r0 + i] = lo[off + i] + hi[off + i];
@@ -247,8 +300,7 @@ static bool plan_check(int64_t n, const int32_t* cmax, int win, std::vector<int6
 
 int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& r0s,
                  std::vector<int32_t>& spans, std::vector<int32_t>& pre, std::vector<int64_t>& off,
-                 int64_t spill_in, int64_t spill_out) {
-    constexpr int64_t kQuantum = 256;
+                 int64_t spill_in, int64_t spill_out, int64_t kQuantum) {
     if (n <= 0) return -1;
     int64_t m = 0;
     for (int64_t i = 0; i < n; ++i) {
@@ -305,7 +357,11 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     (void)hipFree(dcm);
     std::vector<int64_t> r0s, off;
     std::vector<int32_t> spans, pre;
-    if (symsell_plan(n, cm.data(), kSymWin, r0s, spans, pre, off, spill_in, spill_out) != 0) return -1;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || ncu < 1)
+        ncu = 256;
+    if (symsell_plan(n, cm.data(), kSymWin, r0s, spans, pre, off, spill_in, spill_out, ncu) != 0)
+        return -1;
     const int64_t nsb = (int64_t)spans.size();
     // SELL-64 slices of the upper rows, longest first (stable)
     std::vector<int64_t> slice0{0}, sptr{0}, slice_r0;
@@ -397,6 +453,8 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_lo = d_lo;
     A.ss_hi = d_hi;
     A.ss_nsb = nsb;
+    // chains of consecutive superblocks, one workgroup per CU (k_csr_ssell)
+    A.ss_chain = (nsb >= ncu && nsb % ncu == 0) ? (int)(nsb / ncu) : 1;
     A.ss_nnz = nnz_u;
     A.ss_padded = padded;
     A.ss_ncomb = ncomb;
@@ -406,11 +464,16 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     return 0;
 }
 
+// variant 7: no chaining (one superblock per workgroup launch), for A/B
+static int sym_chain(const Csr& A) { return A.ss_variant == 7 ? 1 : A.ss_chain; }
+
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) {
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned)A.ss_nsb), dim3(kSymThreads), 0, s, A.ss_sb_r0,
+        const int chain = sym_chain(A);
+        const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+        hipLaunchKernelGGL(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
-                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff);
+                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb);
     };
     // measured on the NS operator (tools/spmv_sym_time.py, one process): U = 8
     // with non-temporal val/col loads 0.594 ms incl. the combine; U = 8 plain
@@ -429,9 +492,11 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
 }
 
 void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
+    const int chain = sym_chain(A);
+    const int64_t nch = (A.ss_nsb + chain - 1) / chain;
     if (A.ss_ncomb > 0)
-        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)A.ss_nsb), dim3(256), 0, s, A.ss_sb_r0,
-                           A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y);
+        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)nch), dim3(256), 0, s, A.ss_sb_r0,
+                           A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
 }
 
 void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
@@ -448,7 +513,7 @@ extern "C" int arpack_hip_kit_symsell_plan(int64_t n, const int32_t* cmax, int w
                                            int32_t* pre) {
     std::vector<int64_t> r, o;
     std::vector<int32_t> sp, pr;
-    const int rc = ahip::dev::symsell_plan(n, cmax, win, r, sp, pr, o, spill_in, spill_out);
+    const int rc = ahip::dev::symsell_plan(n, cmax, win, r, sp, pr, o, spill_in, spill_out, 256);
     *nsb = rc == 0 ? (int64_t)sp.size() : 0;
     if (rc != 0) return rc;
     std::copy(r.begin(), r.end(), r0s);

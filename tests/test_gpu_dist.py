@@ -119,6 +119,13 @@ def test_sym_csr_symmetric_storage_ranks(tmp_path, golden, fixture):
         assert _resid(A, _z(ranks), d) <= 1e-8
 
 
+def test_symmetric_storage_chained_blocks(tmp_path):
+    """2 ranks x 3e6 rows: each rank's plan chains superblocks; the distributed
+    symmetric SpMV (forward spill) equals the full-storage one to rounding."""
+    for r in _run(tmp_path, "spmv_chain", "-", 2):
+        assert bool(r["spmv_ok"][0]), r["maxdiff"]
+
+
 def test_sym_csr_random_start(tmp_path, golden):
     """info = 0: the dlarnv start vector is drawn at global row offsets, so P
     ranks see the same v0 as one GPU -- same cycles and values."""
