@@ -139,8 +139,20 @@ def main():
         D = pkg.DistOp(A, n, r0)
     storage = "full"
     if args.storage == "sym":  # row blocks: upper-triangle SpMV + forward spill exchange
-        A.set_symmetric(True)
-        storage = "sym"
+        try:
+            A.set_symmetric(True)
+            ok = 1
+        except RuntimeError:
+            ok = 0
+        if dist:  # every rank must run the same SpMV mode (the exchanges differ)
+            import torch
+            t_ok = torch.tensor([ok], dtype=torch.int64)
+            dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+            ok = int(t_ok.item())
+        if ok:
+            storage = "sym"
+        else:
+            A.set_symmetric(False)
     gen_s = time.time() - t
     nnz = A.nnz
     if dist:

@@ -223,7 +223,10 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * superblock fit the LDS windows; otherwise returns -1 and A keeps its
  * full-storage kernel.  y is then not bitwise reproducible run to run
  * (transposed terms are summed in LDS in schedule order).  on == 0 restores
- * the full-storage kernel. */
+ * the full-storage kernel.  For a row-distributed operator (after
+ * arpack_hip_dist_create) every rank must end up in the same mode: the halo and
+ * spill exchanges differ, so call it on all ranks and fall back together if
+ * any rank returns -1. */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
