@@ -24,7 +24,8 @@ from functools import partial
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libarpack_hip.so")
+# ARPACK_HIP_LIB: load another build of the library (same-box A/B of build variants)
+LIB_PATH = os.environ.get("ARPACK_HIP_LIB") or os.path.join(HERE, "libarpack_hip.so")
 
 _lib = None
 

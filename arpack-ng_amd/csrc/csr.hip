@@ -199,7 +199,7 @@ void analyse_window_sell(arpack_hip_csr* A, int64_t ncols) {
     A->A.kernel = ahip::dev::kCsrWVecX;
     if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
         A->A.kernel = ahip::dev::kCsrSell;
-        A->A.s_unroll = 4;
+        A->A.s_unroll = 10;  // U = 4 with non-temporal val/col loads (tools/spmv_full_time.py)
     }
 }
 
@@ -309,7 +309,7 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
     if (kernel == ahip::dev::kCsrSell) {  // tile selects the unroll (4, 8, 16)
         if (!A->sell && ahip::dev::csr_build_sell(A->A, &A->sell) != 0) return -1;
         A->A.kernel = kernel;
-        A->A.s_unroll = (tile >= 2 && tile <= 8) ? tile : 4;  // 5, 7: two slices per wave
+        A->A.s_unroll = (tile >= 2 && tile <= 11) ? tile : 4;  // 5, 7: two slices per wave; 9-11 NT
         return 0;
     }
     if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVecP4) {

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvecp(
 // whole slices (lane = row); a column step is one coalesced 512-B val load and
 // one 128-B colw load per wave.  Each row is summed sequentially in its CSR
 // (column) order.
-template <int U, bool XCD>
+template <int U, bool XCD, bool NTL = false>
 __global__ __launch_bounds__(kWinThreads) void k_csr_sell(
     const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
     const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
@@ -397,8 +397,8 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_sell(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = k0 + u < w;
-            ch.v[u] = in ? sval[base + (int64_t)(k0 + u) * 64 + lane] : 0.0;
-            ch.c[u] = in ? (int)scolw[base + (int64_t)(k0 + u) * 64 + lane] : 0;
+            ch.v[u] = in ? ld<double, NTL>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
+            ch.c[u] = in ? (int)ld<uint16_t, NTL>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : 0;
         }
     };
     int64_t s = s0 + wave;
@@ -793,6 +793,9 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
                                A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y);
         };
         if (A.s_unroll == 4) go(k_csr_sell<4, true>);
+        else if (A.s_unroll == 9) go(k_csr_sell<8, true, true>);   // non-temporal val/col
+        else if (A.s_unroll == 10) go(k_csr_sell<4, true, true>);
+        else if (A.s_unroll == 11) go(k_csr_sell<6, true, true>);
         else if (A.s_unroll == 2) go(k_csr_sell<2, true>);
         else if (A.s_unroll == 3) go(k_csr_sell<3, true>);
         else if (A.s_unroll == 6) go(k_csr_sell<6, true>);
