@@ -370,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t l
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         double v[MAXK];
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) v[k] = (k < kplusp) ? V[i + (int64_t)k * ld] : 0.0;
+        for (int k = 0; k < MAXK; ++k) v[k] = (k < kplusp) ? (double)vld(V + i + (int64_t)k * ld) : 0.0;
         double vnext = 0.0;
         if (next) {
 #pragma unroll

@@ -113,7 +113,7 @@ __device__ __forceinline__ T ldg(const T* p) {
 // with another workgroup's (or rank's) spill through the slots, and only its
 // last superblock's spill leaves through a slot.  Each wave streams its slices
 // with the next slice's first chunk in flight, across superblock boundaries.
-template <int U, int MODE, bool NT = false>
+template <int U, bool NT>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
     const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
@@ -214,10 +214,8 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
                 for (int u = 0; u < U; ++u) {
                     const int c = cur.c[u];
                     if (c >= 0) {
-                        if constexpr (MODE == 2) acc += cur.v[u] * (double)c;
-                        else acc += cur.v[u] * xw[c];
-                        if constexpr (MODE == 0)
-                            if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+                        acc += cur.v[u] * xw[c];
+                        if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
                     }
                 }
                 cur = nxt;
@@ -475,19 +473,18 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
                            A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb);
     };
-    // measured on the NS operator (tools/spmv_sym_time.py, one process): U = 8
-    // with non-temporal val/col loads 0.594 ms incl. the combine; U = 8 plain
-    // 0.611, U = 12 0.611, U = 6 0.626, U = 4 0.652, U = 2 0.671, U = 16 spills.
-    // Diagnostics: without the transposed LDS adds 0.611 (U = 4), without any
-    // LDS traffic 0.559 -- the slice stream itself, not the atomics, bounds it.
-    switch (A.ss_variant) {  // 1, 2: diagnostic (wrong y): no transposed adds / no LDS at all
-        case 1: go(k_csr_ssell<4, 1>); break;
-        case 2: go(k_csr_ssell<4, 2>); break;
-        case 3: go(k_csr_ssell<8, 0>); break;
-        case 4: go(k_csr_ssell<4, 0>); break;
-        case 5: go(k_csr_ssell<6, 0, true>); break;
-        case 6: go(k_csr_ssell<12, 0, true>); break;
-        default: go(k_csr_ssell<8, 0, true>); break;
+    // measured on the NS operator (tools/spmv_sym_time.py, one process, before
+    // chaining): U = 8 with non-temporal val/col loads 0.594 ms incl. the
+    // combine; U = 8 plain 0.611, U = 12 0.611, U = 6 0.626, U = 4 0.652,
+    // U = 2 0.671, U = 16 spills.  Diagnostic builds (wrong y, not kept):
+    // without the transposed LDS adds 0.611 (U = 4), without any LDS traffic
+    // 0.559 -- the slice stream, not the atomics, bounds it.
+    switch (A.ss_variant) {  // alternative unrolls for tools/spmv_sym_time.py
+        case 3: go(k_csr_ssell<8, false>); break;
+        case 4: go(k_csr_ssell<4, false>); break;
+        case 5: go(k_csr_ssell<6, true>); break;
+        case 6: go(k_csr_ssell<12, true>); break;
+        default: go(k_csr_ssell<8, true>); break;  // 7: the same without chaining
     }
 }
 

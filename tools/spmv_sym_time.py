@@ -32,7 +32,7 @@ def main():
     A.set_symmetric(True)
     out["sym_ms"] = A.time_spmv(a.reps)
     A.matvec_device(x.at(0), y2.at(0))
-    for v in (1, 2, 5, 6, 7):
+    for v in (3, 4, 5, 6, 7):
         A.set_kernel(12, v)
         out["sym_v%d_ms" % v] = A.time_spmv(a.reps)
     A.set_kernel(12, 0)
