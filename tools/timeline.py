@@ -22,7 +22,7 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
         c = sqlite3.connect(f)
         names = [r[0] for r in c.execute("select name from sqlite_master where type in ('table','view')")]
-        tab = next((n for n in names if n.lower() in ("kernels", "rocpd_kernel_dispatch")), None)
+        tab = "kernels" if "kernels" in names else None  # rocpd view with kernel names
         if tab is None:
             tab = next(n for n in names if "kernel" in n.lower() and "dispatch" in n.lower())
         cols = [r[1] for r in c.execute("pragma table_info(%s)" % tab)]
