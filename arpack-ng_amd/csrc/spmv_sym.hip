@@ -343,7 +343,11 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     const int64_t n = A.n;
     if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
     int32_t *dcnt = nullptr, *dcm = nullptr;
-    if (hipMalloc(&dcnt, sizeof(int32_t) * n) || hipMalloc(&dcm, sizeof(int32_t) * n)) return -2;
+    if (hipMalloc(&dcnt, sizeof(int32_t) * n) != hipSuccess) return -2;
+    if (hipMalloc(&dcm, sizeof(int32_t) * n) != hipSuccess) {
+        (void)hipFree(dcnt);
+        return -2;
+    }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     hipLaunchKernelGGL(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
