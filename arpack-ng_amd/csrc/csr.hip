@@ -277,7 +277,8 @@ int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* c
 
 int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
     ahip::dev::csr_spmv(nullptr, A->A, x, y);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    // synchronous like the reference callers' OP: y is complete on return
+    return hipStreamSynchronize(nullptr) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {

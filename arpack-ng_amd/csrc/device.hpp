@@ -37,11 +37,13 @@ struct LzState {
     double beta;    // h(j,1)
     int dgks;       // 0: none pending, 1: first refinement pending, 2: second
     int zero;       // residual must be zeroed (refinement failed twice)
-    int abort;      // rnorm == 0 at the start of step abort_j: host restart needed
+    int abort;      // 1: rnorm == 0 at the start of step abort_j (host restart);
+                    // 2: step abort_j needs its second DGKS refinement (kFinDgks1Lazy)
     int abort_j;
     int nrorth;     // counters accumulated on device, drained by the host
     int nitref;
-    int pad[2];
+    int force_dgks2;  // test hook (AHIP_FORCE_DGKS2=1): always take the second refinement
+    int pad;
 };
 
 // Finalize phases (which logic the single-block finalize kernel applies).
@@ -53,6 +55,8 @@ enum FinPhase : int {
     kFinDgks2 = 4,    // second refinement check / give up         (SRC/dsaitr.f:753-781)
     kFinRaw = 5,      // just store the sums (host reads them)
     kFinCoef = 6,     // coef0 = first m-1 sums, state untouched   (getv0 CGS)
+    kFinDgks1Lazy = 7,  // kFinDgks1; a needed second refinement parks the cycle
+                        // (st.abort = 2 at step j) for the host to finish it
 };
 
 struct Workspace {

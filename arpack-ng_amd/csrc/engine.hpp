@@ -146,6 +146,7 @@ private:
     void fin(int m, dev::FinPhase ph, int j, int rstart, int gate);
     R* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
     R* dist_x();  // the distributed operator's x window (double only)
+    void dgks2_tail(int j, int rstart);
 public:
     const R* op_x = nullptr;  // device pointers of the pending OP request
     R* op_y = nullptr;

@@ -313,8 +313,8 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                 st->nrorth += 1;
                 take = 1;
             }
-        } else if (phase == kFinDgks1) {
-            if (rn > 0.717 * st->rnorm) {
+        } else if (phase == kFinDgks1 || phase == kFinDgks1Lazy) {
+            if (rn > 0.717 * st->rnorm && !st->force_dgks2) {
                 st->rnorm = rn;
                 st->dgks = 0;
             } else {
@@ -322,6 +322,10 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                 st->rnorm = rn;
                 st->dgks = 2;
                 take = 2;
+                if (phase == kFinDgks1Lazy) {  // rare: the host runs the second sweep
+                    st->abort = 2;
+                    st->abort_j = j;
+                }
             }
         } else {  // kFinDgks2
             if (rn > 0.717 * st->rnorm) {
@@ -591,8 +595,12 @@ hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
         return e;
-    (void)hipMemsetAsync(ws.st, 0, sizeof(LzState), s);
     memset(ws.st_host, 0, sizeof(LzState));
+    {   // test hook: exercise the (rare) second DGKS refinement on every step
+        const char* e = getenv("AHIP_FORCE_DGKS2");
+        ws.st_host->force_dgks2 = (e && e[0] == '1') ? 1 : 0;
+    }
+    (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(LzState), hipMemcpyHostToDevice, s);
     (void)hipMemsetAsync(ws.coef, 0, sizeof(double) * 3 * (size_t)ws.stride, s);
     return hipSuccess;
 }

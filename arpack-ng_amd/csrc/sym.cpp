@@ -95,6 +95,11 @@ template <class R>
 void ArraysT<R>::h2d_workd(int64_t off, int64_t len) {
     if (host_mode && off >= 0)
         ck(hipMemcpyAsync(d_workd + off, h_workd + off, sizeof(R) * len, hipMemcpyHostToDevice, stream));
+    // device-pointer mode: the caller produced workd(off) with its own GPU work,
+    // possibly still in flight on another stream (the engine's stream does not
+    // order against them) -- the reverse-communication contract is that the
+    // request is complete when *aupd is called again, so make it so
+    if (!host_mode && off >= 0) ck(hipDeviceSynchronize());
 }
 
 template <class R>
@@ -130,6 +135,15 @@ RciAwait SolverT<R>::op(int ido, int64_t x, int64_t y, int64_t bx, const R* xp, 
     op_x = xp;
     op_y = yp;
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+// The second DGKS refinement of step j (SRC/dsaitr.f:753-781), gated on the
+// device decision, and the give-up zeroing of r.
+template <class R>
+void SolverT<R>::dgks2_tail(int j, int rstart) {
+    dev::update(ws, (int64_t)n, j, a.d_v, a.d_ld, 2, a.d_resid, a.d_resid, true, 2);
+    fin(j + 1, dev::kFinDgks2, j, rstart, 2);
+    dev::zero_if(ws, (int64_t)n, a.d_resid);
 }
 
 template <class R>
@@ -295,10 +309,12 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 fin(j + 1, dev::kFinPostCgs, j, rstart, -1);
                 // refinement sweeps, each gated on the device-side decision
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1);
-                fin(j + 1, dev::kFinDgks1, j, rstart, 1);
-                dev::update(ws, nn, j, a.d_v, a.d_ld, 2, a.d_resid, a.d_resid, true, 2);
-                fin(j + 1, dev::kFinDgks2, j, rstart, 2);
-                dev::zero_if(ws, nn, a.d_resid);
+                // free-running: the second refinement (rare) is not enqueued; if
+                // step j needs it, the finalize parks the cycle (abort = 2) and
+                // the host finishes the step below
+                const bool lazy = free_run;
+                fin(j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
+                if (!lazy) dgks2_tail(j, rstart);
             } else {
                 // generalized problem: every B*r is a reverse-communication request,
                 // so the refinement decisions are taken on the host.
@@ -329,6 +345,15 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
+        if (ws.st_host->abort == 2) {  // step abort_j needs its second DGKS sweep
+            const int ja = ws.st_host->abort_j;
+            g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
+            ws.st_host->abort = 0;
+            write_state();
+            dgks2_tail(ja, ja == rstart_j ? 1 : 0);
+            j = ja + 1;
+            continue;
+        }
         if (ws.st_host->abort) {  // free-running cycle hit rnorm == 0 at step abort_j
             const int ja = ws.st_host->abort_j;
             g_stats.nopx -= (k + npk) - ja + 1;  // those OP*x were never applied
