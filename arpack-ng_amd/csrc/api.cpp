@@ -147,6 +147,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             return;
         }
         if (*tol <= 0.0) *tol = Prec<R>::eps;
+        g_sym.erase(v);  // a previous solve on the same V is abandoned: finish it first
         auto up = std::make_unique<SolverT<R>>();
         S = up.get();
         S->bmat = bmat[0];
@@ -257,7 +258,9 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
             continue;
         }
-        if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park (no sync)
+        if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park
+            // the caller may free or reuse its arrays before resuming: drain
+            S->a.sync();
             *ido = r.ido;
             return;
         }

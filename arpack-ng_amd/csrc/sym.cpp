@@ -118,6 +118,8 @@ void ArraysT<R>::sync() { ck(hipStreamSynchronize(stream)); }
 
 template <class R>
 SolverT<R>::~SolverT() {
+    // no kernel of this solve may still be writing the caller's arrays
+    if (a.stream) (void)hipStreamSynchronize(a.stream);
     root.reset();
     dev::ws_destroy(ws);
     a.release();

@@ -24,6 +24,8 @@ using cd = std::complex<double>;
 
 template <class R>
 ZSolverT<R>::~ZSolverT() {
+    // no kernel of this solve may still be writing the caller's arrays
+    if (a.stream) (void)hipStreamSynchronize(a.stream);
     root.reset();
     zdev::ws_destroy(ws);
     a.release();
@@ -397,6 +399,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             return;
         }
         if (*tol <= 0.0) *tol = Prec<R>::eps;
+        g_z.erase(v);  // a previous solve on the same V is abandoned: finish it first
         auto up = std::make_unique<ZSolverT<R>>();
         S = up.get();
         S->bmat = bmat[0];

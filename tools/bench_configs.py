@@ -1,0 +1,88 @@
+"""Restart-cycle throughput of the engine on BASELINE.json's other configs
+(bench.py measures the north star; these are the parity configs at full size).
+
+    python tools/bench_configs.py > profiles/r01_configs.json
+
+C2  dsaupd, 2-D 5-pt Laplacian m = 1000 (n = 1e6), LA, nev 10, ncv 30
+C3  dnaupd, 2-D convection-diffusion m = 1000 (rho = 10), LM, nev 10, ncv 40
+C4  dsaupd, 3-D 7-pt Laplacian m = 215 (n = 9.94e6; the 1-GPU share of the
+    8-GPU config is n/8 -- here the whole operator on one GPU), LA, nev 10, ncv 30
+C5  znaupd, complex random CSR n = 5e5, 100 nnz/row, diag += 100, LM (mode 1:
+    the config's shift-invert needs a caller-side solve that is not part of
+    this library; the Arnoldi engine is the same)
+
+Each real config: W warmup cycles, then K timed cycles (the engine parks at
+cycle boundaries), device-synchronised; symmetric configs also with the
+symmetric-storage SpMV.  C5: a capped solve (mxiter cycles) timed whole.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import load_pkg  # noqa: E402
+
+W, K = 2, 10
+
+
+def timed(pkg, s, A, ns=False):
+    for k in (0, W):
+        ido = s.aupd_cycles(A, k)
+        if ido != 98:
+            raise RuntimeError("solve ended early: ido %d info %d" % (ido, int(s.info[0])))
+    pkg.synchronize()
+    it0 = pkg.stats()["nopx"]
+    t = time.perf_counter()
+    ido = s.aupd_cycles(A, K)
+    pkg.synchronize()
+    el = time.perf_counter() - t
+    nc = K if ido == 98 else int(s.iparam[2]) - W
+    return dict(iters_per_s=nc / el, ms_per_cycle=1e3 * el / nc, cycles=nc,
+                lanczos_steps_per_s=(pkg.stats()["nopx"] - it0) / el)
+
+
+def main():
+    pkg = load_pkg()
+    out = {}
+    mx = W + K + 5
+    for name, make, which, ncv, ns in (
+            ("C2_dsaupd_lap2d_1e6", lambda: pkg.CSR.laplace2d(1000), "LA", 30, False),
+            ("C3_dnaupd_convdiff_1e6", lambda: pkg.CSR.convdiff2d(1000, 10.0), "LM", 40, True),
+            ("C4_dsaupd_lap3d_9.94e6", lambda: pkg.CSR.laplace3d(215), "LA", 30, False)):
+        A = make()
+        n = A.n
+        rec = dict(n=n, nnz=A.nnz, which=which, nev=10, ncv=ncv)
+        cls = pkg.NsRci if ns else pkg.SymRci
+        rec["full_storage"] = timed(pkg, cls(n, 10, ncv, which, 0.0, mxiter=mx, device=True), A, ns)
+        if not ns:
+            try:
+                A.set_symmetric(True)
+                rec["sym_storage"] = timed(pkg, cls(n, 10, ncv, which, 0.0, mxiter=mx, device=True), A)
+            except RuntimeError as e:  # band wider than the LDS windows (3-D natural order)
+                rec["sym_storage"] = "not applicable: %s" % e
+        out[name] = rec
+        print(json.dumps({name: rec}), file=sys.stderr, flush=True)
+        del A
+    # C5 proxy: mode-1 znaupd on the config's operator, capped solve timed whole
+    n = 500_000
+    Z = pkg.ZCSR.random(n, 100, 5, 100.0)
+    cap = 8
+    s = pkg.ZRci(n, 10, 40, "LM", 0.0, mxiter=cap)
+    pkg.synchronize()
+    t = time.perf_counter()
+    s.aupd_zcsr(Z)
+    pkg.synchronize()
+    el = time.perf_counter() - t
+    out["C5_znaupd_zrandom_5e5_mode1"] = dict(
+        n=n, per_row=100, which="LM", nev=10, ncv=40, cycles=int(s.iparam[2]), info=int(s.info[0]),
+        seconds=el, iters_per_s_incl_setup=int(s.iparam[2]) / el,
+        note="mode 1 (OP = A); the config's shift-invert solve is the caller's")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
