@@ -125,7 +125,6 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     __shared__ double xw[kSymWin];
     __shared__ double yw[kSymWin];
     constexpr int NW = kSymThreads / 64;
-    constexpr int PT = kSymWin / kSymThreads;  // window elements per thread
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
     const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
@@ -165,25 +164,14 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         const int64_t s1 = sb_slice0[b + 1];
         int carry = 0;
         if (b > b0) {  // the previous window's tail [R_prev, span_prev) becomes this head
+            // (span <= 2R inside chains, so source and destination do not overlap)
             carry = span_prev - R_prev;
-            double xs[PT], ys[PT];
-#pragma unroll
-            for (int q = 0; q < PT; ++q) {
-                const int i = t + q * kSymThreads;
-                if (i < carry) {
-                    xs[q] = xw[R_prev + i];
-                    ys[q] = yw[R_prev + i];
-                }
+            __syncthreads();  // every wave has read its epilogue values
+            for (int i = t; i < carry; i += kSymThreads) {
+                xw[i] = xw[R_prev + i];
+                yw[i] = yw[R_prev + i];
             }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < PT; ++q) {
-                const int i = t + q * kSymThreads;
-                if (i < carry) {
-                    xw[i] = xs[q];
-                    yw[i] = ys[q];
-                }
-            }
+            __syncthreads();  // the staging below overwrites the shift's source range
         }
         for (int i = carry + t; i < span; i += kSymThreads) {
             xw[i] = x[coff + r0 + i];
@@ -455,8 +443,11 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_lo = d_lo;
     A.ss_hi = d_hi;
     A.ss_nsb = nsb;
-    // chains of consecutive superblocks, one workgroup per CU (k_csr_ssell)
-    A.ss_chain = (nsb >= ncu && nsb % ncu == 0) ? (int)(nsb / ncu) : 1;
+    // chains of consecutive superblocks, one workgroup per CU (k_csr_ssell);
+    // the in-LDS window shift needs span <= 2R (true for the balanced plan)
+    bool shift_ok = true;
+    for (int64_t b = 0; b < nsb; ++b) shift_ok = shift_ok && spans[b] <= 2 * (r0s[b + 1] - r0s[b]);
+    A.ss_chain = (shift_ok && nsb >= ncu && nsb % ncu == 0) ? (int)(nsb / ncu) : 1;
     A.ss_nnz = nnz_u;
     A.ss_padded = padded;
     A.ss_ncomb = ncomb;
