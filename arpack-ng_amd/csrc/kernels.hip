@@ -250,27 +250,33 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    double* __restrict__ hcol, int hld) {
     if (gate_closed(st, gate)) return;
     __shared__ double s_sum[256];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int k = wave; k < m; k += 16) {
-        double s = 0.0;
-        if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
-            s = lane == 0 ? sums[k] : 0.0;
-        } else {
-            // four independent chains so the strided loads overlap
-            const double* p = part + (int64_t)k * nblk;
-            double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-            int b = lane;
-            for (; b + 192 < nblk; b += 256) {
-                s += p[b];
-                s1 += p[b + 64];
-                s2 += p[b + 128];
-                s3 += p[b + 192];
+    if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
+        if (threadIdx.x < m) s_sum[threadIdx.x] = sums[threadIdx.x];
+    } else {
+        // 32 slots per round, 32 threads (half a wave) per slot: thread `sub`
+        // sums blocks sub, sub+32, ... in four independent chains (coalesced
+        // 256-B rows of the k-major partials), then the half wave reduces
+        const int sub = threadIdx.x & 31;
+        for (int k0 = 0; k0 < m; k0 += 32) {
+            const int k = k0 + (threadIdx.x >> 5);
+            double s = 0.0;
+            if (k < m) {
+                const double* p = part + (int64_t)k * nblk;
+                double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+                int b = sub;
+                for (; b + 96 < nblk; b += 128) {
+                    s += p[b];
+                    s1 += p[b + 32];
+                    s2 += p[b + 64];
+                    s3 += p[b + 96];
+                }
+                for (; b < nblk; b += 32) s += p[b];
+                s = (s + s1) + (s2 + s3);
             }
-            for (; b < nblk; b += 64) s += p[b];
-            s = (s + s1) + (s2 + s3);
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 32);
+            if (sub == 0 && k < m) s_sum[k] = s;
         }
-        s = wave_sum(s);
-        if (lane == 0) s_sum[k] = s;
     }
     __syncthreads();
     const int t = threadIdx.x;
