@@ -10,8 +10,9 @@
 //
 // Layout: SYMMETRIC SUPERBLOCKS.  Superblock b owns rows [r0, r1); the upper
 // entries of those rows touch columns [r0, r0 + span) with span <= kSymWin (10240).
-// One 1024-thread workgroup per superblock stages x[r0, r0+span) in LDS,
-// zeroes an LDS y window of the same range, and streams the superblock's
+// A 1024-thread workgroup (one per CU; it walks a chain of consecutive
+// superblocks, see k_csr_ssell) stages x[r0, r0+span) in LDS, zeroes an LDS y
+// window of the same range, and streams the superblock's
 // upper entries as SELL-64 slices (rows sorted by upper length, one row per
 // lane, column-step-major: one 512-B val load + one 128-B 16-bit column load
 // per wave and step).  Each entry feeds the row sum (x gathered from LDS) and,
@@ -22,9 +23,10 @@
 //   [pre, R)     complete rows: stored to y
 //   [R, span)    this superblock's spill into the next one: slot_lo
 // The analysis guarantees every spill lies inside the NEXT superblock's rows,
-// so each combined row has exactly two partial sums; a second small kernel
-// stores y = lo + hi (a two-term sum is commutative, so the combine adds no
-// order dependence of its own).
+// so each combined row has exactly two partial sums; inside a chain the spill
+// simply stays in LDS, and at chain heads a second small kernel stores
+// y = lo + hi (a two-term sum is commutative, so the combine adds no order
+// dependence of its own).
 //
 // Rounding: the transposed contributions arrive in LDS in wave-schedule order,
 // so y is not bitwise reproducible run to run (|dy| ~ 1 ulp of the row's
