@@ -86,7 +86,7 @@ def timing() -> Timing:
 
 def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
                  mode=1, bmat="I", bop=None, rvec=True, sigma=0.0, ishift=1,
-                 shifts=None, return_state=False, prec="d"):
+                 shifts=None, return_state=False, prec="d", howmny="A"):
     """Run dsaupd_/dseupd_ to completion. Returns dict with d, z, iparam, info...
 
     `op(x, ido, bx)` computes OP*x (bx = B*x slice for modes 3-5, else None);
@@ -150,7 +150,7 @@ def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
     z = np.asfortranarray(np.zeros((n, nev), dt))
     select = np.zeros(ncv, np.int32)
     ierr = np.zeros(1, np.int32)
-    getattr(L, prec + "seupd_")(_ci(1 if rvec else 0), C.c_char_p(b"A"), _pi(select), _pd(d),
+    getattr(L, prec + "seupd_")(_ci(1 if rvec else 0), C.c_char_p(howmny.encode()), _pi(select), _pd(d),
               _pd(z), _ci(n), C.byref(ct(sigma)), C.c_char_p(bm), _ci(n), C.c_char_p(wh), _ci(nev),
               C.byref(tolc), _pd(resid), _ci(ncv), _pd(v), _ci(ldv), _pi(iparam), _pi(ipntr),
               _pd(workd), _pd(workl), _ci(lworkl), _pi(ierr),
