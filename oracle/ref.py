@@ -162,7 +162,7 @@ def dsaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300,
 
 def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode=1,
                  bmat="I", bop=None, rvec=True, sigmar=0.0, sigmai=0.0, return_state=False,
-                 prec="d"):
+                 prec="d", ishift=1, shifts=None):
     """Run dnaupd_/dneupd_ (SRC/dnaupd.f:406, SRC/dneupd.f) to completion
     (prec="s": snaupd_/sneupd_ on float32 arrays)."""
     L = lib()
@@ -176,7 +176,7 @@ def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
     v = np.asfortranarray(np.zeros((ldv, ncv), dt))
     iparam = np.zeros(11, np.int32)
     ipntr = np.zeros(14, np.int32)
-    iparam[0] = 1
+    iparam[0] = ishift
     iparam[2] = mxiter
     iparam[6] = mode
     workd = np.zeros(3 * n, dt)
@@ -197,6 +197,12 @@ def dnaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
         elif k == 2:
             x = workd[ipntr[0] - 1: ipntr[0] - 1 + n]
             workd[ipntr[1] - 1: ipntr[1] - 1 + n] = bop(x.copy())
+        elif k == 3:  # user shifts: real parts at ipntr(14), imaginary parts np later
+            np_ = int(iparam[7])
+            re, im = shifts(np_)
+            o = int(ipntr[13]) - 1
+            workl[o:o + np_] = re
+            workl[o + np_:o + 2 * np_] = im
         else:
             break
     out = dict(info=int(info[0]), iparam=iparam.copy(), ipntr=ipntr.copy(), tol=tolc.value)
@@ -264,6 +270,12 @@ def znaupd_solve(op, n, nev, ncv, which="LM", tol=0.0, v0=None, mxiter=300, mode
         elif k == 2:
             x = workd[ipntr[0] - 1: ipntr[0] - 1 + n]
             workd[ipntr[1] - 1: ipntr[1] - 1 + n] = bop(x.copy())
+        elif k == 3:  # user shifts: real parts at ipntr(14), imaginary parts np later
+            np_ = int(iparam[7])
+            re, im = shifts(np_)
+            o = int(ipntr[13]) - 1
+            workl[o:o + np_] = re
+            workl[o + np_:o + 2 * np_] = im
         else:
             break
     out = dict(info=int(info[0]), iparam=iparam.copy(), ipntr=ipntr.copy(), tol=tolc.value)
