@@ -662,6 +662,9 @@ void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc,
 #define AHIP_CASES_1_32(M) \
     M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16) \
     M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
+#define AHIP_CASES_33_64(M) \
+    M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41) M(42) M(43) M(44) M(45) M(46) M(47) M(48) \
+    M(49) M(50) M(51) M(52) M(53) M(54) M(55) M(56) M(57) M(58) M(59) M(60) M(61) M(62) M(63) M(64)
 
 template <class R, int WM, bool REV = false>
 static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R* V, int64_t ld,
@@ -712,7 +715,10 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
                  gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 2));
     const dim3 g(ws.nblk), b(kBlock);
     const bool rev = dir_rev(j, which, false);
-    if (j >= 1 && j <= 32) {
+    // fused up to j = 64 (ncv <= 64: dnaupd's C3 runs ncv = 40); the V row of a
+    // fused pass lives in registers, so a wider J trades occupancy for
+    // in-flight loads per wave (64 column loads per row at J = 64)
+    if (j >= 1 && j <= 64) {
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
     case J:                                                                                        \
@@ -727,6 +733,7 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
                                rin, rout, ws.part, ws.stride, ws.st, gate);                        \
         break;
             AHIP_CASES_1_32(AHIP_UPD_CASE)
+            AHIP_CASES_33_64(AHIP_UPD_CASE)
 #undef AHIP_UPD_CASE
             default: break;
         }

@@ -62,3 +62,65 @@ def test_north_star_full_size(pkg, reference, storage):
         zk = zb.numpy(k * N, N)
         r = np.linalg.norm(y.numpy() - dv[k] * zk)
         assert r <= 10 * TOL * abs(dv[k]), (k, r, dv[k])
+
+
+def _ref_capped(case, cap):
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "ref.npz")
+        threads = min(16, len(os.sched_getaffinity(0)))
+        r = subprocess.run([sys.executable, "-m", "oracle.fullsize_ref", "--case", case, "--mxiter",
+                            str(cap), "--threads", str(threads), "--out", out], cwd=ROOT,
+                           capture_output=True, text=True, timeout=400)
+        assert r.returncode == 0, r.stderr[-2000:]
+        print(r.stdout.strip())
+        return dict(np.load(out, allow_pickle=False))
+
+
+def _close(got, want, rtol):
+    got, want = np.sort_complex(got), np.sort_complex(want)
+    err = np.abs(got - want) / np.maximum(1.0, np.abs(want))
+    print("max rel diff %.3e" % err.max())
+    return err.max() <= rtol
+
+
+@pytest.mark.timeout(600)
+def test_c3_dnaupd_convdiff_full_size(pkg):
+    """BASELINE config 3 at full size (n = 1e6, ncv 40, LM), capped at 8 restart
+    cycles: same cycles, OP*x, nconv; the ncv Ritz values held in workl and the
+    converged ones from dneupd agree with the reference."""
+    cap = 8
+    ref = _ref_capped("c3", cap)
+    A = pkg.CSR.convdiff2d(1000, 10.0)
+    n = A.n
+    s = pkg.NsRci(n, 10, 40, "LM", 1e-6, mxiter=cap, v0=dlarnv_fast(n), device=True)
+    s.aupd_csr(A)
+    assert int(s.info[0]) == int(ref["info"])
+    for k in (2, 4, 8):
+        assert int(s.iparam[k]) == int(ref["iparam"][k]), k
+    o5, o6 = int(s.ipntr[5]) - 1, int(s.ipntr[6]) - 1
+    assert _close(s.workl[o5:o5 + 40] + 1j * s.workl[o6:o6 + 40], ref["ritz"], 1e-10)
+    if int(s.iparam[4]):
+        dr, di, _, nconv = s.eupd(rvec=False)
+        assert _close(dr[:nconv] + 1j * di[:nconv], ref["d"], 1e-10)
+
+
+@pytest.mark.timeout(600)
+def test_c5_znaupd_zrandom_full_size(pkg):
+    """BASELINE config 5's operator at full size (complex random CSR n = 5e5,
+    100 nnz/row, diag += 100), znaupd LM mode 1 (the config's shift-invert
+    solve is the caller's), capped at 5 restart cycles."""
+    cap = 5
+    ref = _ref_capped("c5", cap)
+    Z = pkg.ZCSR.random(500_000, 100, 5, 100.0)
+    n = Z.n
+    s = pkg.ZRci(n, 10, 40, "LM", 1e-6, mxiter=cap, v0=dlarnv_fast(2 * n).view(np.complex128))
+    s.aupd_zcsr(Z)
+    assert int(s.info[0]) == int(ref["info"])
+    for k in (2, 4, 8):
+        assert int(s.iparam[k]) == int(ref["iparam"][k]), k
+    o5 = int(s.ipntr[5]) - 1
+    assert _close(s.workl[o5:o5 + 40], ref["ritz"], 1e-10)
+    if int(s.iparam[4]):
+        d, _, nconv = s.eupd(rvec=False)
+        assert _close(d[:nconv], ref["d"], 1e-10)

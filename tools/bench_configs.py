@@ -2,6 +2,7 @@
 (bench.py measures the north star; these are the parity configs at full size).
 
     python tools/bench_configs.py > profiles/r01_configs.json
+    python tools/bench_configs.py C3      (only the configs whose name has C3)
 
 C2  dsaupd, 2-D 5-pt Laplacian m = 1000 (n = 1e6), LA, nev 10, ncv 30
 C3  dnaupd, 2-D convection-diffusion m = 1000 (rho = 10), LM, nev 10, ncv 40
@@ -49,10 +50,13 @@ def main():
     pkg = load_pkg()
     out = {}
     mx = W + K + 5
+    only = sys.argv[1:]
     for name, make, which, ncv, ns in (
             ("C2_dsaupd_lap2d_1e6", lambda: pkg.CSR.laplace2d(1000), "LA", 30, False),
             ("C3_dnaupd_convdiff_1e6", lambda: pkg.CSR.convdiff2d(1000, 10.0), "LM", 40, True),
             ("C4_dsaupd_lap3d_9.94e6", lambda: pkg.CSR.laplace3d(215), "LA", 30, False)):
+        if only and not any(o in name for o in only):
+            continue
         A = make()
         n = A.n
         rec = dict(n=n, nnz=A.nnz, which=which, nev=10, ncv=ncv)
@@ -67,6 +71,9 @@ def main():
         out[name] = rec
         print(json.dumps({name: rec}), file=sys.stderr, flush=True)
         del A
+    if only and "C5" not in only:
+        print(json.dumps(out), flush=True)
+        return
     # C5 proxy: mode-1 znaupd on the config's operator, capped solve timed whole
     n = 500_000
     Z = pkg.ZCSR.random(n, 100, 5, 100.0)
