@@ -169,3 +169,20 @@ def test_symsell_plan_row_distribution(pkg, P):
         carry = yl[m:]
         assert spans[-1] - (r0s[-1] - r0s[-2]) <= sout
     assert np.all(np.abs(y - yref) <= 1e-13 * scale)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_symsell_plan_bench_sizes(pkg, P):
+    """The bench's row blocks (n = 1e7 over P ranks, band 4096): every rank gets a
+    plan whose superblock count is a multiple of 256 (one chain per CU, the
+    chained k_csr_ssell), with the neighbours' spills at both ends."""
+    n, B = 10_000_000, 4096
+    for q in range(P):
+        a, b = q * n // P, (q + 1) * n // P
+        cmax = np.minimum(np.arange(a, b) + B - 1, n - 1) - a
+        sin = B - 1 if q > 0 else 0
+        sout = B - 1 if q < P - 1 else 0
+        rc, r0s, spans, pre = _plan(pkg, cmax, 10240, sin, sout)
+        assert rc == 0 and r0s[-1] == b - a
+        assert len(spans) % 256 == 0
+        assert pre[0] == sin and spans[-1] - (r0s[-1] - r0s[-2]) <= sout
