@@ -374,6 +374,13 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t l
                                                       double sigmak, double betak,
                                                       R* __restrict__ r,
                                                       double* __restrict__ part, int pstride) {
+    // Q(:, 0:kev] staged in LDS once per block: the per-row sums then read it
+    // with broadcast LDS loads instead of waiting on ~330 scalar-cache loads
+    // per row batch (the scalar-load waits held this kernel at 4.45 TB/s)
+    __shared__ double sq[MAXK * (MAXK + 1)];
+    for (int e = threadIdx.x; e < kplusp * (kev + 1); e += kBlock)
+        sq[e] = Q[e % kplusp + (int64_t)(e / kplusp) * ldq];
+    __syncthreads();
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const bool next = betak > 0.0;
@@ -383,15 +390,17 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t l
         for (int k = 0; k < MAXK; ++k) v[k] = (k < kplusp) ? (double)vld(V + i + (int64_t)k * ld) : 0.0;
         double vnext = 0.0;
         if (next) {
+            const double* q = sq + kev * kplusp;
 #pragma unroll
             for (int k = 0; k < MAXK; ++k)
-                if (k < kplusp) vnext += v[k] * Q[k + (int64_t)kev * ldq];
+                if (k < kplusp) vnext += v[k] * q[k];
         }
         for (int l = 0; l < kev; ++l) {
+            const double* q = sq + l * kplusp;
             double o = 0.0;
 #pragma unroll
             for (int k = 0; k < MAXK; ++k)
-                if (k < kplusp) o += v[k] * Q[k + (int64_t)l * ldq];
+                if (k < kplusp) o += v[k] * q[k];
             V[i + (int64_t)l * ld] = (R)o;
         }
         double ri = sigmak * (double)r[i];
