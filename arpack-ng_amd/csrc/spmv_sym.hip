@@ -232,8 +232,9 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     }
 }
 
-// y(head rows of each chain's first superblock) = lo + hi
-__global__ __launch_bounds__(256) void k_ssell_combine(const int64_t* __restrict__ sb_r0,
+// y(head rows of each chain's first superblock) = lo + hi (1024 threads: a
+// head is ~4k rows, so every load of the block is in flight at once)
+__global__ __launch_bounds__(1024) void k_ssell_combine(const int64_t* __restrict__ sb_r0,
                                                        const int32_t* __restrict__ sb_pre,
                                                        const int64_t* __restrict__ sb_off,
                                                        const double* __restrict__ lo,
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void k_ssell_combine(const int64_t* __restrict
     const int64_t b = (int64_t)blockIdx.x * chain;
     const int pre = sb_pre[b];
     const int64_t off = sb_off[b], r0 = sb_r0[b];
-    for (int i = threadIdx.x; i < pre; i += 256) y[r0 + i] = lo[off + i] + hi[off + i];
+    for (int i = threadIdx.x; i < pre; i += 1024) y[r0 + i] = lo[off + i] + hi[off + i];
 }
 
 }  // namespace
@@ -489,7 +490,7 @@ void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
     if (A.ss_ncomb > 0)
-        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)nch), dim3(256), 0, s, A.ss_sb_r0,
+        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
                            A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
 }
 
