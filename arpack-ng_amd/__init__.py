@@ -331,8 +331,12 @@ class CSR:
     def set_symmetric(self, on: bool = True):
         """Declare the matrix symmetric: the SpMV streams only the upper
         triangle (arpack_hip_csr_set_symmetric; entries below the diagonal are
-        ignored).  Raises if the band structure does not fit the LDS windows."""
+        ignored).  Raises if the band structure does not fit the LDS windows.
+        On one rank's block of a DistOp the call is collective: every rank
+        must make it, and all raise (full storage kept) if any rank's plan
+        fails -- rc = -2 on the ranks whose own plan succeeded."""
         rc = lib().arpack_hip_csr_set_symmetric(self.h, 1 if on else 0)
+        self.last_rc = rc
         if rc != 0:
             raise RuntimeError("symmetric storage not applicable to this matrix (rc=%d)" % rc)
         self.symmetric = bool(on)

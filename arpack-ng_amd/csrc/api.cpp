@@ -71,7 +71,7 @@ static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lw
     int ierr = 0;
     if (n <= 0) ierr = -1;
     else if (nev <= 0) ierr = -2;
-    else if (ncv <= nev || ncv > n) ierr = -3;
+    else if (ncv <= nev || ncv > n || ncv > dev::kMaxNcv) ierr = -3;
     if (mxiter <= 0) ierr = -4;
     if (which != la::Which::LM && which != la::Which::SM && which != la::Which::LA &&
         which != la::Which::SA && which != la::Which::BE)
@@ -91,7 +91,7 @@ static int ns_check(char bmat, int n, la::Which which, int nev, int ncv, int lwo
     int ierr = 0;
     if (n <= 0) ierr = -1;
     else if (nev <= 0) ierr = -2;
-    else if (ncv <= nev + 1 || ncv > n) ierr = -3;
+    else if (ncv <= nev + 1 || ncv > n || ncv > dev::kMaxNcv) ierr = -3;
     else if (mxiter <= 0) ierr = -4;
     else if (which != la::Which::LM && which != la::Which::SM && which != la::Which::LR &&
              which != la::Which::SR && which != la::Which::LI && which != la::Which::SI)

@@ -281,18 +281,29 @@ int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
     return hipStreamSynchronize(nullptr) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+static void csr_full_storage(arpack_hip_csr* A) {
+    if (A->A.kernel == ahip::dev::kCsrSymSell)
+        A->A.kernel = A->sell ? ahip::dev::kCsrSell
+                              : (A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector);
+}
+
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     if (!on) {
-        if (A->A.kernel == ahip::dev::kCsrSymSell)
-            A->A.kernel = A->sell ? ahip::dev::kCsrSell
-                                  : (A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector);
+        csr_full_storage(A);
         return 0;
     }
-    if (!A->symsell) {
-        const int rc = ahip::dev::csr_build_symsell(A->A, A->ncols, A->sym_coff, A->sym_spill_in,
-                                                    A->sym_spill_out, &A->symsell);
-        if (rc != 0) return rc;
+    int rc = 0;
+    if (!A->symsell)
+        rc = ahip::dev::csr_build_symsell(A->A, A->ncols, A->sym_coff, A->sym_spill_in,
+                                          A->sym_spill_out, &A->symsell);
+    // one rank's block of a distributed operator: the symmetric SpMV changes the
+    // exchange pattern (hi-only halo + forward spill), so the switch is collective
+    // and every rank falls back to full storage if any rank's plan failed
+    if (A->dist_comm && !ahip::dist_all_ok(A->dist_comm, rc == 0)) {
+        csr_full_storage(A);
+        return rc != 0 ? rc : -2;
     }
+    if (rc != 0) return rc;
     A->A.kernel = ahip::dev::kCsrSymSell;
     return 0;
 }

@@ -4,6 +4,10 @@
 
 #include "device.hpp"
 
+namespace ahip {
+struct Comm;
+}
+
 struct arpack_hip_csr {
     ahip::dev::Csr A;
     int64_t* rowptr = nullptr;
@@ -19,7 +23,15 @@ struct arpack_hip_csr {
     // x = [sym_coff | local rows | sym_spill_out], sym_spill_in leading rows
     // receive the previous rank's transposed terms
     int64_t sym_coff = 0, sym_spill_in = 0, sym_spill_out = 0;
+    // set by arpack_hip_dist_create: the CSR is one rank's block of a row-
+    // distributed operator, so a storage-mode switch must be agreed by all ranks
+    const ahip::Comm* dist_comm = nullptr;
 };
+
+namespace ahip {
+// collective over the ranks of c: 1 if every rank passes ok_local != 0
+int dist_all_ok(const Comm* c, int ok_local);
+}
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV
 // analysis for an x vector of length ncols; 0 on success

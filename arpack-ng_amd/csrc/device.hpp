@@ -18,6 +18,9 @@
 namespace ahip::dev {
 
 constexpr int kBlock = 256;
+// largest ncv the engine accepts (the finalize stages ncv + 2 sums in 64 KB of
+// dynamic LDS); a larger ncv is rejected with info = -3 like ncv > n
+constexpr int kMaxNcv = 8000;
 constexpr int kMaxRedBlocks = 1024;  // partial-sum grid (A/B: 1024 vs 2048 +1.5% cycle rate with the fused finalize)
 
 // XCD-contiguous block order: the hardware deals workgroups round-robin over
@@ -72,6 +75,9 @@ struct Workspace {
     // recorded by the finalize kernel; hld = ncv (0 for the Lanczos path).
     double* hcol = nullptr;   // hld * ncv
     int hld = 0;
+    // ncv > 64 only: nblk * kBlock * (ncv + 1) doubles of per-thread output
+    // columns for the generic (alias-safe) V*Q and gemm kernels
+    double* scratch = nullptr;
     LzState* st = nullptr;
     LzState* st_host = nullptr;  // pinned mirror
     double* host_scratch = nullptr;  // pinned, >= 4*stride doubles

@@ -29,6 +29,17 @@ void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
     }
     dev::csr_spmv(s, A, D.x_ext, y);
 }
+
+int dist_all_ok(const Comm* c, int ok_local) {
+    if (!c || comm_size(c) == 1) return ok_local != 0;
+    double h = ok_local ? 0.0 : 1.0, *d = nullptr;  // SUM of failures
+    if (hipMalloc(&d, sizeof(double))) return 0;  // (cannot happen on a sane device)
+    (void)hipMemcpy(d, &h, sizeof(double), hipMemcpyHostToDevice);
+    comm_allreduce_sum(c, d, 1, nullptr);
+    (void)hipMemcpy(&h, d, sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return h == 0.0;
+}
 }  // namespace ahip
 
 struct arpack_hip_dist {
@@ -70,7 +81,7 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     const int P = comm_size(c), r = comm_rank(c);
     const int64_t nloc = A->A.n;
     int64_t cmin = 0, cmax = -1;
-    if (ahip_csr_col_span(A, &cmin, &cmax) != 0) return -1;
+    if (!dist_all_ok(c, ahip_csr_col_span(A, &cmin, &cmax) == 0)) return -1;
     if (cmax < 0) cmin = cmax = row0;  // empty operator block
     // share [row0, nloc, cmin, cmax] of every rank (allreduce of a one-hot table)
     std::vector<double> tab(4 * (size_t)P, 0.0);
@@ -98,22 +109,28 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     o.send_hi = plan[3];
     o.comm = c;
     const int64_t next = o.halo_lo + nloc + o.halo_hi;
-    if (hipMalloc(&o.x_ext, sizeof(double) * (next > 0 ? next : 1))) {
-        delete D;
-        return -1;
-    }
-    (void)hipMemset(o.x_ext, 0, sizeof(double) * (next > 0 ? next : 1));
-    // local column indices relative to x_ext
+    // local column indices relative to x_ext; a failure on any rank fails the
+    // call on every rank (the later collectives would otherwise mismatch)
     const bool was_sym = A->A.kernel == ahip::dev::kCsrSymSell;
-    A->sym_coff = o.halo_lo;
-    A->sym_spill_in = o.send_lo;
-    A->sym_spill_out = o.halo_hi;
-    if (ahip_csr_remap_cols(A, row0 - o.halo_lo, next) != 0) {
-        (void)hipFree(o.x_ext);
+    int ok = hipMalloc(&o.x_ext, sizeof(double) * (next > 0 ? next : 1)) == hipSuccess;
+    if (ok) {
+        (void)hipMemset(o.x_ext, 0, sizeof(double) * (next > 0 ? next : 1));
+        A->sym_coff = o.halo_lo;
+        A->sym_spill_in = o.send_lo;
+        A->sym_spill_out = o.halo_hi;
+        ok = ahip_csr_remap_cols(A, row0 - o.halo_lo, next) == 0;
+    }
+    if (!dist_all_ok(c, ok)) {
+        if (o.x_ext) (void)hipFree(o.x_ext);
         delete D;
         return -1;
     }
-    if (was_sym) (void)arpack_hip_csr_set_symmetric(A, 1);
+    // storage mode agreed by all ranks: symmetric only if every rank declared it
+    // and every rank's plan succeeds (arpack_hip_csr_set_symmetric is collective
+    // from here on); otherwise every rank runs the full-storage SpMV (the remap
+    // above already reset the kernel)
+    A->dist_comm = c;
+    if (dist_all_ok(c, was_sym)) (void)arpack_hip_csr_set_symmetric(A, 1);
     o.A = &A->A;
     *out = D;
     return 0;

@@ -234,7 +234,8 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
             (void)hipMemcpy2DAsync(zd, sizeof(R) * ldz, a.d_v, sizeof(R) * a.d_ld,
                                    sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
         } else {
-            (void)hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream);
+            if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess)
+                return -9999;
             (void)hipMemcpyAsync(zd, a.d_v, sizeof(R) * (size_t)a.d_ld * nconv,
                                  hipMemcpyDeviceToDevice, a.stream);
         }

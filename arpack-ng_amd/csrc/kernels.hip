@@ -249,9 +249,12 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    LzState* __restrict__ st,
                                                    double* __restrict__ hcol, int hld) {
     if (gate_closed(st, gate)) return;
-    __shared__ double s_sum[256];
+    // the m = j+1 (<= ncv+2) sums are staged in dynamic LDS sized by the launch
+    // (finalize(): m doubles), so any ncv the argument checks accept fits
+    extern __shared__ double s_sum[];
+    const int nt = blockDim.x;
     if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
-        if (threadIdx.x < m) s_sum[threadIdx.x] = sums[threadIdx.x];
+        for (int k = threadIdx.x; k < m; k += nt) s_sum[k] = sums[k];
     } else {
         // 32 slots per round, 32 threads (half a wave) per slot: thread `sub`
         // sums blocks sub, sub+32, ... in four independent chains (coalesced
@@ -280,11 +283,13 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
     __syncthreads();
     const int t = threadIdx.x;
-    if (t < m) sums[t] = s_sum[t];
+    for (int k = t; k < m; k += nt) sums[k] = s_sum[k];
     const int jm = m - 1;  // index of the w'u / r'r slot
     if (phase == kFinCgs) {
-        if (t < jm) coef[t] = s_sum[t];
-        if (hld && t < jm) hcol[(int64_t)(j - 1) * hld + t] = s_sum[t];  // h(1:j,j) (dnaitr.f:566)
+        for (int k = t; k < jm; k += nt) {
+            coef[k] = s_sum[k];
+            if (hld) hcol[(int64_t)(j - 1) * hld + k] = s_sum[k];  // h(1:j,j) (dnaitr.f:566)
+        }
         if (t == 0) {
             st->zero = 0;
             st->dgks = 0;
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
     if (phase == kFinRaw) return;
     if (phase == kFinCoef) {
-        if (t < jm) coef[t] = s_sum[t];
+        for (int k = t; k < jm; k += nt) coef[k] = s_sum[k];
         return;
     }
     // refinement phases share the "speculative coefficients" layout
@@ -353,9 +358,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
     __syncthreads();
     const int take = s_take;
-    if (take && t < jm) {
-        coef[take * cstride + t] = s_sum[t];
-        if (hld) hcol[(int64_t)(j - 1) * hld + t] += s_sum[t];  // daxpy into h(1:j,j) (dnaitr.f:681)
+    if (take) {
+        for (int k = t; k < jm; k += nt) {
+            coef[take * cstride + k] = s_sum[k];
+            if (hld) hcol[(int64_t)(j - 1) * hld + k] += s_sum[k];  // daxpy into h(1:j,j) (dnaitr.f:681)
+        }
     }
 }
 
@@ -422,20 +429,23 @@ __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
     int64_t n, R* V, int64_t ld, int kplusp, int kev, const double* __restrict__ Q,
     int ldq, double sigmak, double betak, R* __restrict__ r, double* __restrict__ tmp,
     double* __restrict__ part, int pstride) {
-    // tmp: n x (kev+1) scratch (column-major, ld n) — used when kplusp > 64
+    // kplusp > 64: each thread keeps its row's kev+1 outputs in its own column
+    // of the preallocated scratch (tmp[l * S + tid], S = grid threads, coalesced)
+    // while V's row is read in column order; same summation order as k_vq_update
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool next = betak > 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        for (int l = 0; l <= kev; ++l) {
-            double o = 0.0;
-            for (int k = 0; k < kplusp; ++k) o += (double)V[i + (int64_t)k * ld] * Q[k + (int64_t)l * ldq];
-            tmp[i + (int64_t)l * n] = o;
+    for (int64_t i = tid; i < n; i += stride) {
+        for (int l = 0; l <= kev; ++l) tmp[l * stride + tid] = 0.0;
+        for (int k = 0; k < kplusp; ++k) {
+            const double vk = (double)V[i + (int64_t)k * ld];
+            for (int l = 0; l <= kev; ++l) tmp[l * stride + tid] += vk * Q[k + (int64_t)l * ldq];
         }
-        for (int l = 0; l < kev; ++l) V[i + (int64_t)l * ld] = (R)tmp[i + (int64_t)l * n];
+        for (int l = 0; l < kev; ++l) V[i + (int64_t)l * ld] = (R)tmp[l * stride + tid];
         double ri = sigmak * (double)r[i];
         if (next) {
-            const R vn = (R)tmp[i + (int64_t)kev * n];
+            const R vn = (R)tmp[kev * stride + tid];
             V[i + (int64_t)kev * ld] = vn;
             ri += betak * (double)vn;
         }
@@ -445,6 +455,25 @@ __global__ __launch_bounds__(kBlock) void k_vq_update_generic(
     }
     double acc[1] = {0.0};
     block_partials<1>(acc, 0, rr, true, part, 0, 0);
+}
+
+// Z = V(:,0:k) * M(k x nz) for k > 128, alias-safe through the per-thread
+// scratch columns (tmp[l * S + tid], S = grid threads)
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_vq_gemm_generic(int64_t n, const R* V, int64_t ld,
+                                                            int k, int nz,
+                                                            const double* __restrict__ M, R* Z,
+                                                            int64_t ldz, double* __restrict__ tmp) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (int64_t i = tid; i < n; i += stride) {
+        for (int l = 0; l < nz; ++l) tmp[l * stride + tid] = 0.0;
+        for (int t = 0; t < k; ++t) {
+            const double vt = (double)V[i + (int64_t)t * ld];
+            for (int l = 0; l < nz; ++l) tmp[l * stride + tid] += vt * M[t + (int64_t)l * k];
+        }
+        for (int l = 0; l < nz; ++l) Z[i + (int64_t)l * ldz] = (R)tmp[l * stride + tid];
+    }
 }
 
 // Z = V(:,0:k) * M(k x nz) ; row-local, so Z may alias V (rows held in registers)
@@ -595,7 +624,16 @@ int choose_nblk(int64_t n) {
     return (int)b;
 }
 
+static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s);
+
+// on failure everything allocated so far is released (ws left empty)
 hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
+    const hipError_t e = ws_alloc(ws, n, ncv, s);
+    if (e != hipSuccess) ws_destroy(ws);
+    return e;
+}
+
+static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     ws.stream = s;
     ws.nblk = choose_nblk(n);
     ws.stride = ncv + 2;
@@ -606,6 +644,9 @@ hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipMalloc(&ws.rec, sizeof(double) * 2 * (size_t)(ncv + 1)))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * (size_t)ncv * ncv))) return e;
     if ((e = hipMalloc(&ws.hcol, sizeof(double) * (size_t)ncv * ncv))) return e;
+    if (ncv > 64 &&  // per-thread output columns of the generic V*Q / gemm kernels
+        (e = hipMalloc(&ws.scratch, sizeof(double) * (size_t)ws.nblk * kBlock * (ncv + 1))))
+        return e;
     if ((e = hipMalloc(&ws.st, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
@@ -627,6 +668,7 @@ void ws_destroy(Workspace& ws) {
     if (ws.rec) (void)hipFree(ws.rec);
     if (ws.q) (void)hipFree(ws.q);
     if (ws.hcol) (void)hipFree(ws.hcol);
+    if (ws.scratch) (void)hipFree(ws.scratch);
     if (ws.st) (void)hipFree(ws.st);
     if (ws.st_host) (void)hipHostFree(ws.st_host);
     if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
@@ -760,8 +802,9 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
         const char* e = getenv("AHIP_FUSED_FIN");
         return !(e && e[0] == '0');
     }();
+    const size_t lds = sizeof(double) * (size_t)m;  // s_sum (m <= kMaxNcv + 2)
     if (!from_sums && fused) {  // one launch: the finalize block sums the partials itself
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, 0, m, (int)ph,
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, 0, m, (int)ph,
                            j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
         return;
     }
@@ -771,7 +814,7 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
                            ws.st, gate);
     }
     // stage 2b: the phase logic on the m sums (one small workgroup)
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ws.stream, ws.part, ws.nblk, 1, m, (int)ph, j,
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, 1, m, (int)ph, j,
                        rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
 }
 
@@ -796,13 +839,10 @@ void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int
     else if (kplusp <= 64)
         hipLaunchKernelGGL((k_vq_update<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
                            kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
-    else {
-        double* tmp = nullptr;
-        (void)hipMallocAsync(&tmp, sizeof(double) * (size_t)n * (kev + 1), ws.stream);
+    else  // ws.scratch: nblk * kBlock * (ncv + 1) doubles, allocated by ws_create for ncv > 64
         hipLaunchKernelGGL(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
-                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, tmp, ws.part, ws.stride);
-        (void)hipFreeAsync(tmp, ws.stream);
-    }
+                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.scratch, ws.part,
+                           ws.stride);
 }
 
 template <class R>
@@ -818,9 +858,12 @@ void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int 
     else if (k <= 64)
         hipLaunchKernelGGL((k_vq_gemm<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
-    else
+    else if (k <= 128)
         hipLaunchKernelGGL((k_vq_gemm<R, 128>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
+    else  // grid = nblk: the scratch holds nblk * kBlock rows of ncv + 1 outputs
+        hipLaunchKernelGGL(k_vq_gemm_generic<R>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, V, ld,
+                           k, nz, ws.q, Z, ldz, ws.scratch);
 }
 
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,

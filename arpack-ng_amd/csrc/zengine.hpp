@@ -24,6 +24,7 @@ struct Ws {
     double* coef = nullptr;  // complex coefficients (h) staged for the update
     double* q = nullptr;     // complex ncv x ncv (V*Q, eupd)
     double* host = nullptr;  // pinned
+    double* scratch = nullptr;  // ncv > 64: nblk * kB * ncv complex (k_zgemm_generic)
 };
 struct ZCsr {
     int64_t n = 0, nnz = 0;

@@ -109,14 +109,17 @@ __global__ __launch_bounds__(kB) void k_zupdate(int64_t n, int j,
                                                 const double2* __restrict__ h,
                                                 const typename C2<R>::T* rin,
                                                 typename C2<R>::T* rout) {
-    __shared__ double2 sh[256];
-    for (int c = threadIdx.x; c < j; c += kB) sh[c] = h[c];
+    // the first kSh coefficients are staged in LDS; beyond that (ncv > kSh) they
+    // are read from global memory (uniform across the block: cache hits)
+    constexpr int kSh = 256;
+    __shared__ double2 sh[kSh];
+    for (int c = threadIdx.x; c < j && c < kSh; c += kB) sh[c] = h[c];
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * kB;
     for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
         double2 r = d2(rin[i]);
         for (int c = 0; c < j; ++c) {
-            const double2 p = cmul(d2(V[i + (int64_t)c * ld]), sh[c]);
+            const double2 p = cmul(d2(V[i + (int64_t)c * ld]), c < kSh ? sh[c] : h[c]);
             r.x -= p.x;
             r.y -= p.y;
         }
@@ -144,6 +147,32 @@ __global__ __launch_bounds__(kB) void k_zgemm(int64_t n, const typename C2<R>::T
                 }
             Z[i + (int64_t)l * ldz] = st2<R>(o);
         }
+    }
+}
+
+// Z = V(:,0:k) * M for k > 64, alias-safe through per-thread scratch columns
+// (tmp[l * S + tid], S = grid threads); same summation order as k_zgemm
+template <class R>
+__global__ __launch_bounds__(kB) void k_zgemm_generic(int64_t n, const typename C2<R>::T* V,
+                                                      int64_t ld, int k, int nz,
+                                                      const double2* __restrict__ M,
+                                                      typename C2<R>::T* Z, int64_t ldz,
+                                                      double2* __restrict__ tmp) {
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    const int64_t tid = (int64_t)blockIdx.x * kB + threadIdx.x;
+    for (int64_t i = tid; i < n; i += stride) {
+        for (int l = 0; l < nz; ++l) tmp[l * stride + tid] = make_double2(0.0, 0.0);
+        for (int t = 0; t < k; ++t) {
+            const double2 vt = d2(V[i + (int64_t)t * ld]);
+            for (int l = 0; l < nz; ++l) {
+                const double2 p = cmul(vt, M[t + (int64_t)l * k]);
+                double2 o = tmp[l * stride + tid];
+                o.x += p.x;
+                o.y += p.y;
+                tmp[l * stride + tid] = o;
+            }
+        }
+        for (int l = 0; l < nz; ++l) Z[i + (int64_t)l * ldz] = st2<R>(tmp[l * stride + tid]);
     }
 }
 
@@ -342,9 +371,12 @@ void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
     else if (k <= 32)
         hipLaunchKernelGGL((k_zgemm<R, 32>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
                            Z2, ldz);
-    else
+    else if (k <= 64)
         hipLaunchKernelGGL((k_zgemm<R, 64>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
                            Z2, ldz);
+    else  // grid = nblk: ws.scratch holds nblk * kB rows of ncv outputs
+        hipLaunchKernelGGL((k_zgemm_generic<R>), dim3(ws.nblk), dim3(kB), 0, ws.stream, n, V2, ld, k,
+                           nz, M2, Z2, ldz, reinterpret_cast<double2*>(ws.scratch));
     (void)hipStreamSynchronize(ws.stream);
 }
 
@@ -383,7 +415,16 @@ AHIP_ZINST(double)
 AHIP_ZINST(float)
 #undef AHIP_ZINST
 
+static hipError_t ws_alloc(Ws& ws, int64_t n, int ncv, hipStream_t s);
+
+// on failure everything allocated so far is released (ws left empty)
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s) {
+    const hipError_t e = ws_alloc(ws, n, ncv, s);
+    if (e != hipSuccess) ws_destroy(ws);
+    return e;
+}
+
+static hipError_t ws_alloc(Ws& ws, int64_t n, int ncv, hipStream_t s) {
     ws.stream = s;
     int64_t g = (n + kB - 1) / kB;
     ws.nblk = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
@@ -394,6 +435,9 @@ hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipMalloc(&ws.coef, sizeof(double) * slots))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
     if ((e = hipHostMalloc(&ws.host, sizeof(double) * slots))) return e;
+    if (ncv > 64 &&  // per-thread output columns of k_zgemm_generic
+        (e = hipMalloc(&ws.scratch, sizeof(double) * 2 * (size_t)ws.nblk * kB * ncv)))
+        return e;
     return hipSuccess;
 }
 
@@ -403,6 +447,7 @@ void ws_destroy(Ws& ws) {
     if (ws.coef) (void)hipFree(ws.coef);
     if (ws.q) (void)hipFree(ws.q);
     if (ws.host) (void)hipHostFree(ws.host);
+    if (ws.scratch) (void)hipFree(ws.scratch);
     ws = Ws{};
 }
 

@@ -383,7 +383,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         int ierr = 0;  // SRC/znaupd.f:473-505
         if (n <= 0) ierr = -1;
         else if (nev <= 0) ierr = -2;
-        else if (ncv <= nev || ncv > n) ierr = -3;
+        else if (ncv <= nev || ncv > n || ncv > dev::kMaxNcv) ierr = -3;
         else if (mxiter <= 0) ierr = -4;
         else if (w != la::Which::LM && w != la::Which::SM && w != la::Which::LR &&
                  w != la::Which::SR && w != la::Which::LI && w != la::Which::SI)

@@ -140,19 +140,12 @@ def main():
     storage = "full"
     if args.storage == "sym":  # row blocks: upper-triangle SpMV + forward spill exchange
         try:
+            # collective on a distributed operator: every rank ends up in the
+            # same mode (all fall back to full storage if any rank's plan fails)
             A.set_symmetric(True)
-            ok = 1
-        except RuntimeError:
-            ok = 0
-        if dist:  # every rank must run the same SpMV mode (the exchanges differ)
-            import torch
-            t_ok = torch.tensor([ok], dtype=torch.int64)
-            dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
-            ok = int(t_ok.item())
-        if ok:
             storage = "sym"
-        else:
-            A.set_symmetric(False)
+        except RuntimeError:
+            pass
     gen_s = time.time() - t
     nnz = A.nnz
     if dist:

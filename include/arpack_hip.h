@@ -224,9 +224,11 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * full-storage kernel.  y is then not bitwise reproducible run to run
  * (transposed terms are summed in LDS in schedule order).  on == 0 restores
  * the full-storage kernel.  For a row-distributed operator (after
- * arpack_hip_dist_create) every rank must end up in the same mode: the halo and
- * spill exchanges differ, so call it on all ranks and fall back together if
- * any rank returns -1. */
+ * arpack_hip_dist_create) the call is COLLECTIVE with on = 1: the halo and
+ * spill exchanges differ between the modes, so every rank must call it; the
+ * ranks agree (one allreduce) and if any rank's plan fails every rank keeps
+ * the full-storage kernel and returns nonzero (its own plan error, or -2 when
+ * only another rank's plan failed). */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
@@ -308,7 +310,10 @@ typedef struct arpack_hip_dist arpack_hip_dist;
 /* Distributed operator from this rank's CSR rows [row0, row0 + A.n) with GLOBAL
  * column indices: computes the halo plan with the other ranks (collective) and
  * remaps A's columns to the local extended-x layout.  Returns 0; -3/-4 if the
- * row blocks are not contiguous or a halo reaches beyond the neighbours. */
+ * row blocks are not contiguous or a halo reaches beyond the neighbours; -1 on
+ * every rank if any rank fails to set up.  A CSR declared symmetric before this
+ * call keeps symmetric storage only if every rank declared it and every rank's
+ * symmetric plan succeeds; otherwise all ranks run full storage. */
 int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_global, int64_t row0);
 void arpack_hip_dist_destroy(arpack_hip_dist* D);
 /* y = A x on this rank's rows (device pointers), collective over the ranks:

@@ -62,6 +62,44 @@ def spmv_chain(pkg, out, rank, world):
     del DA, DB
 
 
+def sym_mixed(pkg, out, rank, world):
+    """g4's operator plus one symmetric pair (0, j) whose upper entry on rank 0
+    reaches past the symmetric-storage LDS window while rank 1's block stays
+    narrow: rank 0's symmetric plan fails, rank 1's succeeds.  The storage-mode
+    switch is collective, so both ranks must fall back to full storage (rank 0
+    rc = its plan error, rank 1 rc = -2) and the solve must still run."""
+    import scipy.sparse as sp
+    g = dict(np.load(os.path.join(GOLDEN, "g4_banded.npz"), allow_pickle=False))
+    rp, col, val = _mat(g["spec"])
+    n = len(rp) - 1
+    j = n // 2 + 100
+    A = M.to_scipy(rp, col, val).tolil()
+    A[0, j] = A[j, 0] = -0.5
+    A = A.tocsr()
+    A.sort_indices()
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    nloc = r1 - r0
+    B = pkg.CSR.from_arrays(A.indptr[r0:r1 + 1].astype(np.int64) - A.indptr[r0],
+                            A.indices[A.indptr[r0]:A.indptr[r1]].astype(np.int32),
+                            A.data[A.indptr[r0]:A.indptr[r1]].copy())
+    D = pkg.DistOp(B, n, r0)
+    try:
+        B.set_symmetric(True)
+    except RuntimeError:
+        pass
+    s = pkg.SymRci(nloc, int(g["nev"]), int(g["ncv"]), "LA", float(g["tol"]),
+                   mxiter=int(g["mxiter"]), v0=g["v0"][r0:r1], device=True)
+    assert pkg.pdsaupd_cycles(s, D, -1) == 99
+    d, z, nconv = s.eupd(dist=D)
+    z = z.numpy() if hasattr(z, "numpy") else z
+    np.savez(os.path.join(out, "rank%d.npz" % rank), sym_rc=np.array([B.last_rc]), d=d,
+             iparam=s.iparam.copy(), info=s.info.copy(),
+             z=z.reshape(int(g["nev"]), nloc)[:nconv].T.copy())
+    if rank == 0:
+        sp.save_npz(os.path.join(out, "A.npz"), A)
+    del D
+
+
 def main():
     case, fixture, out = sys.argv[1], sys.argv[2], sys.argv[3]
     info0 = len(sys.argv) > 4 and sys.argv[4] == "info0"
@@ -71,8 +109,8 @@ def main():
     dist.init_process_group("gloo")
     pkg = load_pkg()
     pkg.comm_init_host(world, rank, device=0)
-    if case == "spmv_chain":
-        spmv_chain(pkg, out, rank, world)
+    if case in ("spmv_chain", "sym_mixed"):
+        (spmv_chain if case == "spmv_chain" else sym_mixed)(pkg, out, rank, world)
         dist.barrier()
         pkg.comm_destroy()
         dist.destroy_process_group()

@@ -157,3 +157,19 @@ def test_single_precision_error_codes(pkg, fam, cases):
         assert want[0] == 99 and want[1] < 0, (over, want)
         assert _call_icb(_fresh(pkg.LIB_PATH), name + "_c", a, cplx, True) == want, over
         assert _call_fortran(_fresh(pkg.LIB_PATH), name + "_", a, cplx, True) == want, over
+
+
+@pytest.mark.parametrize("name,cplx,lw_of", [
+    ("dsaupd_c", False, lambda ncv: ncv * ncv + 8 * ncv),
+    ("dnaupd_c", False, lambda ncv: 3 * ncv * ncv + 6 * ncv),
+    ("znaupd_c", True, lambda ncv: 3 * ncv * ncv + 5 * ncv)])
+def test_ncv_above_engine_limit(pkg, name, cplx, lw_of):
+    """ncv above the engine's documented limit (8000: the finalize stages ncv + 2
+    sums in 64 KB of LDS) is rejected like ncv > n, info = -3,
+    before any array is touched (the arrays here are untouched lazy zero pages)."""
+    a = dict(BASE_S if name[1] == "s" else BASE_N, n=9000, ncv=8001, nev=4)
+    a["lw"] = lw_of(a["ncv"])
+    assert _call_icb(_fresh(pkg.LIB_PATH), name, a, cplx=cplx) == (99, -3)
+    a["ncv"] = 8000  # at the limit the checks pass (-7 from a short workl proves it)
+    a["lw"] = 1
+    assert _call_icb(_fresh(pkg.LIB_PATH), name, a, cplx=cplx) == (99, -7)
