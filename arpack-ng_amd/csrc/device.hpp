@@ -78,12 +78,16 @@ struct Workspace {
     // ncv > 64 only: nblk * kBlock * (ncv + 1) doubles of per-thread output
     // columns for the generic (alias-safe) V*Q and gemm kernels
     double* scratch = nullptr;
+    // V-load policy of the Gram-Schmidt / V*Q passes (kernels.hip VPol): plain
+    // loads when the n x ncv basis fits the Infinity Cache, else non-temporal
+    bool v_plain = false;
     LzState* st = nullptr;
     LzState* st_host = nullptr;  // pinned mirror
     double* host_scratch = nullptr;  // pinned, >= 4*stride doubles
 };
 
 int choose_nblk(int64_t n);
+bool choose_v_plain(int64_t n, int ncv, int elem);
 hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Workspace& ws);
 

@@ -30,17 +30,22 @@ namespace {
 
 constexpr double kSafminD = DBL_MIN;
 
-// Loads of the Krylov basis V in the Gram-Schmidt passes: non-temporal, so
-// the 1-2.4 GB sweep does not evict the n-vectors every pass re-reads (w, r)
-// from the caches (same-box A/B over 25 cycles: +3.2% cycle rate;
-// -DAHIP_PLAIN_V restores plain loads)
-template <class T>
+// Loads of the Krylov basis V in the Gram-Schmidt and V*Q passes.  Policy POL:
+//   kPolNt / kPolNtRev  non-temporal, sweeping rows first-to-last / last-to-first:
+//            a basis of several hundred MB or more is streamed from HBM; the NT
+//            hint keeps the 1-2.4 GB sweep from evicting the n-vectors every pass
+//            re-reads (w, r) from the caches (+3.2% cycle rate at n = 1e7), and
+//            alternating directions start each pass on rows the previous one left
+//            in the 256 MB Infinity Cache;
+//   kPolPlain  plain loads: a basis that fits the Infinity Cache (<= ~400 MB)
+//            is re-read from it by the next pass (same-box A/B: +7% cycle rate at
+//            n = 1e6, +4% at 1.25e6 rows, -2.7% at 2.5e6 and 1e7 -- hence the
+//            size rule in ws_create, AHIP_V_POLICY=nt|plain to override).
+enum VPol : int { kPolNt = 0, kPolNtRev = 1, kPolPlain = 2 };
+template <int POL, class T>
 __device__ __forceinline__ T vld(const T* p) {
-#ifdef AHIP_PLAIN_V
-    return *p;
-#else
-    return __builtin_nontemporal_load(p);
-#endif
+    if constexpr (POL == kPolPlain) return *p;
+    else return __builtin_nontemporal_load(p);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_place(int64_t n, const R* __restrict
 // ------------------------------------------------------------------- dots ---
 // Exact compile-time column count J (branch-free unrolled loads: all J column
 // loads of a row are in flight together).  WM: 0 no w'u, 1 w == u, 2 w != u.
-template <class R, int J, int WM, bool REV = false>
+template <class R, int J, int WM, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __restrict__ V,
                                                  int64_t ld, const R* __restrict__ u,
                                                  const R* __restrict__ w,
@@ -146,9 +151,9 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
     constexpr int JL = J > 0 ? J : 1;
     double cur[JL], cu = 0.0, cw = 0.0;
     auto load = [&](int64_t it, double (&dst)[JL], double& du, double& dw) {
-        const int64_t r = REV ? n - 1 - it : it;  // REV: sweep last-to-first (see k_update_fused)
+        const int64_t r = POL == kPolNtRev ? n - 1 - it : it;  // see VPol
 #pragma unroll
-        for (int k = 0; k < J; ++k) dst[k] = vld(Vb + r + (int64_t)k * ld);
+        for (int k = 0; k < J; ++k) dst[k] = vld<POL>(Vb + r + (int64_t)k * ld);
         du = u[r];
         if constexpr (WM == 2) dw = w[r];
     };
@@ -173,11 +178,11 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
 // ----------------------------------------------------------------- update ---
 // rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
 // same pass (the V row stays in registers: one HBM read of V serves both).
-// REV: sweep the rows last-to-first.  The preceding V pass (the CGS dots)
+// POL = kPolNtRev: sweep the rows last-to-first.  The preceding V pass (the CGS dots)
 // ended on the last rows, which the 256 MB Infinity Cache still holds, so a
 // reversed sweep starts on cache hits (and the next forward pass on this one's
 // last rows).
-template <class R, int J, bool SPEC, bool REV = false>
+template <class R, int J, bool SPEC, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
     int64_t n, const R* __restrict__ V, int64_t ld, const double* __restrict__ c,
     const R* rin, R* rout, double* __restrict__ part, int pstride,
@@ -189,10 +194,10 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
     double rr = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n; it += stride) {
-        const int64_t i = REV ? n - 1 - it : it;
+        const int64_t i = POL == kPolNtRev ? n - 1 - it : it;
         double vrow[J];
 #pragma unroll
-        for (int k = 0; k < J; ++k) vrow[k] = vld(V + i + (int64_t)k * ld);
+        for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < J; ++k) s += vrow[k] * c[k];
@@ -374,7 +379,7 @@ __global__ void k_zero_if(int64_t n, R* r, const LzState* st) {
 }
 
 // -------------------------------------------------------------- V*Q update --
-template <class R, int MAXK>
+template <class R, int MAXK, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t ld,
                                                       int kplusp, int kev,
                                                       const double* __restrict__ Q, int ldq,
@@ -394,7 +399,8 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t l
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         double v[MAXK];
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) v[k] = (k < kplusp) ? (double)vld(V + i + (int64_t)k * ld) : 0.0;
+        for (int k = 0; k < MAXK; ++k)
+            v[k] = (k < kplusp) ? (double)vld<POL>(V + i + (int64_t)k * ld) : 0.0;
         double vnext = 0.0;
         if (next) {
             const double* q = sq + kev * kplusp;
@@ -611,6 +617,21 @@ inline int grid_for(int64_t n, int per_block = kBlock, int cap = 8192) {
 
 // ================================================================ launchers ==
 
+// V-load policy (VPol): plain loads when the basis fits the Infinity Cache.
+// The element size is taken as 8 B for both families: a float basis of the
+// same n streams half the bytes but its passes are shorter in the same ratio.
+bool choose_v_plain(int64_t n, int ncv, int elem) {
+    static const int forced = [] {
+        const char* e = getenv("AHIP_V_POLICY");
+        if (!e) return -1;
+        if (!strcmp(e, "plain")) return 1;
+        if (!strcmp(e, "nt")) return 0;
+        return -1;
+    }();
+    if (forced >= 0) return forced == 1;
+    return (double)n * ncv * elem <= 400e6;
+}
+
 int choose_nblk(int64_t n) {
     // AHIP_NBLK: tuning knob for the partial-sum grid (default kMaxRedBlocks)
     static const int64_t cap = [] {
@@ -635,6 +656,7 @@ hipError_t ws_create(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
 
 static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     ws.stream = s;
+    ws.v_plain = choose_v_plain(n, ncv, 8);
     ws.nblk = choose_nblk(n);
     ws.stride = ncv + 2;
     hipError_t e;
@@ -717,7 +739,7 @@ void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc,
     M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41) M(42) M(43) M(44) M(45) M(46) M(47) M(48) \
     M(49) M(50) M(51) M(52) M(53) M(54) M(55) M(56) M(57) M(58) M(59) M(60) M(61) M(62) M(63) M(64)
 
-template <class R, int WM, bool REV = false>
+template <class R, int WM, int POL = kPolNt>
 static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R* V, int64_t ld,
                         const R* u, const R* w, int wslot, int gate) {
     const dim3 g(ws.nblk), b(kBlock);
@@ -728,7 +750,7 @@ static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R*
             break;
 #define AHIP_DOTS_CASE(J)                                                                          \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_dots<R, J, WM, REV>), g, b, 0, ws.stream, n, j0, V, ld, u, w,        \
+        hipLaunchKernelGGL((k_dots<R, J, WM, POL>), g, b, 0, ws.stream, n, j0, V, ld, u, w,        \
                            ws.part, ws.stride, wslot, ws.st, gate);                                \
         break;
         AHIP_CASES_1_32(AHIP_DOTS_CASE)
@@ -752,7 +774,8 @@ void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R
     for (int j0 = 0; j0 < j; j0 += 32) {
         const int jc = (j - j0 < 32) ? j - j0 : 32;
         if (j0 > 0) launch_dots<R, 0>(ws, n, j0, jc, V, ld, u, w, j, gate);
-        else if (w == u && rev) launch_dots<R, 1, true>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else if (w == u && ws.v_plain) launch_dots<R, 1, kPolPlain>(ws, n, j0, jc, V, ld, u, w, j, gate);
+        else if (w == u && rev) launch_dots<R, 1, kPolNtRev>(ws, n, j0, jc, V, ld, u, w, j, gate);
         else if (w == u) launch_dots<R, 1>(ws, n, j0, jc, V, ld, u, w, j, gate);
         else launch_dots<R, 2>(ws, n, j0, jc, V, ld, u, w, j, gate);
     }
@@ -773,9 +796,12 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
     case J:                                                                                        \
-        if (spec && rev)                                                                           \
-            hipLaunchKernelGGL((k_update_fused<R, J, true, true>), g, b, 0, ws.stream, n, V, ld, c,\
-                               rin, rout, ws.part, ws.stride, ws.st, gate);                        \
+        if (spec && ws.v_plain)                                                                    \
+            hipLaunchKernelGGL((k_update_fused<R, J, true, kPolPlain>), g, b, 0, ws.stream, n, V,  \
+                               ld, c, rin, rout, ws.part, ws.stride, ws.st, gate);                 \
+        else if (spec && rev)                                                                      \
+            hipLaunchKernelGGL((k_update_fused<R, J, true, kPolNtRev>), g, b, 0, ws.stream, n, V,  \
+                               ld, c, rin, rout, ws.part, ws.stride, ws.st, gate);                 \
         else if (spec)                                                                             \
             hipLaunchKernelGGL((k_update_fused<R, J, true>), g, b, 0, ws.stream, n, V, ld, c, rin, \
                                rout, ws.part, ws.stride, ws.st, gate);                             \
@@ -830,15 +856,13 @@ void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int
     const int g = ws.nblk;
     ProfScope ps(kProfVq, ws.stream,
                  (double)sizeof(R) * n * (kplusp + kev + (betak > 0.0) + 2));
-    if (kplusp <= 16)
-        hipLaunchKernelGGL((k_vq_update<R, 16>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
-                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
-    else if (kplusp <= 32)
-        hipLaunchKernelGGL((k_vq_update<R, 32>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
-                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
-    else if (kplusp <= 64)
-        hipLaunchKernelGGL((k_vq_update<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
-                           kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.part, ws.stride);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev, ws.q,
+                           kplusp, sigmak, betak, r, ws.part, ws.stride);
+    };
+    if (kplusp <= 16) ws.v_plain ? go(k_vq_update<R, 16, kPolPlain>) : go(k_vq_update<R, 16>);
+    else if (kplusp <= 32) ws.v_plain ? go(k_vq_update<R, 32, kPolPlain>) : go(k_vq_update<R, 32>);
+    else if (kplusp <= 64) ws.v_plain ? go(k_vq_update<R, 64, kPolPlain>) : go(k_vq_update<R, 64>);
     else  // ws.scratch: nblk * kBlock * (ncv + 1) doubles, allocated by ws_create for ncv > 64
         hipLaunchKernelGGL(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
                            kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.scratch, ws.part,

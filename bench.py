@@ -108,6 +108,9 @@ def main():
                     help="sym: the operator is declared symmetric (dsaupd's contract) and the "
                          "SpMV streams its upper triangle (arpack_hip_csr_set_symmetric); full: "
                          "full CSR, bitwise SciPy's csr_matvec.")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="measurement aid: with one rank, still run the row-distributed engine "
+                         "(1-rank RCCL communicator, DistOp) to price its machinery")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
     args = ap.parse_args()
@@ -133,9 +136,11 @@ def main():
         r0, r1 = pkg.partition_rows(n, world, rank)
     else:
         r0, r1 = 0, n
+        if args.force_dist:
+            pkg.comm_init(1, 0, pkg.comm_unique_id(), device=0)
     t = time.time()
     A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row, r0, r1)
-    if world > 1:
+    if world > 1 or args.force_dist:
         D = pkg.DistOp(A, n, r0)
     storage = "full"
     if args.storage == "sym":  # row blocks: upper-triangle SpMV + forward spill exchange
@@ -323,9 +328,10 @@ def main():
                 (nopx / elapsed) / out["cpu_baseline"]["lanczos_steps_per_s"]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist:
+    if dist or args.force_dist:
         del D
         pkg.comm_destroy()
+    if dist:
         dist.destroy_process_group()
 
 

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", type=int, nargs="*", default=[3, 4, 5, 6, 7])
     a = ap.parse_args()
     pkg = load_pkg()
     A = pkg.CSR.banded_sym(a.n, 1234, 4096, 25)
@@ -32,10 +33,15 @@ def main():
     A.set_symmetric(True)
     out["sym_ms"] = A.time_spmv(a.reps)
     A.matvec_device(x.at(0), y2.at(0))
-    for v in (3, 4, 5, 6, 7):
+    for v in a.variants:
         A.set_kernel(12, v)
         out["sym_v%d_ms" % v] = A.time_spmv(a.reps)
+        A.matvec_device(x.at(0), y2.at(0))
+        d = np.abs(y1.numpy() - y2.numpy())
+        out["sym_v%d_maxrel" % v] = float((d / np.maximum(np.abs(y1.numpy()), 1e-300)).max())
     A.set_kernel(12, 0)
+    out["sym_ms_again"] = A.time_spmv(a.reps)
+    A.matvec_device(x.at(0), y2.at(0))
     d = np.abs(y1.numpy() - y2.numpy())
     out["max_abs_diff"] = float(d.max())
     out["max_rel_diff"] = float((d / np.maximum(np.abs(y1.numpy()), 1e-300)).max())
