@@ -47,6 +47,8 @@ struct LzState {
     int nitref;
     int force_dgks2;  // test hook (AHIP_FORCE_DGKS2=1): always take the second refinement
     int pad;
+    double vscale;  // chained steps: 1/rnorm, applied by the update pass to the raw
+                    // column V(:,j) and to A*r (1.0 after a plain kFinCgs)
 };
 
 // Finalize phases (which logic the single-block finalize kernel applies).
@@ -60,14 +62,19 @@ enum FinPhase : int {
     kFinCoef = 6,     // coef0 = first m-1 sums, state untouched   (getv0 CGS)
     kFinDgks1Lazy = 7,  // kFinDgks1; a needed second refinement parks the cycle
                         // (st.abort = 2 at step j) for the host to finish it
+    kFinCgsChained = 8, // step j of a chained (free-running) cycle: the deferred
+                        // kFinDgks1Lazy of step j-1 (region 2 sums), then kFinCgs
+                        // on the sums of the RAW residual (v_j not yet formed):
+                        // coefficients rescaled by 1/rnorm (st.vscale).  abort = 3:
+                        // rnorm outside the raw-vector range, redo step j unchained
 };
 
 struct Workspace {
     hipStream_t stream = nullptr;
     int nblk = 0;        // partial-sum blocks for this n
     int stride = 0;      // >= ncv + 2
-    double* part = nullptr;   // nblk * stride
-    double* sums = nullptr;   // stride (raw sums of the last finalize)
+    double* part = nullptr;   // 2 regions of nblk * stride (region 2: chained steps)
+    double* sums = nullptr;   // 2 * stride (raw sums of the last finalize)
     double* coef = nullptr;   // 3 * stride : CGS, DGKS-1, DGKS-2 coefficient vectors
     double* rec = nullptr;    // 2 * (ncv+1): alpha_j, beta_j per step
     double* q = nullptr;      // ncv * ncv  (V*Q matrix for dsapps / eupd)
@@ -103,14 +110,27 @@ void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sca
 template <class R>
 void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, const R* w,
           int gate);
+// Extras of a chained (free-running) Lanczos step's update passes
+// (kernels.hip k_update_fused): normalise the raw column V(:,j) in place and
+// scale w by st.vscale; store rout also to raw1/raw2; write the partials to
+// `part` (default ws.part).
+template <class R>
+struct UpdateChain {
+    bool chained = false;
+    R* raw1 = nullptr;
+    R* raw2 = nullptr;
+    double* part = nullptr;
+};
 // rout = rin - V(:,0:j) * coef[which]; if spec: partials of [V' rout ; rout' rout]
 template <class R>
 void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
-            R* rout, bool spec, int gate);
+            R* rout, bool spec, int gate, const UpdateChain<R>& x = UpdateChain<R>{});
 // single-block fixed-order finalize of m = j+1 sums and the phase logic
 // from_sums: the m sums are already in ws.sums (reduced across ranks).
+// m2 > 0 (kFinCgsChained): a second region of m2 partial slots at
+// ws.part + nblk * stride (the deferred DGKS sums of step j-1).
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
-              bool from_sums = false);
+              bool from_sums = false, int m2 = 0, int rstart_prev = 0);
 // resid = 0 if st.zero
 template <class R>
 void zero_if(const Workspace& ws, int64_t n, R* r);

@@ -182,27 +182,53 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
 // ended on the last rows, which the 256 MB Infinity Cache still holds, so a
 // reversed sweep starts on cache hits (and the next forward pass on this one's
 // last rows).
+//
+// Chained Lanczos steps (free-running engine, kFinCgsChained):
+//   chained: V(:,J-1) holds the RAW residual r (v_j = r / rnorm not formed; the
+//            SpMV ran on r): the pass normalises it in place (the same product
+//            k_place forms) and takes w = vscale * (A r);
+//   raw1/2:  also store rout there (the next step's raw column, and the x
+//            buffer of a row-distributed SpMV); with the gate closed (no DGKS
+//            sweep this step) the pass only copies rin to them.
 template <class R, int J, bool SPEC, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
-    int64_t n, const R* __restrict__ V, int64_t ld, const double* __restrict__ c,
+    int64_t n, R* __restrict__ V, int64_t ld, const double* __restrict__ c,
     const R* rin, R* rout, double* __restrict__ part, int pstride,
-    const LzState* __restrict__ st, int gate) {
-    if (gate_closed(st, gate)) return;
+    const LzState* __restrict__ st, int gate, int chained, R* __restrict__ raw1,
+    R* __restrict__ raw2) {
+    if (st->abort) return;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    if (gate >= 0 && st->dgks != gate) {
+        if (raw1)
+            for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+                const R r = rin[i];
+                raw1[i] = r;
+                if (raw2) raw2[i] = r;
+            }
+        return;
+    }
+    const double vs = chained ? st->vscale : 1.0;  // exact no-op when not chained
     double acc[J];
 #pragma unroll
     for (int k = 0; k < J; ++k) acc[k] = 0.0;
     double rr = 0.0;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n; it += stride) {
         const int64_t i = POL == kPolNtRev ? n - 1 - it : it;
         double vrow[J];
 #pragma unroll
         for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
+        if (chained) {  // v_j = r * (1/rnorm), stored as k_place would
+            const R v = (R)(vrow[J - 1] * vs);
+            V[i + (int64_t)(J - 1) * ld] = v;
+            vrow[J - 1] = (double)v;
+        }
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < J; ++k) s += vrow[k] * c[k];
-        const R r = (R)((double)rin[i] - s);
+        const R r = (R)((double)rin[i] * vs - s);
         rout[i] = r;
+        if (raw1) raw1[i] = r;
+        if (raw2) raw2[i] = r;
         if constexpr (SPEC) {
             const double rd = (double)r;
             rr += rd * rd;
@@ -246,30 +272,86 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const double* __restrict__
     if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// One refinement decision (SRC/dsaitr.f:634-781) on the sums of [V'r ; r'r]
+// (jm = index of r'r) for step jj; returns `take` (which coefficient slot the
+// next sweep uses, 0 for none).  Thread 0 only.
+__device__ int refine_decision(int phase, const double* ss, int jm, int jj, int rstart_jj,
+                               LzState* st, double* rec) {
+    const double rn = sqrt(fabs(ss[jm]));
+    int take = 0;
+    if (phase == kFinPostCgs) {
+        st->rnorm = rn;
+        if (rn > 0.717 * st->wnorm) {
+            st->dgks = 0;
+        } else {
+            st->dgks = 1;
+            st->nrorth += 1;
+            take = 1;
+        }
+    } else if (phase == kFinDgks1 || phase == kFinDgks1Lazy) {
+        if (rn > 0.717 * st->rnorm && !st->force_dgks2) {
+            st->rnorm = rn;
+            st->dgks = 0;
+        } else {
+            st->nitref += 1;
+            st->rnorm = rn;
+            st->dgks = 2;
+            take = 2;
+            if (phase == kFinDgks1Lazy) {  // rare: the host runs the second sweep
+                st->abort = 2;
+                st->abort_j = jj;
+            }
+        }
+    } else {  // kFinDgks2
+        if (rn > 0.717 * st->rnorm) {
+            st->rnorm = rn;
+        } else {
+            st->nitref += 1;
+            st->zero = 1;
+            st->rnorm = 0.0;
+        }
+        st->dgks = 0;
+    }
+    if (take) {
+        st->alpha += ss[jm - 1];
+        if (jj == 1 || rstart_jj) st->beta = 0.0;
+    }
+    rec[2 * (jj - 1)] = st->alpha;
+    rec[2 * (jj - 1) + 1] = st->beta;
+    return take;
+}
+
+// Single-block finalize: fixed-order sums of the per-block partials (region 1:
+// m slots of `part`; region 2: m2 slots of `part2`, only for kFinCgsChained)
+// and the phase logic.  from_sums: the m + m2 sums are already in `sums`
+// (reduced, and allreduced across ranks).
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
                                                    int from_sums, int m, int phase, int j,
                                                    int rstart, int gate, double* __restrict__ sums,
                                                    double* __restrict__ coef, int cstride,
                                                    double* __restrict__ rec,
                                                    LzState* __restrict__ st,
-                                                   double* __restrict__ hcol, int hld) {
+                                                   double* __restrict__ hcol, int hld,
+                                                   const double* __restrict__ part2, int m2,
+                                                   int rstart_prev) {
     if (gate_closed(st, gate)) return;
-    // the m = j+1 (<= ncv+2) sums are staged in dynamic LDS sized by the launch
-    // (finalize(): m doubles), so any ncv the argument checks accept fits
+    // the m + m2 (<= 2 ncv + 4) sums are staged in dynamic LDS sized by the
+    // launch, so any ncv the argument checks accept fits
     extern __shared__ double s_sum[];
     const int nt = blockDim.x;
+    const int mt = m + m2;
     if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
-        for (int k = threadIdx.x; k < m; k += nt) s_sum[k] = sums[k];
+        for (int k = threadIdx.x; k < mt; k += nt) s_sum[k] = sums[k];
     } else {
         // 32 slots per round, 32 threads (half a wave) per slot: thread `sub`
         // sums blocks sub, sub+32, ... in four independent chains (coalesced
         // 256-B rows of the k-major partials), then the half wave reduces
         const int sub = threadIdx.x & 31;
-        for (int k0 = 0; k0 < m; k0 += 32) {
+        for (int k0 = 0; k0 < mt; k0 += 32) {
             const int k = k0 + (threadIdx.x >> 5);
             double s = 0.0;
-            if (k < m) {
-                const double* p = part + (int64_t)k * nblk;
+            if (k < mt) {
+                const double* p = k < m ? part + (int64_t)k * nblk : part2 + (int64_t)(k - m) * nblk;
                 double s1 = 0.0, s2 = 0.0, s3 = 0.0;
                 int b = sub;
                 for (; b + 96 < nblk; b += 128) {
@@ -283,19 +365,73 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
             }
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 32);
-            if (sub == 0 && k < m) s_sum[k] = s;
+            if (sub == 0 && k < mt) s_sum[k] = s;
         }
     }
     __syncthreads();
     const int t = threadIdx.x;
-    for (int k = t; k < m; k += nt) sums[k] = s_sum[k];
+    for (int k = t; k < mt; k += nt) sums[k] = s_sum[k];
     const int jm = m - 1;  // index of the w'u / r'r slot
+    if (phase == kFinCgsChained) {
+        // (1) the first DGKS refinement of step j-1, deferred to here: region 2
+        //     holds its [V_{j-1}' r ; r'r] (SRC/dsaitr.f:730-771)
+        __shared__ int s_take2, s_go;
+        if (t == 0) {
+            s_take2 = 0;
+            if (st->dgks == 1)
+                s_take2 = refine_decision(kFinDgks1Lazy, s_sum + m, m2 - 1, j - 1, rstart_prev, st, rec);
+            // (2) v_j = r / rnorm was NOT formed: the SpMV ran on the raw residual
+            //     (A r = rnorm * A v_j), so the CGS sums are rescaled here and the
+            //     update pass normalises V(:,j) in place (scale st->vscale)
+            const double rn = st->rnorm;
+            s_go = 0;
+            if (st->abort) {
+            } else if (!(rn > 0.0)) {  // invariant subspace at step j (SRC/dsaitr.f:378)
+                st->abort = 1;
+                st->abort_j = j;
+            } else if (rn < 1e-150 || rn > 1e150) {  // raw-vector range guard: the host
+                st->abort = 3;                       // redoes step j with v_j formed first
+                st->abort_j = j;
+            } else {
+                s_go = 1;
+            }
+        }
+        __syncthreads();
+        if (s_take2) {  // the parked second refinement's coefficients (host path)
+            for (int k = t; k < m2 - 1; k += nt) {
+                coef[2 * cstride + k] = s_sum[m + k];
+                if (hld) hcol[(int64_t)(j - 2) * hld + k] += s_sum[m + k];
+            }
+        }
+        if (!s_go) return;
+        const double vs = 1.0 / st->rnorm;  // k_place's factor for rnorm >= safmin
+        for (int k = t; k < jm - 1; k += nt) {  // h(k) = V_k' w = vs * V_k' (A r)
+            const double h = s_sum[k] * vs;
+            coef[k] = h;
+            if (hld) hcol[(int64_t)(j - 1) * hld + k] = h;
+        }
+        if (t == 0) {
+            const double hj = (s_sum[jm - 1] * vs) * vs;  // v_j' w = vs^2 r' (A r)
+            coef[jm - 1] = hj;
+            if (hld) hcol[(int64_t)(j - 1) * hld + jm - 1] = hj;
+            st->vscale = vs;
+            st->zero = 0;
+            st->dgks = 0;
+            st->wnorm = sqrt(fabs(s_sum[jm])) * vs;
+            st->alpha = hj;
+            st->beta = (j == 1 || rstart) ? 0.0 : st->rnorm;
+            rec[2 * (j - 1)] = st->alpha;
+            rec[2 * (j - 1) + 1] = st->beta;
+        }
+        return;
+    }
     if (phase == kFinCgs) {
         for (int k = t; k < jm; k += nt) {
             coef[k] = s_sum[k];
             if (hld) hcol[(int64_t)(j - 1) * hld + k] = s_sum[k];  // h(1:j,j) (dnaitr.f:566)
         }
         if (t == 0) {
+            st->vscale = 1.0;
             st->zero = 0;
             st->dgks = 0;
             st->wnorm = sqrt(fabs(s_sum[jm]));
@@ -317,50 +453,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     }
     // refinement phases share the "speculative coefficients" layout
     __shared__ int s_take;
-    if (t == 0) {
-        const double rn = sqrt(fabs(s_sum[jm]));
-        int take = 0;  // 1: store next-sweep coefficients into coef slot
-        if (phase == kFinPostCgs) {
-            st->rnorm = rn;
-            if (rn > 0.717 * st->wnorm) {
-                st->dgks = 0;
-            } else {
-                st->dgks = 1;
-                st->nrorth += 1;
-                take = 1;
-            }
-        } else if (phase == kFinDgks1 || phase == kFinDgks1Lazy) {
-            if (rn > 0.717 * st->rnorm && !st->force_dgks2) {
-                st->rnorm = rn;
-                st->dgks = 0;
-            } else {
-                st->nitref += 1;
-                st->rnorm = rn;
-                st->dgks = 2;
-                take = 2;
-                if (phase == kFinDgks1Lazy) {  // rare: the host runs the second sweep
-                    st->abort = 2;
-                    st->abort_j = j;
-                }
-            }
-        } else {  // kFinDgks2
-            if (rn > 0.717 * st->rnorm) {
-                st->rnorm = rn;
-            } else {
-                st->nitref += 1;
-                st->zero = 1;
-                st->rnorm = 0.0;
-            }
-            st->dgks = 0;
-        }
-        if (take) {
-            st->alpha += s_sum[jm - 1];
-            if (j == 1 || rstart) st->beta = 0.0;
-        }
-        rec[2 * (j - 1)] = st->alpha;
-        rec[2 * (j - 1) + 1] = st->beta;
-        s_take = take;
-    }
+    if (t == 0) s_take = refine_decision(phase, s_sum, jm, j, rstart, st, rec);
     __syncthreads();
     const int take = s_take;
     if (take) {
@@ -660,8 +753,9 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     ws.nblk = choose_nblk(n);
     ws.stride = ncv + 2;
     hipError_t e;
-    if ((e = hipMalloc(&ws.part, sizeof(double) * (size_t)ws.nblk * ws.stride))) return e;
-    if ((e = hipMalloc(&ws.sums, sizeof(double) * (size_t)ws.stride))) return e;
+    // two partial regions: the second holds a chained step's deferred DGKS sums
+    if ((e = hipMalloc(&ws.part, sizeof(double) * 2 * (size_t)ws.nblk * ws.stride))) return e;
+    if ((e = hipMalloc(&ws.sums, sizeof(double) * 2 * (size_t)ws.stride))) return e;
     if ((e = hipMalloc(&ws.coef, sizeof(double) * 3 * (size_t)ws.stride))) return e;
     if ((e = hipMalloc(&ws.rec, sizeof(double) * 2 * (size_t)(ncv + 1)))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * (size_t)ncv * ncv))) return e;
@@ -783,65 +877,74 @@ void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R
 
 template <class R>
 void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
-            R* rout, bool spec, int gate) {
+            R* rout, bool spec, int gate, const UpdateChain<R>& x) {
     const double* c = ws.coef + (size_t)which * ws.stride;
     ProfScope ps(gate == 2 ? kProfOther : kProfUpdate, ws.stream,
-                 gate == 2 ? 0.0 : (double)sizeof(R) * n * (j + 2));
+                 gate == 2 ? 0.0
+                           : (double)sizeof(R) * n *
+                                 (j + 2 + (x.chained ? 1 : 0) + (x.raw1 ? 1 : 0) + (x.raw2 ? 1 : 0)));
     const dim3 g(ws.nblk), b(kBlock);
     const bool rev = dir_rev(j, which, false);
+    double* part = x.part ? x.part : ws.part;
+    R* Vw = const_cast<R*>(V);  // written only by a chained pass (its column j)
     // fused up to j = 64 (ncv <= 64: dnaupd's C3 runs ncv = 40); the V row of a
     // fused pass lives in registers, so a wider J trades occupancy for
     // in-flight loads per wave (64 column loads per row at J = 64)
     if (j >= 1 && j <= 64) {
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, g, b, 0, ws.stream, n, Vw, ld, c, rin, rout, part, ws.stride,
+                               ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2);
+        };
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
     case J:                                                                                        \
-        if (spec && ws.v_plain)                                                                    \
-            hipLaunchKernelGGL((k_update_fused<R, J, true, kPolPlain>), g, b, 0, ws.stream, n, V,  \
-                               ld, c, rin, rout, ws.part, ws.stride, ws.st, gate);                 \
-        else if (spec && rev)                                                                      \
-            hipLaunchKernelGGL((k_update_fused<R, J, true, kPolNtRev>), g, b, 0, ws.stream, n, V,  \
-                               ld, c, rin, rout, ws.part, ws.stride, ws.st, gate);                 \
-        else if (spec)                                                                             \
-            hipLaunchKernelGGL((k_update_fused<R, J, true>), g, b, 0, ws.stream, n, V, ld, c, rin, \
-                               rout, ws.part, ws.stride, ws.st, gate);                             \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_update_fused<R, J, false>), g, b, 0, ws.stream, n, V, ld, c,     \
-                               rin, rout, ws.part, ws.stride, ws.st, gate);                        \
+        if (spec && ws.v_plain) go(k_update_fused<R, J, true, kPolPlain>);                         \
+        else if (spec && rev) go(k_update_fused<R, J, true, kPolNtRev>);                           \
+        else if (spec) go(k_update_fused<R, J, true>);                                             \
+        else go(k_update_fused<R, J, false>);                                                      \
         break;
             AHIP_CASES_1_32(AHIP_UPD_CASE)
             AHIP_CASES_33_64(AHIP_UPD_CASE)
 #undef AHIP_UPD_CASE
             default: break;
         }
-    } else {
+    } else {  // (chained steps run only with ncv <= 64: the solver's choice)
         hipLaunchKernelGGL(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
                            gate);
         if (spec) dots<R>(ws, n, j, V, ld, rout, rout, gate);
     }
 }
 
-void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums) {
-    ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * m);
+void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums,
+              int m2, int rstart_prev) {
+    ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * (m + m2));
     // AHIP_FUSED_FIN=0: two launches (per-slot reduction, then the phase logic)
     static const bool fused = [] {
         const char* e = getenv("AHIP_FUSED_FIN");
         return !(e && e[0] == '0');
     }();
-    const size_t lds = sizeof(double) * (size_t)m;  // s_sum (m <= kMaxNcv + 2)
+    const double* part2 = ws.part + (size_t)ws.nblk * ws.stride;  // region 2 (chained steps)
+    const size_t lds = sizeof(double) * (size_t)(m + m2);  // s_sum (m + m2 <= 2 kMaxNcv + 4)
+    auto fin = [&](int fs) {
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, fs, m,
+                           (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st,
+                           ws.hcol, ws.hld, part2, m2, rstart_prev);
+    };
     if (!from_sums && fused) {  // one launch: the finalize block sums the partials itself
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, 0, m, (int)ph,
-                           j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
+        fin(0);
         return;
     }
     if (!from_sums) {
-        // stage 2a: one workgroup per slot sums that slot's nblk partials (coalesced)
+        // stage 2a: one workgroup per slot sums that slot's nblk partials (coalesced;
+        // region 2 follows region 1 in memory only when m == stride -- so two launches)
         hipLaunchKernelGGL(k_reduce_slots, dim3(m), dim3(256), 0, ws.stream, ws.part, ws.nblk, ws.sums,
                            ws.st, gate);
+        if (m2)
+            hipLaunchKernelGGL(k_reduce_slots, dim3(m2), dim3(256), 0, ws.stream, part2, ws.nblk,
+                               ws.sums + m, ws.st, gate);
     }
-    // stage 2b: the phase logic on the m sums (one small workgroup)
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, 1, m, (int)ph, j,
-                       rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st, ws.hcol, ws.hld);
+    // stage 2b: the phase logic on the m + m2 sums (one small workgroup)
+    fin(1);
 }
 
 template <class R>
@@ -973,7 +1076,7 @@ void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z
     template void dots<R>(const Workspace&, int64_t, int, const R*, int64_t, const R*, const R*,   \
                           int);                                                                    \
     template void update<R>(const Workspace&, int64_t, int, const R*, int64_t, int, const R*, R*,  \
-                            bool, int);                                                            \
+                            bool, int, const UpdateChain<R>&);                                     \
     template void zero_if<R>(const Workspace&, int64_t, R*);                                       \
     template void vq_update<R>(const Workspace&, int64_t, R*, int64_t, int, int, double, double,  \
                                R*);                                                                \

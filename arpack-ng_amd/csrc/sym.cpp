@@ -159,13 +159,13 @@ R* SolverT<R>::dist_x() {
 // Finalize of a reduction; with a multi-GPU distribution the local sums are
 // allreduced across ranks (one RCCL collective) before the phase logic runs.
 template <class R>
-void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate) {
+void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m2, int rstart_prev) {
     if (dist && dist->comm) {
-        dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate);
-        comm_allreduce_sum(dist->comm, ws.sums, m, a.stream);
-        if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true);
+        dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate, false, m2);
+        comm_allreduce_sum(dist->comm, ws.sums, m + m2, a.stream);
+        if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true, m2, rstart_prev);
     } else {
-        dev::finalize(ws, m, ph, j, rstart, gate);
+        dev::finalize(ws, m, ph, j, rstart, gate, false, m2, rstart_prev);
     }
 }
 
@@ -261,6 +261,25 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     int j = k + 1;
     bool restart_pending = !(rnorm > 0.0);
     int rstart_j = -1;  // step at which a restart happened (h(j,1) = 0)
+    // Chained steps (free-running engine, bmat = 'I', ncv <= 64): step j's DGKS
+    // sweep also stores its residual r as the RAW column V(:,j+1) (and the x of a
+    // row-distributed SpMV); step j+1 then runs OP on r instead of forming
+    // v_{j+1} = r/rnorm first, and ONE finalize (kFinCgsChained) takes step j's
+    // deferred refinement decision and step j+1's rescaled CGS coefficients; the
+    // update pass normalises V(:,j+1) in place.  Per step that drops the
+    // k_place pass, one finalize launch and -- on a row distribution -- one
+    // allreduce (3 -> 2).  AHIP_CHAIN=0 disables it.  Lanczos (dsaupd) only: the
+    // rounding of A r / rnorm differs from A (r / rnorm) in the last bit, and the
+    // non-normal operators the Arnoldi path serves (n3: conv-diff, rho = 100) turn
+    // that into a different restart count (42 vs the reference's 40 at tol 1e-10),
+    // while every symmetric fixture keeps the reference's cycles and OP*x counts.
+    static const bool chain_env = [] {
+        const char* e = getenv("AHIP_CHAIN");
+        return !(e && e[0] == '0');
+    }();
+    const bool chain_ok = chain_env && free_run && bI && mode == 1 && ncv <= 64 && !arnoldi;
+    bool chained = false;  // V(:,j) holds the raw residual of step j-1
+    int rstart_prev = 0;
 
     for (;;) {
         while (j <= k + npk) {
@@ -277,6 +296,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                     co_return;
                 }
                 restart_pending = false;
+                chained = false;
                 rstart = 1;
                 rstart_j = j;
                 ws.st_host->abort = 0;
@@ -285,8 +305,9 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
             // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
             R* xop = dist_x() ? dist_x() : (free_run ? vcol(j) : wd + ivj);
-            dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
-                       bI ? nullptr : wd + ipj, j);
+            if (!chained)
+                dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
+                           bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
             g_stats.nopx += 1;
             co_await op(1, ivj, irj, ipj, xop, wd + irj);
@@ -303,20 +324,40 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
             // wnorm and the CGS coefficients h = V_j' B r (SRC/dsaitr.f:538-594)
             dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
-            fin(j + 1, dev::kFinCgs, j, rstart, -1);
+            if (chained)  // + the deferred refinement decision of step j-1 (region 2)
+                fin(j + 1, dev::kFinCgsChained, j, rstart, -1, j, rstart_prev);
+            else
+                fin(j + 1, dev::kFinCgs, j, rstart, -1);
             // r_j = OP*v_j - V_j h; for bmat='I' the same pass also produces the
             // DGKS coefficients V_j' r_j and r_j' r_j (SRC/dsaitr.f:582-639)
-            dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1);
+            {
+                dev::UpdateChain<R> x;
+                x.chained = chained;
+                dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1, x);
+            }
             if (bI) {
                 fin(j + 1, dev::kFinPostCgs, j, rstart, -1);
-                // refinement sweeps, each gated on the device-side decision
-                dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1);
-                // free-running: the second refinement (rare) is not enqueued; if
-                // step j needs it, the finalize parks the cycle (abort = 2) and
-                // the host finishes the step below
-                const bool lazy = free_run;
-                fin(j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
-                if (!lazy) dgks2_tail(j, rstart);
+                const bool next_chained = chain_ok && j < k + npk;
+                if (next_chained) {
+                    // the DGKS sweep (or, without one, a copy) also stores r as the
+                    // raw V(:,j+1); its decision waits for step j+1's finalize
+                    dev::UpdateChain<R> x;
+                    x.raw1 = vcol(j + 1);
+                    x.raw2 = dist_x();
+                    x.part = ws.part + (size_t)ws.nblk * ws.stride;
+                    dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1, x);
+                } else {
+                    // refinement sweeps, each gated on the device-side decision
+                    dev::update(ws, nn, j, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, true, 1);
+                    // free-running: the second refinement (rare) is not enqueued; if
+                    // step j needs it, the finalize parks the cycle (abort = 2) and
+                    // the host finishes the step below
+                    const bool lazy = free_run;
+                    fin(j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
+                    if (!lazy) dgks2_tail(j, rstart);
+                }
+                chained = next_chained;
+                rstart_prev = rstart;
             } else {
                 // generalized problem: every B*r is a reverse-communication request,
                 // so the refinement decisions are taken on the host.
@@ -347,6 +388,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
+        chained = false;  // a resumed cycle restarts with a formed v_j
         if (ws.st_host->abort == 2) {  // step abort_j needs its second DGKS sweep
             const int ja = ws.st_host->abort_j;
             g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
@@ -354,6 +396,14 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             write_state();
             dgks2_tail(ja, ja == rstart_j ? 1 : 0);
             j = ja + 1;
+            continue;
+        }
+        if (ws.st_host->abort == 3) {  // chained step abort_j: rnorm outside the raw
+            const int ja = ws.st_host->abort_j;  // range -- redo it with v_j formed
+            g_stats.nopx -= (k + npk) - ja + 1;
+            ws.st_host->abort = 0;
+            write_state();
+            j = ja;
             continue;
         }
         if (ws.st_host->abort) {  // free-running cycle hit rnorm == 0 at step abort_j
