@@ -142,3 +142,34 @@ def test_znaupd_full_krylov(pkg):
     assert nconv == want["nconv"]
     got, exp = np.sort_complex(d[:nconv]), np.sort_complex(want["d"])
     assert np.all(np.abs(got - exp) <= 1e-9 * max(1.0, np.abs(exp).max())), (got, exp)
+
+
+def test_chained_steps_range_guard(pkg):
+    """Chained free-running Lanczos steps run OP on the raw residual r instead
+    of v = r / rnorm; a residual norm outside [1e-150, 1e150] parks the step
+    (abort = 3) and the host redoes it with v formed first.  An operator scaled
+    by 2^500 (~3e150) puts the early residual norms above the range (later ones,
+    shrinking with convergence, fall back inside it), so both paths alternate.
+    Power-of-two scaling is exact in every operation of the reference, so its
+    results for the scaled operator are its unscaled ones times 2^500: Ritz
+    values, restart cycles and OP*x counts must match.  (Norms here are
+    sqrt(sum x^2), not dnrm2's scaled sum -- DESIGN.md §2 -- so a scale that
+    pushes sum x^2 past the double range, 2^600 or 2^-510, is outside what
+    either path supports; the guard keeps the raw path inside it.)"""
+    e = 500
+    A = M.to_scipy(*M.anderson(20, 2, 4.0, 7))
+    As = (A * 2.0 ** e).tocsr()
+    n, nev, ncv = A.shape[0], 6, 20
+    v0 = M.dlarnv_uniform(n)[0]
+    want = ref.dsaupd_solve(lambda x, *_: As @ x, n, nev, ncv, "LA", 1e-9, v0=v0, mxiter=3000)
+    base = ref.dsaupd_solve(lambda x, *_: A @ x, n, nev, ncv, "LA", 1e-9, v0=v0, mxiter=3000)
+    assert int(want["iparam"][2]) == int(base["iparam"][2])  # the scaling is exact
+    op = pkg.CSR.from_arrays(As.indptr.astype(np.int64), As.indices, As.data)
+    d, z, res = pkg.eigsh(op, n, nev, ncv, "LA", 1e-9, v0=v0, mxiter=3000, device=False)
+    assert res["info"] == want["info"] == 0
+    assert res["iters"] == int(want["iparam"][2])
+    assert res["nopx"] == int(want["iparam"][8])
+    d0 = d * 2.0 ** -e
+    _close(d0, np.asarray(want["d"]) * 2.0 ** -e)
+    r = np.linalg.norm(A @ z - z * d0, axis=0)
+    assert np.all(r <= 1e-8 * max(1.0, np.abs(d0).max())), r
