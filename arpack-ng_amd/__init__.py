@@ -120,6 +120,7 @@ def _declare(L):
     L.arpack_hip_zcsr_destroy.argtypes = [C.c_void_p]
     L.arpack_hip_zcsr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.arpack_hip_zcsr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_zcsr_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_profile.argtypes = [_I]
     L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
     L.arpack_hip_synchronize.restype = C.c_int

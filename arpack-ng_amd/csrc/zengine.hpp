@@ -25,6 +25,16 @@ struct Ws {
     double* q = nullptr;     // complex ncv x ncv (V*Q, eupd)
     double* host = nullptr;  // pinned
     double* scratch = nullptr;  // ncv > 64: nblk * kB * ncv complex (k_zgemm_generic)
+    // device-resident Arnoldi step (zstep.hip, bmat = 'I'): the decisions'
+    // state, the coefficient vectors (3 x cstride complex: CGS, DGKS-1, DGKS-2
+    // -- slot 0 also stages the host-driven update's h), the recorded columns
+    // h(1:j,j) (hld = ncv) and the subdiagonals h(j,j-1) per step
+    dev::LzState* st = nullptr;
+    dev::LzState* st_host = nullptr;  // pinned mirror
+    int cstride = 0;
+    double* hcol = nullptr;  // ncv x ncv complex
+    int hld = 0;
+    double* rec = nullptr;   // ncv + 1
 };
 struct ZCsr {
     int64_t n = 0, nnz = 0;
@@ -57,6 +67,20 @@ void axpby(const Ws& ws, int64_t n, std::complex<double> a, R* y, std::complex<d
 template <class R>
 void ger(const Ws& ws, int64_t n, int k, const R* x, const std::complex<double>* w, R* Z,
          int64_t ldz);
+// device-resident step (zstep.hip): v_j = r/rnorm (+ copy), partials of
+// [V(:,0:j)^H u ; u^H u], r = rin - V coef[which] (+ partials of [V^H r ; r^H r]),
+// the single-block finalize of m complex slots, r = 0 if st.zero
+template <class R>
+void step_place(const Ws& ws, int64_t n, const R* r, R* vcol, R* copy1, R* copy2, double safmin,
+                int j);
+template <class R>
+void step_dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, int gate);
+template <class R>
+void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
+                 R* rout, bool spec, int gate);
+void step_finalize(const Ws& ws, int m, dev::FinPhase ph, int j, int rstart, int gate);
+template <class R>
+void step_zero_if(const Ws& ws, int64_t n, R* r);
 void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
 int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift);
 }  // namespace zdev
@@ -100,6 +124,11 @@ private:
     R* wd(int64_t off) { return a.d_workd + 2 * off; }           // complex offset
     int64_t ldc() const { return a.d_ld / 2; }                    // ld in complex units
     double cnorm(const R* x);                                     // dznrm2 on device
+    // device-resident step path (bmat = 'I', zstep.hip)
+    Task naitr_dev(int k, int npk, int& iinfo);
+    void dgks2_tail(int j, int rstart);
+    void read_state();
+    void write_state();
 };
 using ZSolver = ZSolverT<double>;
 

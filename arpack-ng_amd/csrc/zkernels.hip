@@ -4,53 +4,25 @@
 //   zdots   partial sums of V(:,c0:c0+8)^H u, 8 columns per pass over u
 //   zupdate r = w - V h
 //   zgemm   Z = V(:,0:k) M (row-local, alias-safe): znapps V*Q, zneupd
-//   zcsr    y = A x, one wavefront per row
+//   zcsr    y = A x, one wavefront per row (measured against 4..32 lanes per row
+//           on the config-5 operator: 0.64 ms vs 0.67-0.73 -- the random x
+//           gathers, not idle lanes, bound it)
 // Reductions are two-stage and fixed-order (bitwise reproducible).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "../../include/arpack_hip.h"
+#include "zcommon.hpp"
 #include "zengine.hpp"
 
 namespace ahip::zdev {
 
 namespace {
-constexpr int kB = 256;
-
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {  // conj(a) * b
-    return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
-}
-
-// storage of one complex element: double2 (complex128, z*) or float2
-// (complex64, c*); arithmetic is always complex128
-template <class R>
-struct C2;
-template <>
-struct C2<double> {
-    using T = double2;
-};
-template <>
-struct C2<float> {
-    using T = float2;
-};
-__device__ __forceinline__ double2 d2(double2 v) { return v; }
-__device__ __forceinline__ double2 d2(float2 v) { return make_double2(v.x, v.y); }
-template <class R>
-__device__ __forceinline__ typename C2<R>::T st2(double2 v) {
-    if constexpr (std::is_same_v<R, double>) return v;
-    else return make_float2((float)v.x, (float)v.y);
-}
-
+using namespace zc;
 // part layout: part[slot * nblk + block]; slot 2c = Re, 2c+1 = Im of column c0+c
 template <class R, int C>
 __global__ __launch_bounds__(kB) void k_zdots(int64_t n, int c0, int cnt,
@@ -432,7 +404,19 @@ static hipError_t ws_alloc(Ws& ws, int64_t n, int ncv, hipStream_t s) {
     hipError_t e;
     if ((e = hipMalloc(&ws.part, sizeof(double) * (size_t)ws.nblk * slots))) return e;
     if ((e = hipMalloc(&ws.sums, sizeof(double) * slots))) return e;
-    if ((e = hipMalloc(&ws.coef, sizeof(double) * slots))) return e;
+    ws.cstride = ncv + 2;
+    if ((e = hipMalloc(&ws.coef, sizeof(double) * 2 * 3 * (size_t)ws.cstride))) return e;
+    ws.hld = ncv;
+    if ((e = hipMalloc(&ws.hcol, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
+    if ((e = hipMalloc(&ws.rec, sizeof(double) * (size_t)(ncv + 1)))) return e;
+    if ((e = hipMalloc(&ws.st, sizeof(dev::LzState)))) return e;
+    if ((e = hipHostMalloc(&ws.st_host, sizeof(dev::LzState)))) return e;
+    memset(ws.st_host, 0, sizeof(dev::LzState));
+    {   // test hook, as the real engine's (AHIP_FORCE_DGKS2=1)
+        const char* f = getenv("AHIP_FORCE_DGKS2");
+        ws.st_host->force_dgks2 = (f && f[0] == '1') ? 1 : 0;
+    }
+    (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, s);
     if ((e = hipMalloc(&ws.q, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
     if ((e = hipHostMalloc(&ws.host, sizeof(double) * slots))) return e;
     if (ncv > 64 &&  // per-thread output columns of k_zgemm_generic
@@ -448,6 +432,10 @@ void ws_destroy(Ws& ws) {
     if (ws.q) (void)hipFree(ws.q);
     if (ws.host) (void)hipHostFree(ws.host);
     if (ws.scratch) (void)hipFree(ws.scratch);
+    if (ws.hcol) (void)hipFree(ws.hcol);
+    if (ws.rec) (void)hipFree(ws.rec);
+    if (ws.st) (void)hipFree(ws.st);
+    if (ws.st_host) (void)hipHostFree(ws.st_host);
     ws = Ws{};
 }
 

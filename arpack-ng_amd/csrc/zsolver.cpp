@@ -113,7 +113,139 @@ Task ZSolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
     co_return;
 }
 
-// znaitr: extend a k-step Arnoldi factorization to k+npk steps (host-driven).
+template <class R>
+void ZSolverT<R>::read_state() {
+    (void)hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream);
+    a.sync();
+}
+
+template <class R>
+void ZSolverT<R>::write_state() {
+    (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream);
+}
+
+// The second DGKS sweep of step j (SRC/znaitr.f:730-780, gated on the device
+// decision), its finalize, and the give-up zeroing of r.
+template <class R>
+void ZSolverT<R>::dgks2_tail(int j, int rstart) {
+    zdev::step_update(ws, (int64_t)n, j, a.d_v, ldc(), 2, a.d_resid, a.d_resid, true, 2);
+    zdev::step_finalize(ws, j + 1, dev::kFinDgks2, j, rstart, 2);
+    zdev::step_zero_if(ws, (int64_t)n, a.d_resid);
+}
+
+// znaitr for bmat = 'I' with the device-resident step (zstep.hip): every
+// reduction and 0.717 decision stays on the device; the free-running form
+// (OP = a device complex CSR) enqueues the whole extension and reads the state
+// once, the RCI form once per step (where it returns to the caller anyway).  A
+// second DGKS sweep in the free-running form parks the rest of the extension
+// (st.abort = 2) and is finished here, as in the real engine.
+template <class R>
+Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
+    const int64_t nn = n;
+    const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
+    const int ldh = ncv;
+    cd* h = workl + ih;
+    const bool free_run = csr != nullptr;
+    iinfo = 0;
+    dev::LzState& sh = *ws.st_host;
+    sh.rnorm = rnorm;  // the host's rnorm (zgetv0, or after znapps) seeds the state
+    sh.abort = 0;
+    sh.dgks = 0;
+    sh.zero = 0;
+    write_state();
+    bool restart_pending = !(rnorm > 0.0);
+    int rstart_j = -1;
+    int j = k + 1;
+    for (;;) {
+        while (j <= k + npk) {
+            int rstart = 0;
+            if (restart_pending) {  // restart with a vector orthogonal to V (znaitr.f:373-422)
+                g_stats.nrstrt += 1;
+                int itry = 1, ierr = 0;
+                for (;;) {
+                    co_await getv0(false, j, itry, ierr);
+                    if (ierr >= 0) break;
+                    if (++itry <= 3) continue;
+                    iinfo = j - 1;
+                    co_return;
+                }
+                restart_pending = false;
+                rstart = 1;
+                rstart_j = j;
+                sh.abort = 0;
+                sh.rnorm = rnorm;
+                write_state();
+            }
+            // v_j = r / rnorm; the OP input workd(ivj) and, as the reference keeps
+            // it, workd(ipj) = B v_j = v_j (znaitr.f:453-476)
+            zdev::step_place(ws, nn, a.d_resid, col(j), wd(ivj), free_run ? nullptr : wd(ipj),
+                             Prec<R>::safmin, j);
+            g_stats.nopx += 1;
+            co_await op(1, ivj, irj, ipj);
+            const R* w = wd(irj);
+            // h(1:j,j) = V^H w, wnorm (znaitr.f:545-577)
+            zdev::step_dots(ws, nn, j, a.d_v, ldc(), w, -1);
+            zdev::step_finalize(ws, j + 1, dev::kFinCgs, j, rstart, -1);
+            // r = w - V h with the partials of [V^H r ; r^H r] (znaitr.f:585-640)
+            zdev::step_update(ws, nn, j, a.d_v, ldc(), 0, w, a.d_resid, true, -1);
+            zdev::step_finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+            // DGKS sweeps, each gated on the device decision (znaitr.f:651-780)
+            zdev::step_update(ws, nn, j, a.d_v, ldc(), 1, a.d_resid, a.d_resid, true, 1);
+            const bool lazy = free_run;
+            zdev::step_finalize(ws, j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
+            if (!lazy) dgks2_tail(j, rstart);
+            ++j;
+            if (!free_run) {
+                read_state();
+                rnorm = sh.rnorm;
+                if (!(rnorm > 0.0)) restart_pending = true;
+            }
+        }
+        read_state();
+        if (sh.abort == 2) {  // step abort_j needs its second DGKS sweep
+            const int ja = sh.abort_j;
+            g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
+            sh.abort = 0;
+            write_state();
+            dgks2_tail(ja, ja == rstart_j ? 1 : 0);
+            j = ja + 1;
+            continue;
+        }
+        if (sh.abort) {  // rnorm == 0 at step abort_j: restart there
+            const int ja = sh.abort_j;
+            g_stats.nopx -= (k + npk) - ja + 1;
+            j = ja;
+            restart_pending = true;
+            continue;
+        }
+        break;
+    }
+    rnorm = sh.rnorm;
+    g_stats.nrorth += sh.nrorth;
+    g_stats.nitref += sh.nitref;
+    sh.nrorth = sh.nitref = 0;
+    write_state();
+    // H(:, k+1 : k+npk) from the device records: h(1:j,j) and h(j,j-1)
+    {
+        std::vector<cd> hc((size_t)ncv * npk);
+        std::vector<double> beta((size_t)(k + npk));
+        (void)hipMemcpyAsync(hc.data(), ws.hcol + 2 * (size_t)k * ncv, sizeof(cd) * hc.size(),
+                             hipMemcpyDeviceToHost, a.stream);
+        (void)hipMemcpyAsync(beta.data(), ws.rec, sizeof(double) * beta.size(), hipMemcpyDeviceToHost,
+                             a.stream);
+        a.sync();
+        for (int jj = k + 1; jj <= k + npk; ++jj) {
+            cd* colh = h + (size_t)(jj - 1) * ldh;
+            std::memcpy(static_cast<void*>(colh), hc.data() + (size_t)(jj - 1 - k) * ncv,
+                        sizeof(cd) * jj);
+            if (jj > 1) h[(jj - 1) + (size_t)(jj - 2) * ldh] = cd(beta[jj - 1], 0.0);
+        }
+    }
+    co_return;
+}
+
+// znaitr: extend a k-step Arnoldi factorization to k+npk steps (host-driven
+// decisions: bmat = 'G', where every B*r is a reverse-communication request).
 template <class R>
 Task ZSolverT<R>::naitr(int k, int npk, int& iinfo) {
     const int64_t nn = n;
@@ -123,6 +255,14 @@ Task ZSolverT<R>::naitr(int k, int npk, int& iinfo) {
     const double unfl = Prec<R>::safmin;
     iinfo = 0;
     std::vector<cd> c(ncv + 1);
+    static const bool dev_steps = [] {  // AHIP_ZHOST=1: the host-driven step for bmat = 'I' too
+        const char* e = getenv("AHIP_ZHOST");
+        return !(e && e[0] == '1');
+    }();
+    if (bmat == 'I' && dev_steps) {
+        co_await naitr_dev(k, npk, iinfo);
+        if (iinfo > 0) co_return;
+    } else
     for (int j = k + 1; j <= k + npk; ++j) {
         double betaj = rnorm;
         if (!(rnorm > 0.0)) {  // restart with a vector orthogonal to V (SRC/znaitr.f:373-422)
