@@ -250,12 +250,17 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
-            dev::prof_begin(dev::kProfSpmv, S->a.stream);
+            // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
+            // it); a row-distributed SpMV also holds its halo exchange: marker mode
+            const double by = dev::csr_bytes(*S->csr);
+            if (S->dist) dev::prof_begin(dev::kProfSpmv, S->a.stream);
+            else dev::prof_arm(dev::kProfSpmv);
             if constexpr (!kShadow) {
                 if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
                 else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
             }
-            dev::prof_end(dev::kProfSpmv, S->a.stream, dev::csr_bytes(*S->csr));
+            if (S->dist) dev::prof_end(dev::kProfSpmv, S->a.stream, by);
+            else dev::prof_disarm(dev::kProfSpmv, by);
             continue;
         }
         if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park

@@ -207,7 +207,12 @@ struct Csr {
     const int32_t* ss_row = nullptr;       // 64 per slice, -1 = padding lane
     const double* ss_val = nullptr;
     const uint16_t* ss_colw = nullptr;     // col - r0 (16 bit)
-    double* ss_lo = nullptr;               // spill partials (written by superblock b-1)
+    // balanced walk: superblock b's slices flattened into column steps and cut
+    // into one contiguous step range per wave: range (b, q) starts at step
+    // ss_wg0[b * 16 + q] (nsb * 16 + 1 entries) inside slice ss_wsl[b * 16 + q]
+    const int64_t* ss_wg0 = nullptr;
+    const int32_t* ss_wsl = nullptr;
+    double* ss_lo = nullptr;              // spill partials (written by superblock b-1)
     double* ss_hi = nullptr;               // prefix partials (written by superblock b)
     int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;
     int ss_variant = 0;                    // kernel variant (tools/spmv_sym_time.py)
@@ -279,8 +284,31 @@ struct ProfStat {
 };
 void prof_enable(bool on);
 bool prof_on();
+// Marker mode: an event pair recorded on the stream around the span (used
+// where the span holds more than kernels, e.g. a row-distributed SpMV's halo
+// exchange).
 void prof_begin(ProfClass c, hipStream_t s);
 void prof_end(ProfClass c, hipStream_t s, double bytes);
+// Kernel mode: the span's launches go through AHIP_LAUNCH, which attaches the
+// start event to the first kernel's dispatch and the stop event to the last
+// one's (hipExtLaunchKernel), so the measured time is the kernels' own
+// execution -- what rocprofv3's kernel trace reports -- without marker packets
+// between the launches.  Nested spans are counted in the outermost one.
+void prof_arm(ProfClass c);
+void prof_disarm(ProfClass c, double bytes);
+bool prof_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 void prof_collect(ProfStat out[kProfClasses]);  // synchronises, returns and resets
 
 }  // namespace ahip::dev
+
+#include <hip/hip_ext.h>
+// hipLaunchKernelGGL, or hipExtLaunchKernelGGL with the profiler's events when
+// a kernel-mode span is open (see prof_arm)
+#define AHIP_LAUNCH(K, G, B, SH, S, ...)                                                        \
+    do {                                                                                       \
+        hipEvent_t ahip_ev0_, ahip_ev1_;                                                       \
+        if (::ahip::dev::prof_kernel_events(&ahip_ev0_, &ahip_ev1_))                           \
+            hipExtLaunchKernelGGL(K, G, B, SH, S, ahip_ev0_, ahip_ev1_, 0, __VA_ARGS__);       \
+        else                                                                                   \
+            hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                   \
+    } while (0)

@@ -792,12 +792,12 @@ void ws_destroy(Workspace& ws) {
 }
 
 namespace {
-struct ProfScope {  // event pair around one launch when profiling is on
+struct ProfScope {  // kernel-mode span (prof_arm) around one launcher when profiling is on
     ProfClass c;
     hipStream_t s;
     double bytes;
-    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_begin(c, s); }
-    ~ProfScope() { prof_end(c, s, bytes); }
+    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_arm(c); }
+    ~ProfScope() { prof_disarm(c, bytes); }
 };
 }  // namespace
 
@@ -822,7 +822,7 @@ template <class R>
 void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc, int j) {
     ProfScope ps(kProfPlace, ws.stream,
                  (double)sizeof(R) * n * (2 + (copy1 != nullptr) + 2 * (sc != nullptr)));
-    hipLaunchKernelGGL(k_place<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
+    AHIP_LAUNCH(k_place<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
                        sc, ws.st, j);
 }
 
@@ -839,12 +839,12 @@ static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R*
     const dim3 g(ws.nblk), b(kBlock);
     switch (jc) {
         case 0:
-            hipLaunchKernelGGL((k_dots<R, 0, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,
+            AHIP_LAUNCH((k_dots<R, 0, WM>), g, b, 0, ws.stream, n, j0, V, ld, u, w, ws.part,
                                ws.stride, wslot, ws.st, gate);
             break;
 #define AHIP_DOTS_CASE(J)                                                                          \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_dots<R, J, WM, POL>), g, b, 0, ws.stream, n, j0, V, ld, u, w,        \
+        AHIP_LAUNCH((k_dots<R, J, WM, POL>), g, b, 0, ws.stream, n, j0, V, ld, u, w,        \
                            ws.part, ws.stride, wslot, ws.st, gate);                                \
         break;
         AHIP_CASES_1_32(AHIP_DOTS_CASE)
@@ -892,7 +892,7 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
     // in-flight loads per wave (64 column loads per row at J = 64)
     if (j >= 1 && j <= 64) {
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, g, b, 0, ws.stream, n, Vw, ld, c, rin, rout, part, ws.stride,
+            AHIP_LAUNCH(kern, g, b, 0, ws.stream, n, Vw, ld, c, rin, rout, part, ws.stride,
                                ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2);
         };
         switch (j) {
@@ -909,7 +909,7 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
             default: break;
         }
     } else {  // (chained steps run only with ncv <= 64: the solver's choice)
-        hipLaunchKernelGGL(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
+        AHIP_LAUNCH(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
                            gate);
         if (spec) dots<R>(ws, n, j, V, ld, rout, rout, gate);
     }
@@ -926,7 +926,7 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
     const double* part2 = ws.part + (size_t)ws.nblk * ws.stride;  // region 2 (chained steps)
     const size_t lds = sizeof(double) * (size_t)(m + m2);  // s_sum (m + m2 <= 2 kMaxNcv + 4)
     auto fin = [&](int fs) {
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, fs, m,
+        AHIP_LAUNCH(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, fs, m,
                            (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st,
                            ws.hcol, ws.hld, part2, m2, rstart_prev);
     };
@@ -937,10 +937,10 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
     if (!from_sums) {
         // stage 2a: one workgroup per slot sums that slot's nblk partials (coalesced;
         // region 2 follows region 1 in memory only when m == stride -- so two launches)
-        hipLaunchKernelGGL(k_reduce_slots, dim3(m), dim3(256), 0, ws.stream, ws.part, ws.nblk, ws.sums,
+        AHIP_LAUNCH(k_reduce_slots, dim3(m), dim3(256), 0, ws.stream, ws.part, ws.nblk, ws.sums,
                            ws.st, gate);
         if (m2)
-            hipLaunchKernelGGL(k_reduce_slots, dim3(m2), dim3(256), 0, ws.stream, part2, ws.nblk,
+            AHIP_LAUNCH(k_reduce_slots, dim3(m2), dim3(256), 0, ws.stream, part2, ws.nblk,
                                ws.sums + m, ws.st, gate);
     }
     // stage 2b: the phase logic on the m + m2 sums (one small workgroup)
@@ -950,7 +950,7 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
 template <class R>
 void zero_if(const Workspace& ws, int64_t n, R* r) {
     ProfScope ps(kProfOther, ws.stream, 0.0);
-    hipLaunchKernelGGL(k_zero_if<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
+    AHIP_LAUNCH(k_zero_if<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, ws.st);
 }
 
 template <class R>
@@ -960,14 +960,14 @@ void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int
     ProfScope ps(kProfVq, ws.stream,
                  (double)sizeof(R) * n * (kplusp + kev + (betak > 0.0) + 2));
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev, ws.q,
+        AHIP_LAUNCH(kern, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev, ws.q,
                            kplusp, sigmak, betak, r, ws.part, ws.stride);
     };
     if (kplusp <= 16) ws.v_plain ? go(k_vq_update<R, 16, kPolPlain>) : go(k_vq_update<R, 16>);
     else if (kplusp <= 32) ws.v_plain ? go(k_vq_update<R, 32, kPolPlain>) : go(k_vq_update<R, 32>);
     else if (kplusp <= 64) ws.v_plain ? go(k_vq_update<R, 64, kPolPlain>) : go(k_vq_update<R, 64>);
     else  // ws.scratch: nblk * kBlock * (ncv + 1) doubles, allocated by ws_create for ncv > 64
-        hipLaunchKernelGGL(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
+        AHIP_LAUNCH(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
                            kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.scratch, ws.part,
                            ws.stride);
 }
@@ -977,25 +977,25 @@ void vq_gemm(const Workspace& ws, int64_t n, const R* V, int64_t ld, int k, int 
              int64_t ldz) {
     const int g = grid_for(n);
     if (k <= 16)
-        hipLaunchKernelGGL((k_vq_gemm<R, 16>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+        AHIP_LAUNCH((k_vq_gemm<R, 16>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
     else if (k <= 32)
-        hipLaunchKernelGGL((k_vq_gemm<R, 32>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+        AHIP_LAUNCH((k_vq_gemm<R, 32>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
     else if (k <= 64)
-        hipLaunchKernelGGL((k_vq_gemm<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+        AHIP_LAUNCH((k_vq_gemm<R, 64>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
     else if (k <= 128)
-        hipLaunchKernelGGL((k_vq_gemm<R, 128>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
+        AHIP_LAUNCH((k_vq_gemm<R, 128>), dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, k, nz,
                            ws.q, Z, ldz);
     else  // grid = nblk: the scratch holds nblk * kBlock rows of ncv + 1 outputs
-        hipLaunchKernelGGL(k_vq_gemm_generic<R>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, V, ld,
+        AHIP_LAUNCH(k_vq_gemm_generic<R>, dim3(ws.nblk), dim3(kBlock), 0, ws.stream, n, V, ld,
                            k, nz, ws.q, Z, ldz, ws.scratch);
 }
 
 uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, double* x,
                        int64_t offset, int) {
-    hipLaunchKernelGGL(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x);
+    AHIP_LAUNCH(k_larnv, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48, offset, x);
     return lcg_pow(seed48, (uint64_t)n);
 }
 
@@ -1034,7 +1034,7 @@ uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x
     bool redraw = true;  // no flag memory: take the sequential path
     if (flag) {
         *flag = ~0ull;  // pinned host memory, visible to the kernel
-        hipLaunchKernelGGL(k_larnv_f, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48,
+        AHIP_LAUNCH(k_larnv_f, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, seed48,
                            offset, x, flag);
         (void)hipStreamSynchronize(ws.stream);
         redraw = (*flag != ~0ull);
@@ -1051,24 +1051,24 @@ uint64_t larnv_uniform(const Workspace& ws, int64_t n, uint64_t seed48, float* x
 
 template <class R>
 void copy(hipStream_t s, int64_t n, const R* src, R* dst) {
-    hipLaunchKernelGGL(k_copy<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, src, dst);
+    AHIP_LAUNCH(k_copy<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, src, dst);
 }
 template <class R>
 void scal(hipStream_t s, int64_t n, double a, R* x) {
-    hipLaunchKernelGGL(k_scal<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+    AHIP_LAUNCH(k_scal<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
 }
 template <class R>
 void fill(hipStream_t s, int64_t n, double a, R* x) {
-    hipLaunchKernelGGL(k_fill<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
+    AHIP_LAUNCH(k_fill<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x);
 }
 template <class R>
 void axpby(hipStream_t s, int64_t n, double alpha, R* y, double beta, const R* x) {
-    hipLaunchKernelGGL(k_axpby<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, alpha, y, beta, x);
+    AHIP_LAUNCH(k_axpby<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, alpha, y, beta, x);
 }
 
 template <class R>
 void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z, int64_t ldz) {
-    hipLaunchKernelGGL(k_ger_cols<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
+    AHIP_LAUNCH(k_ger_cols<R>, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, x, w, Z, ldz);
 }
 
 #define AHIP_INST(R)                                                                               \

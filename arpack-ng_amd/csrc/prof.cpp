@@ -20,6 +20,10 @@ std::vector<hipEvent_t> g_pool;
 std::vector<Pending> g_pending;
 hipEvent_t g_open[kProfClasses] = {};
 ProfStat g_acc[kProfClasses];
+// kernel mode: the open span (one at a time; nested spans count in the outer)
+int g_arm = -1, g_depth = 0;
+hipEvent_t g_kstart = nullptr, g_kstop = nullptr;
+std::vector<hipEvent_t> g_retire;  // stop events superseded by a later launch
 
 hipEvent_t take() {
     if (!g_pool.empty()) {
@@ -45,6 +49,11 @@ void drain_locked() {
         g_pool.push_back(p.b);
     }
     g_pending.clear();
+    for (hipEvent_t e : g_retire) {
+        (void)hipEventSynchronize(e);
+        g_pool.push_back(e);
+    }
+    g_retire.clear();
 }
 }  // namespace
 
@@ -72,6 +81,42 @@ void prof_end(ProfClass c, hipStream_t s, double bytes) {
     (void)hipEventRecord(e, s);
     g_pending.push_back(Pending{c, g_open[c], e, bytes});
     g_open[c] = nullptr;
+}
+
+void prof_arm(ProfClass c) {
+    if (!g_on) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_arm >= 0) {
+        ++g_depth;
+        return;
+    }
+    if (g_pending.size() > 4096) drain_locked();
+    g_arm = c;
+    g_kstart = g_kstop = nullptr;
+}
+
+void prof_disarm(ProfClass c, double bytes) {
+    if (!g_on) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_depth > 0) {
+        --g_depth;
+        return;
+    }
+    if (g_arm != c) return;
+    if (g_kstart && g_kstop) g_pending.push_back(Pending{c, g_kstart, g_kstop, bytes});
+    g_arm = -1;
+    g_kstart = g_kstop = nullptr;
+}
+
+bool prof_kernel_events(hipEvent_t* start, hipEvent_t* stop) {
+    *start = *stop = nullptr;
+    if (!g_on) return false;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_arm < 0) return false;
+    if (!g_kstart) *start = g_kstart = take();
+    if (g_kstop) g_retire.push_back(g_kstop);
+    *stop = g_kstop = take();
+    return true;
 }
 
 void prof_collect(ProfStat out[kProfClasses]) {

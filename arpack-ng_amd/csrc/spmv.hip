@@ -574,7 +574,7 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     if (hipMalloc(&dmn, sizeof(int32_t) * n) || hipMalloc(&dmx, sizeof(int32_t) * n)) return -2;
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(k_row_span, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dmn, dmx);
+    AHIP_LAUNCH(k_row_span, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dmn, dmx);
     (void)hipMemcpy(mn.data(), dmn, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
     (void)hipMemcpy(mx.data(), dmx, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
     (void)hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
@@ -638,7 +638,7 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     // 16-bit window-relative column indices (one per nonzero)
     uint16_t* cw = nullptr;
     if (A.nnz > 0 && hipMalloc(&cw, sizeof(uint16_t) * A.nnz) == hipSuccess) {
-        hipLaunchKernelGGL(k_colw, dim3((unsigned)nsb), dim3(256), 0, nullptr, A.w_sb_tile0, A.w_tiles,
+        AHIP_LAUNCH(k_colw, dim3((unsigned)nsb), dim3(256), 0, nullptr, A.w_sb_tile0, A.w_tiles,
                            A.w_sb_c0, A.rowptr, A.col, cw);
         (void)hipDeviceSynchronize();
         A.w_colw = cw;
@@ -696,7 +696,7 @@ int csr_build_sell(Csr& A, void** owned) {
     (void)hipMemcpy(d1, sptr.data(), b1, hipMemcpyHostToDevice);
     (void)hipMemcpy(d2, srow.data(), b2, hipMemcpyHostToDevice);
     if (ns > 0)
-        hipLaunchKernelGGL(k_sell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d1, d2, A.rowptr,
+        AHIP_LAUNCH(k_sell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d1, d2, A.rowptr,
                            A.w_colw, A.val, dc, dv);
     if (hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(d);
@@ -765,7 +765,7 @@ static void launch_wvec1(hipStream_t s, const Csr& A, const double* x, double* y
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((k_csr_wvec<L, U, NT, CW, XCD>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+    AHIP_LAUNCH((k_csr_wvec<L, U, NT, CW, XCD>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
                        A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.w_colw,
                        A.val, x, y);
 }
@@ -789,7 +789,7 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
-            hipLaunchKernelGGL(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
+            AHIP_LAUNCH(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
                                A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y);
         };
         if (A.s_unroll == 4) go(k_csr_sell<4, true>);
@@ -820,7 +820,7 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
         const double avg = A.n > 0 ? (double)A.nnz / (double)A.n : 1.0;
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.w_sb_tile0, A.w_tiles,
+            AHIP_LAUNCH(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.w_sb_tile0, A.w_tiles,
                                A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.w_colw, A.val, x, y);
         };
         const bool p4 = A.kernel == kCsrWVecP4;
@@ -848,10 +848,10 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
             attr = true;
         }
         if (A.kernel == kCsrWindowNT)
-            hipLaunchKernelGGL((k_csr_window<true>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+            AHIP_LAUNCH((k_csr_window<true>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
                                A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.val, x, y);
         else
-            hipLaunchKernelGGL((k_csr_window<false>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+            AHIP_LAUNCH((k_csr_window<false>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
                                A.w_sb_tile0, A.w_tiles, A.w_sb_c0, A.w_sb_span, A.rowptr, A.col, A.val, x, y);
         return;
     }
@@ -859,11 +859,11 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
         const dim3 g((unsigned)A.nrblk), b(kBlock);
         const bool nt = A.kernel == kCsrStreamNT;
         if (A.tile == 2048) {
-            if (nt) hipLaunchKernelGGL((k_csr_stream<2048, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
-            else hipLaunchKernelGGL((k_csr_stream<2048, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            if (nt) AHIP_LAUNCH((k_csr_stream<2048, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            else AHIP_LAUNCH((k_csr_stream<2048, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
         } else {
-            if (nt) hipLaunchKernelGGL((k_csr_stream<4096, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
-            else hipLaunchKernelGGL((k_csr_stream<4096, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            if (nt) AHIP_LAUNCH((k_csr_stream<4096, true>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
+            else AHIP_LAUNCH((k_csr_stream<4096, false>), g, b, 0, s, A.rblk, A.rowptr, A.col, A.val, x, y);
         }
         return;
     }
@@ -873,11 +873,11 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
     if (g > 65536) g = 65536;
     if (g < 1) g = 1;
     switch (G) {
-        case 4: hipLaunchKernelGGL(k_csr_vector<4>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 8: hipLaunchKernelGGL(k_csr_vector<8>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 16: hipLaunchKernelGGL(k_csr_vector<16>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        case 32: hipLaunchKernelGGL(k_csr_vector<32>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
-        default: hipLaunchKernelGGL(k_csr_vector<64>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 4: AHIP_LAUNCH(k_csr_vector<4>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 8: AHIP_LAUNCH(k_csr_vector<8>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 16: AHIP_LAUNCH(k_csr_vector<16>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        case 32: AHIP_LAUNCH(k_csr_vector<32>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
+        default: AHIP_LAUNCH(k_csr_vector<64>, dim3(g), dim3(kBlock), 0, s, A.n, A.rowptr, A.col, A.val, x, y); break;
     }
 }
 
@@ -920,9 +920,9 @@ extern "C" double arpack_hip_stream_probe(int64_t nbytes, int width, int grid, i
     const int64_t n8 = nbytes / 8;
     auto launch = [&]() {
         if (width == 16)
-            hipLaunchKernelGGL(ahip::dev::k_probe<16>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
+            AHIP_LAUNCH(ahip::dev::k_probe<16>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
         else
-            hipLaunchKernelGGL(ahip::dev::k_probe<8>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
+            AHIP_LAUNCH(ahip::dev::k_probe<8>, dim3(grid), dim3(256), 0, nullptr, n8, a, o);
     };
     launch();
     (void)hipEventRecord(e0, nullptr);

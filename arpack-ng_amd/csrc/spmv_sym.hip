@@ -232,6 +232,144 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     }
 }
 
+// The same chained walk with the superblock's work cut evenly over its waves.
+// Above, wave q takes slices q, q + 16, ...: a superblock of ~77 slices gives 13
+// waves five slices and three waves four, and every wave then idles at the
+// barrier until the five-slice waves finish.  Here the superblock's slices are
+// flattened into their column steps (sptr / 64: a slice of width w is w steps)
+// and wave q takes the contiguous steps [wg0[b*16+q], wg0[b*16+q+1]) -- equal
+// counts to within one step, and one contiguous val / col stream per wave.  A
+// range may start or end inside a slice, so a row can receive its upper-row
+// sum from two waves (both LDS atomic adds, like the transposed terms).
+template <int U, bool NT>
+__global__ __launch_bounds__(kSymThreads) void k_csr_ssell_bal(
+    const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
+    const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
+    const int64_t* __restrict__ wg0, const int32_t* __restrict__ wsl,
+    const int64_t* __restrict__ sptr, const int32_t* __restrict__ srow,
+    const uint16_t* __restrict__ scolw, const double* __restrict__ sval,
+    const double* __restrict__ x, double* __restrict__ y, double* __restrict__ slot_lo,
+    double* __restrict__ slot_hi, int64_t coff, int chain, int64_t nsb) {
+    __shared__ double xw[kSymWin];
+    __shared__ double yw[kSymWin];
+    constexpr int NW = kSymThreads / 64;
+    // wave-uniform: the unit bookkeeping below lives in scalar registers
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
+    struct Chunk {
+        double v[U];
+        int c[U];
+    };
+    // a unit: steps [k, khi) of slice s (element offset base); khi < 0 = none
+    struct Unit {
+        int64_t s, base, g1;
+        int k, khi;
+    };
+    auto load = [&](Chunk& c, int64_t base, int khi, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < khi;
+            c.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
+            c.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
+        }
+    };
+    auto first = [&](int64_t b, Unit& q) {  // this wave's first unit in superblock b
+        const int64_t g0 = wg0[b * NW + wave];
+        q.g1 = wg0[b * NW + wave + 1];
+        q.s = wsl[b * NW + wave];
+        q.base = sptr[q.s];
+        const int64_t st = q.base >> 6, w = (sptr[q.s + 1] - q.base) >> 6;
+        q.k = (int)(g0 - st);
+        q.khi = g0 < q.g1 ? (int)min(w, q.g1 - st) : -1;
+    };
+    auto advance = [&](const Unit& q, Unit& nq) {  // the next slice of the same range
+        if ((q.base >> 6) + q.khi >= q.g1) return false;
+        nq.s = q.s + 1;
+        nq.g1 = q.g1;
+        nq.base = sptr[nq.s];
+        const int64_t w = (sptr[nq.s + 1] - nq.base) >> 6;
+        nq.k = 0;
+        nq.khi = (int)min(w, q.g1 - (nq.base >> 6));
+        return true;
+    };
+    Chunk cur, nxt;
+    Unit u;
+    first(b0, u);
+    if (u.khi >= 0) load(cur, u.base, u.khi, u.k);
+    int R_prev = 0, span_prev = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+        const int64_t r0 = sb_r0[b];
+        const int R = (int)(sb_r0[b + 1] - r0);
+        const int span = sb_span[b];
+        int carry = 0;
+        if (b > b0) {  // the previous window's tail [R_prev, span_prev) becomes this head
+            carry = span_prev - R_prev;
+            __syncthreads();
+            for (int i = t; i < carry; i += kSymThreads) {
+                xw[i] = xw[R_prev + i];
+                yw[i] = yw[R_prev + i];
+            }
+            __syncthreads();
+        }
+        for (int i = carry + t; i < span; i += kSymThreads) {
+            xw[i] = x[coff + r0 + i];
+            yw[i] = 0.0;
+        }
+        __syncthreads();
+        // `u` (first chunk in `cur`) is this wave's first unit of superblock b
+        if (u.khi >= 0) {
+            bool more;
+            do {
+                const int row = srow[u.s * 64 + lane];
+                const int rl = row >= 0 ? row - (int)r0 : 0;
+                const double xi = xw[rl];
+                Unit nu;
+                more = advance(u, nu);
+                if (!more) {
+                    if (b + 1 < b1) first(b + 1, nu);
+                    else nu.khi = -1;
+                }
+                double acc = 0.0;
+                int k = u.k;
+                do {
+                    if (k + U < u.khi) load(nxt, u.base, u.khi, k + U);
+                    else if (nu.khi >= 0) load(nxt, nu.base, nu.khi, nu.k);
+#pragma unroll
+                    for (int q = 0; q < U; ++q) {
+                        const int c = cur.c[q];
+                        if (c >= 0) {
+                            acc += cur.v[q] * xw[c];
+                            if (c != rl) atomicAdd(&yw[c], cur.v[q] * xi);
+                        }
+                    }
+                    cur = nxt;
+                    k += U;
+                } while (k < u.khi);
+                if (row >= 0) atomicAdd(&yw[rl], acc);
+                u = nu;
+            } while (more);
+        } else if (b + 1 < b1) {  // empty range here: set up the next superblock's
+            first(b + 1, u);
+            if (u.khi >= 0) load(cur, u.base, u.khi, u.k);
+        }
+        __syncthreads();
+        const int head = b == b0 ? sb_pre[b] : 0;
+        const int64_t off = sb_off[b];
+        for (int i = t; i < R; i += kSymThreads) {
+            const double v = yw[i];
+            if (i < head) slot_hi[off + i] = v;
+            else y[r0 + i] = v;
+        }
+        if (b == b1 - 1) {
+            const int64_t offn = sb_off[b + 1];
+            for (int i = R + t; i < span; i += kSymThreads) slot_lo[offn + (i - R)] = yw[i];
+        }
+        R_prev = R;
+        span_prev = span;
+    }
+}
+
 // y(head rows of each chain's first superblock) = lo + hi (1024 threads: a
 // head is ~4k rows, so every load of the block is in flight at once)
 __global__ __launch_bounds__(1024) void k_ssell_combine(const int64_t* __restrict__ sb_r0,
@@ -341,7 +479,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
+    AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
                        dcnt, dcm);
     std::vector<int32_t> cnt(n), cm(n);
     (void)hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
@@ -377,6 +515,23 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
         }
         slice0.push_back((int64_t)sptr.size() - 1);
     }
+    // balanced walk (k_csr_ssell_bal): wave q of superblock b takes the column
+    // steps [wg0[b*NW+q], wg0[b*NW+q+1]) of the superblock's flattened slices,
+    // starting in slice wsl[b*NW+q] (the non-empty slice holding its first step)
+    constexpr int NW = kSymThreads / 64;
+    std::vector<int64_t> wg0((size_t)nsb * NW + 1);
+    std::vector<int32_t> wsl((size_t)nsb * NW);
+    for (int64_t b = 0; b < nsb; ++b) {
+        const int64_t sa = slice0[b], sz = slice0[b + 1];
+        const int64_t G0 = sptr[sa] >> 6, T = (sptr[sz] >> 6) - G0;
+        for (int q = 0; q < NW; ++q) {
+            const int64_t g0 = G0 + T * q / NW;
+            const int64_t s = std::upper_bound(sptr.begin() + sa, sptr.begin() + sz, g0 << 6) - sptr.begin() - 1;
+            wg0[(size_t)b * NW + q] = g0;
+            wsl[(size_t)b * NW + q] = (int32_t)std::max<int64_t>(s, sa);
+        }
+    }
+    wg0[(size_t)nsb * NW] = sptr.back() >> 6;
     // slots: off[nsb] combined rows, then the outgoing spill (spill_out)
     const int64_t ns = (int64_t)sptr.size() - 1, padded = sptr.back(), ncomb = off[nsb];
     const int64_t nslot = ncomb + spill_out;
@@ -387,10 +542,11 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
                  b_row = sizeof(int32_t) * srow.size(),
                  b_val = sizeof(double) * (size_t)std::max<int64_t>(padded, 1),
                  b_cw = sizeof(uint16_t) * (size_t)std::max<int64_t>(padded, 1),
-                 b_slot = sizeof(double) * (size_t)std::max<int64_t>(nslot, 1);
+                 b_slot = sizeof(double) * (size_t)std::max<int64_t>(nslot, 1),
+                 b_wg0 = sizeof(int64_t) * wg0.size(), b_wsl = sizeof(int32_t) * wsl.size();
     char* d = nullptr;
     if (hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) + up(b_row) +
-                          up(b_val) + up(b_cw) + 2 * up(b_slot)))
+                          up(b_val) + up(b_cw) + 2 * up(b_slot) + up(b_wg0) + up(b_wsl)))
         return -2;
     char* p = d;
     auto take = [&](size_t bytes) {
@@ -409,6 +565,10 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     auto* d_cw = (uint16_t*)take(b_cw);
     auto* d_lo = (double*)take(b_slot);
     auto* d_hi = (double*)take(b_slot);
+    auto* d_wg0 = (int64_t*)take(b_wg0);
+    auto* d_wsl = (int32_t*)take(b_wsl);
+    (void)hipMemcpy(d_wg0, wg0.data(), b_wg0, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_wsl, wsl.data(), b_wsl, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_r0, r0s.data(), b_r0, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_sp, spans.data(), b_sp, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_pre, pre.data(), b_pre, hipMemcpyHostToDevice);
@@ -423,7 +583,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
             return -2;
         }
         (void)hipMemcpy(d_sr0, slice_r0.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, coff, d_ptr, d_row,
+        AHIP_LAUNCH(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, coff, d_ptr, d_row,
                            d_sr0, A.rowptr, A.col, A.val, d_cw, d_val);
     }
     // the outgoing spill's tail past the last window is never written: zero it once
@@ -445,6 +605,8 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_colw = d_cw;
     A.ss_lo = d_lo;
     A.ss_hi = d_hi;
+    A.ss_wg0 = d_wg0;
+    A.ss_wsl = d_wsl;
     A.ss_nsb = nsb;
     // chains of consecutive superblocks, one workgroup per CU (k_csr_ssell);
     // the in-LDS window shift needs span <= 2R (true for the balanced plan)
@@ -467,7 +629,7 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
     auto go = [&](auto kern) {
         const int chain = sym_chain(A);
         const int64_t nch = (A.ss_nsb + chain - 1) / chain;
-        hipLaunchKernelGGL(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
+        AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
                            A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb);
     };
@@ -477,7 +639,18 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
     // U = 2 0.671, U = 16 spills.  Diagnostic builds (wrong y, not kept):
     // without the transposed LDS adds 0.611 (U = 4), without any LDS traffic
     // 0.559 -- the slice stream, not the atomics, bounds it.
+    auto go_bal = [&](auto kern) {
+        const int chain = A.ss_chain;
+        const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+        AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
+                           A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_wg0, A.ss_wsl, A.ss_ptr,
+                           A.ss_row, A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain,
+                           A.ss_nsb);
+    };
     switch (A.ss_variant) {  // alternative unrolls for tools/spmv_sym_time.py
+        case 8: go_bal(k_csr_ssell_bal<8, true>); break;
+        case 9: go_bal(k_csr_ssell_bal<6, true>); break;
+        case 10: go_bal(k_csr_ssell_bal<12, true>); break;
         case 3: go(k_csr_ssell<8, false>); break;
         case 4: go(k_csr_ssell<4, false>); break;
         case 5: go(k_csr_ssell<6, true>); break;
@@ -490,7 +663,7 @@ void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
     if (A.ss_ncomb > 0)
-        hipLaunchKernelGGL(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
+        AHIP_LAUNCH(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
                            A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
 }
 

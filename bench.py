@@ -211,9 +211,9 @@ def main():
         del s_f
         A.set_symmetric(True)
     s, ido, elapsed, nopx, nsolves = timed_run()
-    # Per-kernel roofline: the next K cycles of the same solve with a hipEvent
-    # pair around every launch on its stream (the events cost ~7% of the cycle,
-    # so they are kept out of the timed region above); if that solve has
+    # Per-kernel roofline: the next K cycles of the same solve with hipEvents on
+    # every kernel's dispatch (start event on a span's first kernel, stop event
+    # on its last: hipExtLaunchKernel), kept out of the timed region above; if that solve has
     # finished, min(K, 10) cycles of a fresh one after its warmup.
     prof = None
     if not args.no_profile:
@@ -307,8 +307,10 @@ def main():
                                else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "
                                      "x windows, 16-bit window-relative cols, XCD-contiguous "
                                      "superblocks)"),
-                     "measured_on": "hipEvents around each launch over a second run of the same "
-                                    "K cycles (events kept out of the timed region)",
+                     "measured_on": "hipEvents attached to the SpMV kernels' own dispatches "
+                                    "(hipExtLaunchKernel start/stop: kernel execution time, as "
+                                    "rocprofv3's kernel trace measures it) over a second run of the "
+                                    "same K cycles (events kept out of the timed region)",
                      "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},

@@ -33,9 +33,10 @@ def main():
     A.set_symmetric(True)
     out["sym_ms"] = A.time_spmv(a.reps)
     A.matvec_device(x.at(0), y2.at(0))
-    for v in a.variants:
+    for i, v in enumerate(a.variants):
         A.set_kernel(12, v)
-        out["sym_v%d_ms" % v] = A.time_spmv(a.reps)
+        key = "sym_v%d_ms" % v if "sym_v%d_ms" % v not in out else "sym_v%d_ms_%d" % (v, i)
+        out[key] = A.time_spmv(a.reps)
         A.matvec_device(x.at(0), y2.at(0))
         d = np.abs(y1.numpy() - y2.numpy())
         out["sym_v%d_maxrel" % v] = float((d / np.maximum(np.abs(y1.numpy()), 1e-300)).max())
