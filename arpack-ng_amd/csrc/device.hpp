@@ -46,7 +46,8 @@ struct LzState {
     int nrorth;     // counters accumulated on device, drained by the host
     int nitref;
     int force_dgks2;  // test hook (AHIP_FORCE_DGKS2=1): always take the second refinement
-    int pad;
+    int fold;       // folded steps: step j's DGKS sweep (coef slot 1) was taken and is
+                    // applied by step j+1's passes (kFinPostCgsFold sets it)
     double vscale;  // chained steps: 1/rnorm, applied by the update pass to the raw
                     // column V(:,j) and to A*r (1.0 after a plain kFinCgs)
 };
@@ -67,6 +68,14 @@ enum FinPhase : int {
                         // on the sums of the RAW residual (v_j not yet formed):
                         // coefficients rescaled by 1/rnorm (st.vscale).  abort = 3:
                         // rnorm outside the raw-vector range, redo step j unchained
+    kFinCgsFolded = 9,  // step j of a folded cycle: as kFinCgsChained, but region 2 holds
+                        // ONE slot (r'r' of step j-1's DGKS-corrected residual, formed by
+                        // the fold pass); a needed second refinement parks with
+                        // abort = 2 and leaves the coefficients to the host
+    kFinPostCgsFold = 10,  // kFinPostCgs + t = T_j s (coef slot 3) and st.fold for the
+                           // next step's fold pass
+    kFinFoldCoef2 = 11,    // host fallback of a folded park: coef2 = V'r' sums,
+                           // h(j,2) += the last one (refine_decision's take path)
 };
 
 struct Workspace {
@@ -75,7 +84,8 @@ struct Workspace {
     int stride = 0;      // >= ncv + 2
     double* part = nullptr;   // 2 regions of nblk * stride (region 2: chained steps)
     double* sums = nullptr;   // 2 * stride (raw sums of the last finalize)
-    double* coef = nullptr;   // 3 * stride : CGS, DGKS-1, DGKS-2 coefficient vectors
+    double* coef = nullptr;   // 4 * stride : CGS, DGKS-1, DGKS-2 coefficient vectors,
+                              // t = T_j * DGKS-1 (folded steps)
     double* rec = nullptr;    // 2 * (ncv+1): alpha_j, beta_j per step
     double* q = nullptr;      // ncv * ncv  (V*Q matrix for dsapps / eupd)
     // Arnoldi (dnaitr): column j of H, h(1:j, j) = V_j' w + DGKS corrections,
@@ -117,10 +127,24 @@ void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R
 template <class R>
 struct UpdateChain {
     bool chained = false;
+    bool fold = false;  // folded step: w = A r' is rebuilt from the SpMV of the
+                        // pre-DGKS residual (k_fold_dots' expression), see fold_dots
+    int rev = -1;       // sweep direction override (-1: dir_rev's choice)
     R* raw1 = nullptr;
     R* raw2 = nullptr;
     double* part = nullptr;
 };
+// Folded Lanczos step j (free-running, dsaupd): the DGKS sweep of step j-1 is
+// applied here instead of in a pass of its own.  The SpMV ran on r (step j-1's
+// residual BEFORE its DGKS correction); with s = coef[1] (step j-1's DGKS
+// coefficients, applied only if st.fold) and t = T_{j-1} s (coef slot 3):
+//   r' = r - V(:,1:j-1) s        -> stored as the RAW column V(:,j)
+//   w  = A r - V(:,1:j-1) t - s_{j-1} r'   (= A r' by the Lanczos relation
+//        A V_{j-1} = V_{j-1} T_{j-1} + r' e', exact up to O(eps*|s|) terms)
+// and the partials of [V(:,1:j)' w ; w'w] (region 1, j+1 slots) and r''r'
+// (region 2, one slot) for kFinCgsFolded.
+template <class R>
+void fold_dots(const Workspace& ws, int64_t n, int j, R* V, int64_t ld, const R* r, const R* y);
 // rout = rin - V(:,0:j) * coef[which]; if spec: partials of [V' rout ; rout' rout]
 template <class R>
 void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,

@@ -175,6 +175,65 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
     block_partials<JJ>(acc, J, aw, WM != 0, part, j0, wslot);
 }
 
+// ------------------------------------------------------------------- fold ---
+// w = A r' of a folded step from y = A r (r: the residual before its DGKS
+// sweep, r' = r - V s after it): A r' = y - A V s and, by the Lanczos relation
+// A V_J = V_J T_J + r' e_J', A V s = V_J (T_J s) + s_J r'.  t = T_J s, c = s_J.
+// Explicit fma: the fold pass and the update pass evaluate it bit-identically.
+template <int JN>
+__device__ __forceinline__ double fold_w(double y, const double* vrow, const double* __restrict__ t,
+                                         double c, double rp) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < JN; ++k) a = fma(vrow[k], t[k], a);
+    a = fma(c, rp, a);
+    return y - a;
+}
+
+// Folded step j (device.hpp fold_dots): J = j-1 formed columns V(:,0:J); the
+// pass forms r' (stored as the raw column V(:,J)) and w, and the partials of
+// [V(:,0:J)' w ; r'' w ; w'w] (slots 0..J+1) and r''r' (region 2, slot 0).
+// Without a pending sweep (st.fold == 0) r' = r and w = y exactly.
+template <class R, int J, int POL = kPolNt>
+__global__ __launch_bounds__(kBlock) void k_fold_dots(int64_t n, R* __restrict__ V, int64_t ld,
+                                                      const R* __restrict__ r,
+                                                      const R* __restrict__ y,
+                                                      const double* __restrict__ s,
+                                                      const double* __restrict__ t,
+                                                      double* __restrict__ part, int pstride,
+                                                      const LzState* __restrict__ st) {
+    if (st->abort) return;
+    const bool fold = st->fold != 0;
+    const double c = fold ? s[J - 1] : 0.0;
+    double acc[J + 2];
+#pragma unroll
+    for (int k = 0; k < J + 2; ++k) acc[k] = 0.0;
+    double rr = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    R* vraw = V + (int64_t)J * ld;
+    for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n; it += stride) {
+        const int64_t i = POL == kPolNtRev ? n - 1 - it : it;
+        double vrow[J];
+#pragma unroll
+        for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
+        double rp = (double)r[i], w = (double)y[i];
+        if (fold) {
+            double sv = 0.0;
+#pragma unroll
+            for (int k = 0; k < J; ++k) sv += vrow[k] * s[k];
+            rp = (double)(R)(rp - sv);
+            w = fold_w<J>(w, vrow, t, c, rp);
+        }
+        vraw[i] = (R)rp;
+#pragma unroll
+        for (int k = 0; k < J; ++k) acc[k] += vrow[k] * w;
+        acc[J] += rp * w;
+        acc[J + 1] += w * w;
+        rr += rp * rp;
+    }
+    block_partials<J + 2>(acc, J + 2, rr, true, part, 0, pstride);
+}
+
 // ----------------------------------------------------------------- update ---
 // rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
 // same pass (the V row stays in registers: one HBM read of V serves both).
@@ -190,12 +249,16 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
 //   raw1/2:  also store rout there (the next step's raw column, and the x
 //            buffer of a row-distributed SpMV); with the gate closed (no DGKS
 //            sweep this step) the pass only copies rin to them.
+//   fold:    (chained) a folded step: rin is A r of the pre-DGKS residual and the
+//            raw column is r'; w = A r' is rebuilt with k_fold_dots' fold_w
+//            (fs = step j-1's DGKS coefficients, ft = T fs), if st.fold.
 template <class R, int J, bool SPEC, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
     int64_t n, R* __restrict__ V, int64_t ld, const double* __restrict__ c,
     const R* rin, R* rout, double* __restrict__ part, int pstride,
     const LzState* __restrict__ st, int gate, int chained, R* __restrict__ raw1,
-    R* __restrict__ raw2) {
+    R* __restrict__ raw2, int fold, const double* __restrict__ fs,
+    const double* __restrict__ ft) {
     if (st->abort) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     if (gate >= 0 && st->dgks != gate) {
@@ -208,6 +271,8 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         return;
     }
     const double vs = chained ? st->vscale : 1.0;  // exact no-op when not chained
+    const bool fw = J >= 2 && chained && fold && st->fold;
+    const double fc = fw ? fs[J >= 2 ? J - 2 : 0] : 0.0;
     double acc[J];
 #pragma unroll
     for (int k = 0; k < J; ++k) acc[k] = 0.0;
@@ -217,7 +282,10 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         double vrow[J];
 #pragma unroll
         for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
+        double win = (double)rin[i];
         if (chained) {  // v_j = r * (1/rnorm), stored as k_place would
+            if constexpr (J >= 2)
+                if (fw) win = fold_w<J - 1>(win, vrow, ft, fc, vrow[J - 1]);
             const R v = (R)(vrow[J - 1] * vs);
             V[i + (int64_t)(J - 1) * ld] = v;
             vrow[J - 1] = (double)v;
@@ -225,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < J; ++k) s += vrow[k] * c[k];
-        const R r = (R)((double)rin[i] * vs - s);
+        const R r = (R)(win * vs - s);
         rout[i] = r;
         if (raw1) raw1[i] = r;
         if (raw2) raw2[i] = r;
@@ -276,7 +344,7 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const double* __restrict__
 // (jm = index of r'r) for step jj; returns `take` (which coefficient slot the
 // next sweep uses, 0 for none).  Thread 0 only.
 __device__ int refine_decision(int phase, const double* ss, int jm, int jj, int rstart_jj,
-                               LzState* st, double* rec) {
+                               LzState* st, double* rec, bool defer = false) {
     const double rn = sqrt(fabs(ss[jm]));
     int take = 0;
     if (phase == kFinPostCgs) {
@@ -312,7 +380,7 @@ __device__ int refine_decision(int phase, const double* ss, int jm, int jj, int 
         }
         st->dgks = 0;
     }
-    if (take) {
+    if (take && !defer) {  // defer: a folded park; kFinFoldCoef2 does this on the host path
         st->alpha += ss[jm - 1];
         if (jj == 1 || rstart_jj) st->beta = 0.0;
     }
@@ -372,14 +440,16 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     const int t = threadIdx.x;
     for (int k = t; k < mt; k += nt) sums[k] = s_sum[k];
     const int jm = m - 1;  // index of the w'u / r'r slot
-    if (phase == kFinCgsChained) {
+    if (phase == kFinCgsChained || phase == kFinCgsFolded) {
         // (1) the first DGKS refinement of step j-1, deferred to here: region 2
-        //     holds its [V_{j-1}' r ; r'r] (SRC/dsaitr.f:730-771)
+        //     holds its [V_{j-1}' r ; r'r] (SRC/dsaitr.f:730-771) -- folded: r'r only
+        const bool folded = phase == kFinCgsFolded;
         __shared__ int s_take2, s_go;
         if (t == 0) {
             s_take2 = 0;
             if (st->dgks == 1)
-                s_take2 = refine_decision(kFinDgks1Lazy, s_sum + m, m2 - 1, j - 1, rstart_prev, st, rec);
+                s_take2 = refine_decision(kFinDgks1Lazy, s_sum + m, m2 - 1, j - 1, rstart_prev, st,
+                                          rec, folded);
             // (2) v_j = r / rnorm was NOT formed: the SpMV ran on the raw residual
             //     (A r = rnorm * A v_j), so the CGS sums are rescaled here and the
             //     update pass normalises V(:,j) in place (scale st->vscale)
@@ -397,7 +467,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
             }
         }
         __syncthreads();
-        if (s_take2) {  // the parked second refinement's coefficients (host path)
+        if (s_take2 && !folded) {  // the parked second refinement's coefficients (host path)
             for (int k = t; k < m2 - 1; k += nt) {
                 coef[2 * cstride + k] = s_sum[m + k];
                 if (hld) hcol[(int64_t)(j - 2) * hld + k] += s_sum[m + k];
@@ -451,9 +521,34 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         for (int k = t; k < jm; k += nt) coef[k] = s_sum[k];
         return;
     }
+    if (phase == kFinFoldCoef2) {  // a folded park's second sweep (host path)
+        for (int k = t; k < jm; k += nt) coef[2 * cstride + k] = s_sum[k];
+        if (t == 0) {
+            st->alpha += s_sum[jm - 1];
+            if (j == 1 || rstart) st->beta = 0.0;
+            rec[2 * (j - 1)] = st->alpha;
+            rec[2 * (j - 1) + 1] = st->beta;
+        }
+        return;
+    }
     // refinement phases share the "speculative coefficients" layout
     __shared__ int s_take;
-    if (t == 0) s_take = refine_decision(phase, s_sum, jm, j, rstart, st, rec);
+    const bool pfold = phase == kFinPostCgsFold;
+    if (t == 0) {
+        s_take = refine_decision(pfold ? (int)kFinPostCgs : phase, s_sum, jm, j, rstart, st, rec);
+        if (pfold) {
+            // t = T_j s for the next step's fold: T tridiagonal, alpha_k = rec[2(k-1)]
+            // (step j's includes s_j), beta_k = rec[2(k-1)+1] = T(k, k-1)
+            st->fold = s_take;
+            if (s_take)
+                for (int k = 0; k < jm; ++k) {
+                    double tk = rec[2 * k] * s_sum[k];
+                    if (k > 0) tk = fma(rec[2 * k + 1], s_sum[k - 1], tk);
+                    if (k + 1 < jm) tk = fma(rec[2 * (k + 1) + 1], s_sum[k + 1], tk);
+                    coef[3 * cstride + k] = tk;
+                }
+        }
+    }
     __syncthreads();
     const int take = s_take;
     if (take) {
@@ -756,7 +851,7 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     // two partial regions: the second holds a chained step's deferred DGKS sums
     if ((e = hipMalloc(&ws.part, sizeof(double) * 2 * (size_t)ws.nblk * ws.stride))) return e;
     if ((e = hipMalloc(&ws.sums, sizeof(double) * 2 * (size_t)ws.stride))) return e;
-    if ((e = hipMalloc(&ws.coef, sizeof(double) * 3 * (size_t)ws.stride))) return e;
+    if ((e = hipMalloc(&ws.coef, sizeof(double) * 4 * (size_t)ws.stride))) return e;
     if ((e = hipMalloc(&ws.rec, sizeof(double) * 2 * (size_t)(ncv + 1)))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * (size_t)ncv * ncv))) return e;
     if ((e = hipMalloc(&ws.hcol, sizeof(double) * (size_t)ncv * ncv))) return e;
@@ -773,7 +868,7 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
         ws.st_host->force_dgks2 = (e && e[0] == '1') ? 1 : 0;
     }
     (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(LzState), hipMemcpyHostToDevice, s);
-    (void)hipMemsetAsync(ws.coef, 0, sizeof(double) * 3 * (size_t)ws.stride, s);
+    (void)hipMemsetAsync(ws.coef, 0, sizeof(double) * 4 * (size_t)ws.stride, s);
     return hipSuccess;
 }
 
@@ -884,8 +979,10 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
                            : (double)sizeof(R) * n *
                                  (j + 2 + (x.chained ? 1 : 0) + (x.raw1 ? 1 : 0) + (x.raw2 ? 1 : 0)));
     const dim3 g(ws.nblk), b(kBlock);
-    const bool rev = dir_rev(j, which, false);
+    const bool rev = x.rev >= 0 ? x.rev != 0 : dir_rev(j, which, false);
     double* part = x.part ? x.part : ws.part;
+    const double* fs = ws.coef + ws.stride;       // step j-1's DGKS coefficients
+    const double* ft = ws.coef + 3 * (size_t)ws.stride;  // T fs
     R* Vw = const_cast<R*>(V);  // written only by a chained pass (its column j)
     // fused up to j = 64 (ncv <= 64: dnaupd's C3 runs ncv = 40); the V row of a
     // fused pass lives in registers, so a wider J trades occupancy for
@@ -893,7 +990,8 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
     if (j >= 1 && j <= 64) {
         auto go = [&](auto kern) {
             AHIP_LAUNCH(kern, g, b, 0, ws.stream, n, Vw, ld, c, rin, rout, part, ws.stride,
-                               ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2);
+                               ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2, x.fold ? 1 : 0, fs,
+                               ft);
         };
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
@@ -912,6 +1010,29 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
         AHIP_LAUNCH(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
                            gate);
         if (spec) dots<R>(ws, n, j, V, ld, rout, rout, gate);
+    }
+}
+
+template <class R>
+void fold_dots(const Workspace& ws, int64_t n, int j, R* V, int64_t ld, const R* r, const R* y) {
+    // j = step (2 <= j <= 64): V(:,0:j-1) formed, V(:,j-1) receives r'
+    ProfScope ps(kProfDots, ws.stream, (double)sizeof(R) * n * (j + 2));
+    const dim3 g(ws.nblk), b(kBlock);
+    const double* s = ws.coef + ws.stride;
+    const double* t = ws.coef + 3 * (size_t)ws.stride;
+    auto go = [&](auto kern) {
+        AHIP_LAUNCH(kern, g, b, 0, ws.stream, n, V, ld, r, y, s, t, ws.part, ws.stride, ws.st);
+    };
+    switch (j - 1) {
+#define AHIP_FOLD_CASE(J)                                                                          \
+    case J:                                                                                        \
+        if (ws.v_plain) go(k_fold_dots<R, J, kPolPlain>);                                          \
+        else go(k_fold_dots<R, J>);                                                                \
+        break;
+        AHIP_CASES_1_32(AHIP_FOLD_CASE)
+        AHIP_CASES_33_64(AHIP_FOLD_CASE)
+#undef AHIP_FOLD_CASE
+        default: break;
     }
 }
 
@@ -1077,6 +1198,7 @@ void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z
                           int);                                                                    \
     template void update<R>(const Workspace&, int64_t, int, const R*, int64_t, int, const R*, R*,  \
                             bool, int, const UpdateChain<R>&);                                     \
+    template void fold_dots<R>(const Workspace&, int64_t, int, R*, int64_t, const R*, const R*);   \
     template void zero_if<R>(const Workspace&, int64_t, R*);                                       \
     template void vq_update<R>(const Workspace&, int64_t, R*, int64_t, int, int, double, double,  \
                                R*);                                                                \

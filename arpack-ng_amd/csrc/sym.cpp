@@ -278,8 +278,32 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
         return !(e && e[0] == '0');
     }();
     const bool chain_ok = chain_env && free_run && bI && mode == 1 && ncv <= 64 && !arnoldi;
+    // Folded steps (on top of chaining; AHIP_FOLD=0 disables): step j-1's DGKS
+    // sweep is not a pass of its own.  Its update pass leaves r (before the
+    // sweep) in resid, the SpMV runs on r, and step j's first pass over V
+    // (dev::fold_dots) forms r' = r - V s as the raw V(:,j), rebuilds A r' from
+    // A r with the Lanczos relation, and sums the CGS coefficients of step j
+    // and r''r' (step j-1's deferred refinement check).  Two V passes per step
+    // instead of three.  The last step of a cycle takes its sweep as usual.
+    static const bool fold_env = [] {
+        const char* e = getenv("AHIP_FOLD");
+        return !(e && e[0] == '0');
+    }();
+    const bool fold_ok = chain_ok && fold_env;
     bool chained = false;  // V(:,j) holds the raw residual of step j-1
+    bool folded = false;   // ... which step j's fold pass forms from resid (step j-1's r)
     int rstart_prev = 0;
+    if (fold_ok && k > 0) {
+        // T(1:k,1:k) after dsapps for the fold's t = T s (the device records
+        // hold only this cycle's new steps): rec = (alpha_i, beta_i)
+        double* hs = ws.host_scratch + 4 * (size_t)ws.stride;  // its own tail: 2 (ncv+1)
+        const double* h = workl + ih;
+        for (int i = 1; i <= k; ++i) {
+            hs[2 * (i - 1)] = h[(i - 1) + ncv];
+            hs[2 * (i - 1) + 1] = h[i - 1];
+        }
+        ck(hipMemcpyAsync(ws.rec, hs, sizeof(double) * 2 * k, hipMemcpyHostToDevice, a.stream));
+    }
 
     for (;;) {
         while (j <= k + npk) {
@@ -304,8 +328,8 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 write_state();
             }
             // STEP 2: v_j = r/rnorm; p_j scaled too for bmat='G' (SRC/dsaitr.f:438-454)
-            R* xop = dist_x() ? dist_x() : (free_run ? vcol(j) : wd + ivj);
-            if (!chained)
+            R* xop = dist_x() ? dist_x() : (free_run ? (folded ? a.d_resid : vcol(j)) : wd + ivj);
+            if (!chained && !folded)
                 dev::place(ws, nn, a.d_resid, vcol(j), xop == vcol(j) ? nullptr : xop,
                            bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
@@ -323,19 +347,37 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 u = wd + irj;
             }
             // wnorm and the CGS coefficients h = V_j' B r (SRC/dsaitr.f:538-594)
-            dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
-            if (chained)  // + the deferred refinement decision of step j-1 (region 2)
-                fin(j + 1, dev::kFinCgsChained, j, rstart, -1, j, rstart_prev);
-            else
-                fin(j + 1, dev::kFinCgs, j, rstart, -1);
+            if (folded) {  // + forms r' = V(:,j) and A r' (see fold_ok)
+                dev::fold_dots(ws, nn, j, a.d_v, a.d_ld, a.d_resid, u);
+                fin(j + 1, dev::kFinCgsFolded, j, rstart, -1, 1, rstart_prev);
+            } else {
+                dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
+                if (chained)  // + the deferred refinement decision of step j-1 (region 2)
+                    fin(j + 1, dev::kFinCgsChained, j, rstart, -1, j, rstart_prev);
+                else
+                    fin(j + 1, dev::kFinCgs, j, rstart, -1);
+            }
             // r_j = OP*v_j - V_j h; for bmat='I' the same pass also produces the
             // DGKS coefficients V_j' r_j and r_j' r_j (SRC/dsaitr.f:582-639)
+            const bool next_folded = fold_ok && j < k + npk;
             {
                 dev::UpdateChain<R> x;
                 x.chained = chained;
+                if (folded) {
+                    x.chained = x.fold = true;
+                    x.rev = 1;  // the fold pass sweeps forward, this one back
+                }
+                // a folded next step's SpMV reads r from resid, or from the
+                // distributed operator's x window
+                if (next_folded) x.raw2 = dist_x();
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1, x);
             }
-            if (bI) {
+            if (bI && next_folded) {
+                fin(j + 1, dev::kFinPostCgsFold, j, rstart, -1);  // + t = T s, st.fold
+                chained = false;
+                folded = true;
+                rstart_prev = rstart;
+            } else if (bI) {
                 fin(j + 1, dev::kFinPostCgs, j, rstart, -1);
                 const bool next_chained = chain_ok && j < k + npk;
                 if (next_chained) {
@@ -357,6 +399,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                     if (!lazy) dgks2_tail(j, rstart);
                 }
                 chained = next_chained;
+                folded = false;
                 rstart_prev = rstart;
             } else {
                 // generalized problem: every B*r is a reverse-communication request,
@@ -388,12 +431,21 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
-        chained = false;  // a resumed cycle restarts with a formed v_j
+        const bool was_folded = fold_ok;  // parks inside a folded cycle: resid holds r,
+        chained = false;                  // the raw V(:,ja+1) holds r' (see below)
+        folded = false;  // a resumed cycle restarts with a formed v_j
         if (ws.st_host->abort == 2) {  // step abort_j needs its second DGKS sweep
             const int ja = ws.st_host->abort_j;
             g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
             ws.st_host->abort = 0;
             write_state();
+            if (was_folded && ja < k + npk) {
+                // parked by step ja+1's kFinCgsFolded: r' is the raw V(:,ja+1) and
+                // the second sweep's coefficients V_ja' r' were not summed
+                dev::copy(a.stream, nn, vcol(ja + 1), a.d_resid);
+                dev::dots(ws, nn, ja, a.d_v, a.d_ld, a.d_resid, a.d_resid, -1);
+                fin(ja + 1, dev::kFinFoldCoef2, ja, ja == rstart_j ? 1 : 0, -1);
+            }
             dgks2_tail(ja, ja == rstart_j ? 1 : 0);
             j = ja + 1;
             continue;
@@ -403,6 +455,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             g_stats.nopx -= (k + npk) - ja + 1;
             ws.st_host->abort = 0;
             write_state();
+            if (was_folded) dev::copy(a.stream, nn, vcol(ja), a.d_resid);  // r' of step ja-1
             j = ja;
             continue;
         }
