@@ -51,6 +51,20 @@ def load_pkg():
     return m
 
 
+def json_stdout():
+    """stdout carries exactly ONE JSON line (rank 0's; the driver's contract).
+    Everything else that writes to fd 1 -- RCCL's version banner at
+    communicator init, gloo's "[Gloo] Rank r is connected ..." from every rank,
+    library prints -- is sent to stderr: fd 1 is pointed at stderr for the
+    whole run and the JSON goes to a saved duplicate of the original stdout."""
+    import ctypes
+    sys.stdout.flush()
+    ctypes.CDLL(None).fflush(None)
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return fd
+
+
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of `kernel_substr` from the committed rocprofv3 PMC
     summary (profiles/r*_pmc.json, written by tools/pmc_summary.py from separate
@@ -119,6 +133,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
+    out_fd = json_stdout()
     pkg = load_pkg()
     n, nev, ncv = args.n, args.nev, args.ncv
     D = None
@@ -329,7 +344,7 @@ def main():
             out["speedup_vs_cpu_lanczos_steps"] = \
                 (nopx / elapsed) / out["cpu_baseline"]["lanczos_steps_per_s"]
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist or args.force_dist:
         del D
         pkg.comm_destroy()
