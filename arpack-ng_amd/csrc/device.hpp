@@ -127,9 +127,6 @@ void dots(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, const R
 template <class R>
 struct UpdateChain {
     bool chained = false;
-    bool fold = false;  // folded step: w = A r' is rebuilt from the SpMV of the
-                        // pre-DGKS residual (k_fold_dots' expression), see fold_dots
-    int rev = -1;       // sweep direction override (-1: dir_rev's choice)
     R* raw1 = nullptr;
     R* raw2 = nullptr;
     double* part = nullptr;
@@ -138,13 +135,18 @@ struct UpdateChain {
 // applied here instead of in a pass of its own.  The SpMV ran on r (step j-1's
 // residual BEFORE its DGKS correction); with s = coef[1] (step j-1's DGKS
 // coefficients, applied only if st.fold) and t = T_{j-1} s (coef slot 3):
-//   r' = r - V(:,1:j-1) s        -> stored as the RAW column V(:,j)
+//   r' = r - V(:,1:j-1) s        (in registers; fold_update stores v_j)
 //   w  = A r - V(:,1:j-1) t - s_{j-1} r'   (= A r' by the Lanczos relation
 //        A V_{j-1} = V_{j-1} T_{j-1} + r' e', exact up to O(eps*|s|) terms)
 // and the partials of [V(:,1:j)' w ; w'w] (region 1, j+1 slots) and r''r'
 // (region 2, one slot) for kFinCgsFolded.
 template <class R>
 void fold_dots(const Workspace& ws, int64_t n, int j, R* V, int64_t ld, const R* r, const R* y);
+// The folded step's second pass: r' and w again (bit-identically), v_j =
+// r' / rnorm -> V(:,j), r_j = w / rnorm - V(:,1:j) h -> r (in place) and x2
+// (nullable), partials of [V(:,1:j)' r_j ; r_j' r_j].
+template <class R>
+void fold_update(const Workspace& ws, int64_t n, int j, R* V, int64_t ld, const R* y, R* r, R* x2);
 // rout = rin - V(:,0:j) * coef[which]; if spec: partials of [V' rout ; rout' rout]
 template <class R>
 void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,

@@ -23,78 +23,14 @@
 #include <vector>
 
 #include "device.hpp"
+#include "passes.hpp"
+#include "reduce.hpp"
 
 namespace ahip::dev {
 
 namespace {
 
 constexpr double kSafminD = DBL_MIN;
-
-// Loads of the Krylov basis V in the Gram-Schmidt and V*Q passes.  Policy POL:
-//   kPolNt / kPolNtRev  non-temporal, sweeping rows first-to-last / last-to-first:
-//            a basis of several hundred MB or more is streamed from HBM; the NT
-//            hint keeps the 1-2.4 GB sweep from evicting the n-vectors every pass
-//            re-reads (w, r) from the caches (+3.2% cycle rate at n = 1e7), and
-//            alternating directions start each pass on rows the previous one left
-//            in the 256 MB Infinity Cache;
-//   kPolPlain  plain loads: a basis that fits the Infinity Cache (<= ~400 MB)
-//            is re-read from it by the next pass (same-box A/B: +7% cycle rate at
-//            n = 1e6, +4% at 1.25e6 rows, -2.7% at 2.5e6 and 1e7 -- hence the
-//            size rule in ws_create, AHIP_V_POLICY=nt|plain to override).
-enum VPol : int { kPolNt = 0, kPolNtRev = 1, kPolPlain = 2 };
-template <int POL, class T>
-__device__ __forceinline__ T vld(const T* p) {
-    if constexpr (POL == kPolPlain) return *p;
-    else return __builtin_nontemporal_load(p);
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// Reduce CH per-thread accumulators over the block and write them (plus an
-// optional extra value) as this block's partial row.
-template <int CH>
-__device__ __forceinline__ void block_partials(double (&acc)[CH], int jc, double extra,
-                                               bool with_extra, double* part, int col0,
-                                               int extra_slot) {
-    // k-major layout part[slot * nblk + block]: the finalize reads each slot
-    // as one contiguous (coalesced) run
-    __shared__ double red[kBlock / 64][CH + 1];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-        if (k < jc) {
-            const double s = wave_sum(acc[k]);
-            if (lane == 0) red[wave][k] = s;
-        }
-    }
-    if (with_extra) {
-        const double s = wave_sum(extra);
-        if (lane == 0) red[wave][CH] = s;
-    }
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < jc) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][t];
-        part[(size_t)(col0 + t) * gridDim.x + blockIdx.x] = s;
-    }
-    if (with_extra && t == kBlock - 1) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][CH];
-        part[(size_t)extra_slot * gridDim.x + blockIdx.x] = s;
-    }
-}
-
-__device__ __forceinline__ bool gate_closed(const LzState* st, int gate) {
-    if (st->abort) return true;
-    return gate >= 0 && st->dgks != gate;
-}
 
 // ------------------------------------------------------------------ place ---
 template <class R>
@@ -175,65 +111,6 @@ __global__ __launch_bounds__(kBlock) void k_dots(int64_t n, int j0, const R* __r
     block_partials<JJ>(acc, J, aw, WM != 0, part, j0, wslot);
 }
 
-// ------------------------------------------------------------------- fold ---
-// w = A r' of a folded step from y = A r (r: the residual before its DGKS
-// sweep, r' = r - V s after it): A r' = y - A V s and, by the Lanczos relation
-// A V_J = V_J T_J + r' e_J', A V s = V_J (T_J s) + s_J r'.  t = T_J s, c = s_J.
-// Explicit fma: the fold pass and the update pass evaluate it bit-identically.
-template <int JN>
-__device__ __forceinline__ double fold_w(double y, const double* vrow, const double* __restrict__ t,
-                                         double c, double rp) {
-    double a = 0.0;
-#pragma unroll
-    for (int k = 0; k < JN; ++k) a = fma(vrow[k], t[k], a);
-    a = fma(c, rp, a);
-    return y - a;
-}
-
-// Folded step j (device.hpp fold_dots): J = j-1 formed columns V(:,0:J); the
-// pass forms r' (stored as the raw column V(:,J)) and w, and the partials of
-// [V(:,0:J)' w ; r'' w ; w'w] (slots 0..J+1) and r''r' (region 2, slot 0).
-// Without a pending sweep (st.fold == 0) r' = r and w = y exactly.
-template <class R, int J, int POL = kPolNt>
-__global__ __launch_bounds__(kBlock) void k_fold_dots(int64_t n, R* __restrict__ V, int64_t ld,
-                                                      const R* __restrict__ r,
-                                                      const R* __restrict__ y,
-                                                      const double* __restrict__ s,
-                                                      const double* __restrict__ t,
-                                                      double* __restrict__ part, int pstride,
-                                                      const LzState* __restrict__ st) {
-    if (st->abort) return;
-    const bool fold = st->fold != 0;
-    const double c = fold ? s[J - 1] : 0.0;
-    double acc[J + 2];
-#pragma unroll
-    for (int k = 0; k < J + 2; ++k) acc[k] = 0.0;
-    double rr = 0.0;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    R* vraw = V + (int64_t)J * ld;
-    for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n; it += stride) {
-        const int64_t i = POL == kPolNtRev ? n - 1 - it : it;
-        double vrow[J];
-#pragma unroll
-        for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
-        double rp = (double)r[i], w = (double)y[i];
-        if (fold) {
-            double sv = 0.0;
-#pragma unroll
-            for (int k = 0; k < J; ++k) sv += vrow[k] * s[k];
-            rp = (double)(R)(rp - sv);
-            w = fold_w<J>(w, vrow, t, c, rp);
-        }
-        vraw[i] = (R)rp;
-#pragma unroll
-        for (int k = 0; k < J; ++k) acc[k] += vrow[k] * w;
-        acc[J] += rp * w;
-        acc[J + 1] += w * w;
-        rr += rp * rp;
-    }
-    block_partials<J + 2>(acc, J + 2, rr, true, part, 0, pstride);
-}
-
 // ----------------------------------------------------------------- update ---
 // rout = rin - V(:,0:J) c ; SPEC: partials of [V' rout ; rout' rout] from the
 // same pass (the V row stays in registers: one HBM read of V serves both).
@@ -249,16 +126,12 @@ __global__ __launch_bounds__(kBlock) void k_fold_dots(int64_t n, R* __restrict__
 //   raw1/2:  also store rout there (the next step's raw column, and the x
 //            buffer of a row-distributed SpMV); with the gate closed (no DGKS
 //            sweep this step) the pass only copies rin to them.
-//   fold:    (chained) a folded step: rin is A r of the pre-DGKS residual and the
-//            raw column is r'; w = A r' is rebuilt with k_fold_dots' fold_w
-//            (fs = step j-1's DGKS coefficients, ft = T fs), if st.fold.
 template <class R, int J, bool SPEC, int POL = kPolNt>
 __global__ __launch_bounds__(kBlock) void k_update_fused(
     int64_t n, R* __restrict__ V, int64_t ld, const double* __restrict__ c,
     const R* rin, R* rout, double* __restrict__ part, int pstride,
     const LzState* __restrict__ st, int gate, int chained, R* __restrict__ raw1,
-    R* __restrict__ raw2, int fold, const double* __restrict__ fs,
-    const double* __restrict__ ft) {
+    R* __restrict__ raw2) {
     if (st->abort) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     if (gate >= 0 && st->dgks != gate) {
@@ -271,8 +144,6 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         return;
     }
     const double vs = chained ? st->vscale : 1.0;  // exact no-op when not chained
-    const bool fw = J >= 2 && chained && fold && st->fold;
-    const double fc = fw ? fs[J >= 2 ? J - 2 : 0] : 0.0;
     double acc[J];
 #pragma unroll
     for (int k = 0; k < J; ++k) acc[k] = 0.0;
@@ -282,10 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_update_fused(
         double vrow[J];
 #pragma unroll
         for (int k = 0; k < J; ++k) vrow[k] = vld<POL>(V + i + (int64_t)k * ld);
-        double win = (double)rin[i];
+        const double win = (double)rin[i];
         if (chained) {  // v_j = r * (1/rnorm), stored as k_place would
-            if constexpr (J >= 2)
-                if (fw) win = fold_w<J - 1>(win, vrow, ft, fc, vrow[J - 1]);
             const R v = (R)(vrow[J - 1] * vs);
             V[i + (int64_t)(J - 1) * ld] = v;
             vrow[J - 1] = (double)v;
@@ -420,16 +289,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
             double s = 0.0;
             if (k < mt) {
                 const double* p = k < m ? part + (int64_t)k * nblk : part2 + (int64_t)(k - m) * nblk;
-                double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-                int b = sub;
-                for (; b + 96 < nblk; b += 128) {
-                    s += p[b];
-                    s1 += p[b + 32];
-                    s2 += p[b + 64];
-                    s3 += p[b + 96];
-                }
-                for (; b < nblk; b += 32) s += p[b];
-                s = (s + s1) + (s2 + s3);
+                s = slot_partial(p, nblk, sub);
             }
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 32);
@@ -886,16 +746,6 @@ void ws_destroy(Workspace& ws) {
     ws = Workspace{};
 }
 
-namespace {
-struct ProfScope {  // kernel-mode span (prof_arm) around one launcher when profiling is on
-    ProfClass c;
-    hipStream_t s;
-    double bytes;
-    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_arm(c); }
-    ~ProfScope() { prof_disarm(c, bytes); }
-};
-}  // namespace
-
 // Sweep direction of the V passes.  Each pass starts where the previous one
 // ended, on the rows the 256 MB Infinity Cache still holds: within step j the
 // CGS dots, the CGS update and the first DGKS update alternate, and so do
@@ -920,13 +770,6 @@ void place(const Workspace& ws, int64_t n, const R* r, R* vcol, R* copy1, R* sc,
     AHIP_LAUNCH(k_place<R>, dim3(grid_for(n)), dim3(kBlock), 0, ws.stream, n, r, vcol, copy1,
                        sc, ws.st, j);
 }
-
-#define AHIP_CASES_1_32(M) \
-    M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16) \
-    M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
-#define AHIP_CASES_33_64(M) \
-    M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41) M(42) M(43) M(44) M(45) M(46) M(47) M(48) \
-    M(49) M(50) M(51) M(52) M(53) M(54) M(55) M(56) M(57) M(58) M(59) M(60) M(61) M(62) M(63) M(64)
 
 template <class R, int WM, int POL = kPolNt>
 static void launch_dots(const Workspace& ws, int64_t n, int j0, int jc, const R* V, int64_t ld,
@@ -979,10 +822,8 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
                            : (double)sizeof(R) * n *
                                  (j + 2 + (x.chained ? 1 : 0) + (x.raw1 ? 1 : 0) + (x.raw2 ? 1 : 0)));
     const dim3 g(ws.nblk), b(kBlock);
-    const bool rev = x.rev >= 0 ? x.rev != 0 : dir_rev(j, which, false);
+    const bool rev = dir_rev(j, which, false);
     double* part = x.part ? x.part : ws.part;
-    const double* fs = ws.coef + ws.stride;       // step j-1's DGKS coefficients
-    const double* ft = ws.coef + 3 * (size_t)ws.stride;  // T fs
     R* Vw = const_cast<R*>(V);  // written only by a chained pass (its column j)
     // fused up to j = 64 (ncv <= 64: dnaupd's C3 runs ncv = 40); the V row of a
     // fused pass lives in registers, so a wider J trades occupancy for
@@ -990,8 +831,7 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
     if (j >= 1 && j <= 64) {
         auto go = [&](auto kern) {
             AHIP_LAUNCH(kern, g, b, 0, ws.stream, n, Vw, ld, c, rin, rout, part, ws.stride,
-                               ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2, x.fold ? 1 : 0, fs,
-                               ft);
+                               ws.st, gate, x.chained ? 1 : 0, x.raw1, x.raw2);
         };
         switch (j) {
 #define AHIP_UPD_CASE(J)                                                                           \
@@ -1010,29 +850,6 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
         AHIP_LAUNCH(k_update_generic<R>, g, b, 0, ws.stream, n, j, V, ld, c, rin, rout, ws.st,
                            gate);
         if (spec) dots<R>(ws, n, j, V, ld, rout, rout, gate);
-    }
-}
-
-template <class R>
-void fold_dots(const Workspace& ws, int64_t n, int j, R* V, int64_t ld, const R* r, const R* y) {
-    // j = step (2 <= j <= 64): V(:,0:j-1) formed, V(:,j-1) receives r'
-    ProfScope ps(kProfDots, ws.stream, (double)sizeof(R) * n * (j + 2));
-    const dim3 g(ws.nblk), b(kBlock);
-    const double* s = ws.coef + ws.stride;
-    const double* t = ws.coef + 3 * (size_t)ws.stride;
-    auto go = [&](auto kern) {
-        AHIP_LAUNCH(kern, g, b, 0, ws.stream, n, V, ld, r, y, s, t, ws.part, ws.stride, ws.st);
-    };
-    switch (j - 1) {
-#define AHIP_FOLD_CASE(J)                                                                          \
-    case J:                                                                                        \
-        if (ws.v_plain) go(k_fold_dots<R, J, kPolPlain>);                                          \
-        else go(k_fold_dots<R, J>);                                                                \
-        break;
-        AHIP_CASES_1_32(AHIP_FOLD_CASE)
-        AHIP_CASES_33_64(AHIP_FOLD_CASE)
-#undef AHIP_FOLD_CASE
-        default: break;
     }
 }
 
@@ -1198,7 +1015,6 @@ void ger_cols(hipStream_t s, int64_t n, int k, const R* x, const double* w, R* Z
                           int);                                                                    \
     template void update<R>(const Workspace&, int64_t, int, const R*, int64_t, int, const R*, R*,  \
                             bool, int, const UpdateChain<R>&);                                     \
-    template void fold_dots<R>(const Workspace&, int64_t, int, R*, int64_t, const R*, const R*);   \
     template void zero_if<R>(const Workspace&, int64_t, R*);                                       \
     template void vq_update<R>(const Workspace&, int64_t, R*, int64_t, int, int, double, double,  \
                                R*);                                                                \

@@ -115,7 +115,7 @@ __device__ __forceinline__ T ldg(const T* p) {
 // with another workgroup's (or rank's) spill through the slots, and only its
 // last superblock's spill leaves through a slot.  Each wave streams its slices
 // with the next slice's first chunk in flight, across superblock boundaries.
-template <int U, bool NT>
+template <int U, bool NT, bool YNT = false>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
     const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
@@ -221,6 +221,7 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         for (int i = t; i < R; i += kSymThreads) {
             const double v = yw[i];
             if (i < head) slot_hi[off + i] = v;
+            else if constexpr (YNT) __builtin_nontemporal_store(v, y + r0 + i);
             else y[r0 + i] = v;
         }
         if (b == b1 - 1) {  // the chain's last spill leaves through a slot
@@ -624,6 +625,14 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
 
 // variant 7: no chaining (one superblock per workgroup launch), for A/B
 static int sym_chain(const Csr& A) { return A.ss_variant == 7 ? 1 : A.ss_chain; }
+// AHIP_SPMV_YNT=1: the default kernel stores y with non-temporal stores (A/B knob)
+static bool spmv_ynt() {
+    static const bool on = [] {
+        const char* e = getenv("AHIP_SPMV_YNT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) {
     auto go = [&](auto kern) {
@@ -655,7 +664,11 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
         case 4: go(k_csr_ssell<4, false>); break;
         case 5: go(k_csr_ssell<6, true>); break;
         case 6: go(k_csr_ssell<12, true>); break;
-        default: go(k_csr_ssell<8, true>); break;  // 7: the same without chaining
+        case 11: go(k_csr_ssell<8, true, true>); break;  // y stored non-temporally
+        default:  // 7: the same without chaining
+            if (spmv_ynt()) go(k_csr_ssell<8, true, true>);
+            else go(k_csr_ssell<8, true>);
+            break;
     }
 }
 

@@ -281,10 +281,12 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     // Folded steps (on top of chaining; AHIP_FOLD=0 disables): step j-1's DGKS
     // sweep is not a pass of its own.  Its update pass leaves r (before the
     // sweep) in resid, the SpMV runs on r, and step j's first pass over V
-    // (dev::fold_dots) forms r' = r - V s as the raw V(:,j), rebuilds A r' from
-    // A r with the Lanczos relation, and sums the CGS coefficients of step j
-    // and r''r' (step j-1's deferred refinement check).  Two V passes per step
-    // instead of three.  The last step of a cycle takes its sweep as usual.
+    // (dev::fold_dots, reads only) forms r' = r - V s in registers, rebuilds
+    // A r' from A r with the Lanczos relation, and sums the CGS coefficients of
+    // step j and r''r' (step j-1's deferred refinement check); the second pass
+    // (dev::fold_update) forms them again, stores v_j = r'/rnorm and r_j.  Two V
+    // passes per step instead of three.  The last step of a cycle takes its
+    // sweep as usual.
     static const bool fold_env = [] {
         const char* e = getenv("AHIP_FOLD");
         return !(e && e[0] == '0');
@@ -360,15 +362,14 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             // r_j = OP*v_j - V_j h; for bmat='I' the same pass also produces the
             // DGKS coefficients V_j' r_j and r_j' r_j (SRC/dsaitr.f:582-639)
             const bool next_folded = fold_ok && j < k + npk;
-            {
+            // a folded next step's SpMV reads r from resid, or from the
+            // distributed operator's x window
+            if (folded) {
+                dev::fold_update(ws, nn, j, a.d_v, a.d_ld, wd + irj, a.d_resid,
+                                 next_folded ? dist_x() : nullptr);
+            } else {
                 dev::UpdateChain<R> x;
                 x.chained = chained;
-                if (folded) {
-                    x.chained = x.fold = true;
-                    x.rev = 1;  // the fold pass sweeps forward, this one back
-                }
-                // a folded next step's SpMV reads r from resid, or from the
-                // distributed operator's x window
                 if (next_folded) x.raw2 = dist_x();
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1, x);
             }
@@ -431,18 +432,24 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
-        const bool was_folded = fold_ok;  // parks inside a folded cycle: resid holds r,
-        chained = false;                  // the raw V(:,ja+1) holds r' (see below)
+        // a park inside a folded cycle leaves resid = r of the step before the
+        // parked one, BEFORE its DGKS sweep (st.fold: the sweep was taken)
+        const bool was_folded = fold_ok;
+        chained = false;
         folded = false;  // a resumed cycle restarts with a formed v_j
+        auto unfold = [&](int jprev) {  // resid = r' = r - V(:,1:jprev) s
+            if (was_folded && ws.st_host->fold)
+                dev::update(ws, nn, jprev, a.d_v, a.d_ld, 1, a.d_resid, a.d_resid, false, -1);
+        };
         if (ws.st_host->abort == 2) {  // step abort_j needs its second DGKS sweep
             const int ja = ws.st_host->abort_j;
             g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
             ws.st_host->abort = 0;
             write_state();
             if (was_folded && ja < k + npk) {
-                // parked by step ja+1's kFinCgsFolded: r' is the raw V(:,ja+1) and
-                // the second sweep's coefficients V_ja' r' were not summed
-                dev::copy(a.stream, nn, vcol(ja + 1), a.d_resid);
+                // parked by step ja+1's kFinCgsFolded: r' was formed only in
+                // registers and the second sweep's coefficients V_ja' r' not summed
+                unfold(ja);
                 dev::dots(ws, nn, ja, a.d_v, a.d_ld, a.d_resid, a.d_resid, -1);
                 fin(ja + 1, dev::kFinFoldCoef2, ja, ja == rstart_j ? 1 : 0, -1);
             }
@@ -455,7 +462,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             g_stats.nopx -= (k + npk) - ja + 1;
             ws.st_host->abort = 0;
             write_state();
-            if (was_folded) dev::copy(a.stream, nn, vcol(ja), a.d_resid);  // r' of step ja-1
+            unfold(ja - 1);  // r' of step ja-1
             j = ja;
             continue;
         }

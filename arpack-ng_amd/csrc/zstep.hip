@@ -24,6 +24,7 @@
 
 #include "zcommon.hpp"
 #include "zengine.hpp"
+#include "reduce.hpp"
 
 namespace ahip::zdev {
 
@@ -231,17 +232,7 @@ __global__ __launch_bounds__(1024) void k_zs_finalize(const double* __restrict__
             const int k = k0 + (t >> 5);
             double s = 0.0;
             if (k < mt) {
-                const double* p = part + (int64_t)k * nblk;
-                double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-                int b = sub;
-                for (; b + 96 < nblk; b += 128) {
-                    s += p[b];
-                    s1 += p[b + 32];
-                    s2 += p[b + 64];
-                    s3 += p[b + 96];
-                }
-                for (; b < nblk; b += 32) s += p[b];
-                s = (s + s1) + (s2 + s3);
+                s = dev::slot_partial(part + (int64_t)k * nblk, nblk, sub);
             }
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 32);
