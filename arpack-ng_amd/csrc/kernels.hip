@@ -262,16 +262,14 @@ __device__ int refine_decision(int phase, const double* ss, int jm, int jj, int 
 // m slots of `part`; region 2: m2 slots of `part2`, only for kFinCgsChained)
 // and the phase logic.  from_sums: the m + m2 sums are already in `sums`
 // (reduced, and allreduced across ranks).
-__global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
-                                                   int from_sums, int m, int phase, int j,
-                                                   int rstart, int gate, double* __restrict__ sums,
-                                                   double* __restrict__ coef, int cstride,
-                                                   double* __restrict__ rec,
-                                                   LzState* __restrict__ st,
-                                                   double* __restrict__ hcol, int hld,
-                                                   const double* __restrict__ part2, int m2,
-                                                   int rstart_prev) {
-    if (gate_closed(st, gate)) return;
+// The kernel body; st is the block's LDS copy of the state (k_finalize).
+__device__ __forceinline__ void fin_body(const double* __restrict__ part, int nblk, int from_sums,
+                                         int m, int phase, int j, int rstart,
+                                         double* __restrict__ sums, double* __restrict__ coef,
+                                         int cstride, double* __restrict__ rec, LzState* st,
+                                         double* __restrict__ hcol, int hld,
+                                         const double* __restrict__ part2, int m2,
+                                         int rstart_prev, double* s_rec) {
     // the m + m2 (<= 2 ncv + 4) sums are staged in dynamic LDS sized by the
     // launch, so any ncv the argument checks accept fits
     extern __shared__ double s_sum[];
@@ -398,13 +396,16 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         s_take = refine_decision(pfold ? (int)kFinPostCgs : phase, s_sum, jm, j, rstart, st, rec);
         if (pfold) {
             // t = T_j s for the next step's fold: T tridiagonal, alpha_k = rec[2(k-1)]
-            // (step j's includes s_j), beta_k = rec[2(k-1)+1] = T(k, k-1)
+            // (step j's includes s_j), beta_k = rec[2(k-1)+1] = T(k, k-1); the
+            // records come from the LDS copy (step j's just updated)
             st->fold = s_take;
+            s_rec[2 * (j - 1)] = st->alpha;
+            s_rec[2 * (j - 1) + 1] = st->beta;
             if (s_take)
                 for (int k = 0; k < jm; ++k) {
-                    double tk = rec[2 * k] * s_sum[k];
-                    if (k > 0) tk = fma(rec[2 * k + 1], s_sum[k - 1], tk);
-                    if (k + 1 < jm) tk = fma(rec[2 * (k + 1) + 1], s_sum[k + 1], tk);
+                    double tk = s_rec[2 * k] * s_sum[k];
+                    if (k > 0) tk = fma(s_rec[2 * k + 1], s_sum[k - 1], tk);
+                    if (k + 1 < jm) tk = fma(s_rec[2 * (k + 1) + 1], s_sum[k + 1], tk);
                     coef[3 * cstride + k] = tk;
                 }
         }
@@ -417,6 +418,33 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
             if (hld) hcol[(int64_t)(j - 1) * hld + k] += s_sum[k];  // daxpy into h(1:j,j) (dnaitr.f:681)
         }
     }
+}
+
+// Single-block finalize.  The state is read once into LDS and written back
+// once: the phase logic is one thread's chain of dependent accesses, which on
+// the global copy (last written by another XCD's finalize) cost a memory
+// latency each.
+constexpr int kFoldRecMax = 2 * 66;  // T records staged for the fold's t (j <= 64)
+__global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
+                                                   int from_sums, int m, int phase, int j,
+                                                   int rstart, int gate, double* __restrict__ sums,
+                                                   double* __restrict__ coef, int cstride,
+                                                   double* __restrict__ rec,
+                                                   LzState* __restrict__ st,
+                                                   double* __restrict__ hcol, int hld,
+                                                   const double* __restrict__ part2, int m2,
+                                                   int rstart_prev) {
+    __shared__ LzState s_st;
+    __shared__ double s_rec[kFoldRecMax];
+    if (threadIdx.x == 0) s_st = *st;
+    if (phase == kFinPostCgsFold && 2 * (j + 1) <= kFoldRecMax)
+        for (int k = threadIdx.x; k < 2 * (j + 1); k += blockDim.x) s_rec[k] = rec[k];
+    __syncthreads();
+    if (gate_closed(&s_st, gate)) return;
+    fin_body(part, nblk, from_sums, m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol,
+             hld, part2, m2, rstart_prev, s_rec);
+    __syncthreads();
+    if (threadIdx.x == 0) *st = s_st;
 }
 
 template <class R>
