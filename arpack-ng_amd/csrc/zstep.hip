@@ -216,14 +216,12 @@ __global__ void k_zs_zero_if(int64_t n, typename C2<R>::T* r, const LzState* st)
 }
 
 // Single-block finalize over m complex slots (2m real; slot m-1 = the norm).
-__global__ __launch_bounds__(1024) void k_zs_finalize(const double* __restrict__ part, int nblk, int m,
-                                                      int phase, int j, int rstart, int gate,
-                                                      double* __restrict__ sums,
-                                                      double2* __restrict__ coef, int cstride,
-                                                      double* __restrict__ rec,
-                                                      LzState* __restrict__ st,
-                                                      double2* __restrict__ hcol, int hld) {
-    if (zgate_closed(st, gate)) return;
+__device__ __forceinline__ void zs_fin_body(const double* __restrict__ part, int nblk, int m,
+                                            int phase, int j, int rstart,
+                                            double* __restrict__ sums,
+                                            double2* __restrict__ coef, int cstride,
+                                            double* __restrict__ rec, LzState* st,
+                                            double2* __restrict__ hcol, int hld) {
     extern __shared__ double s_sum[];  // 2m doubles
     const int mt = 2 * m, nt = blockDim.x, t = threadIdx.x;
     {   // 32 slots per round, 32 threads per slot in four chains (as k_finalize)
@@ -316,6 +314,24 @@ __global__ __launch_bounds__(1024) void k_zs_finalize(const double* __restrict__
             hcol[(int64_t)(j - 1) * hld + k] = h;
         }
     }
+}
+
+// The state is read once into LDS and written back once (as k_finalize): the
+// phase logic is one thread's chain of dependent state accesses.
+__global__ __launch_bounds__(1024) void k_zs_finalize(const double* __restrict__ part, int nblk, int m,
+                                                      int phase, int j, int rstart, int gate,
+                                                      double* __restrict__ sums,
+                                                      double2* __restrict__ coef, int cstride,
+                                                      double* __restrict__ rec,
+                                                      LzState* __restrict__ st,
+                                                      double2* __restrict__ hcol, int hld) {
+    __shared__ LzState s_st;
+    if (threadIdx.x == 0) s_st = *st;
+    __syncthreads();
+    if (zgate_closed(&s_st, gate)) return;
+    zs_fin_body(part, nblk, m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol, hld);
+    __syncthreads();
+    if (threadIdx.x == 0) *st = s_st;
 }
 
 inline int sgrid(const Ws& ws) { return ws.nblk; }
