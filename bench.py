@@ -147,7 +147,9 @@ def main():
         else:
             box = [pkg.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
-            pkg.comm_init(world, rank, box[0], device=local_rank)
+            # one GPU per rank; a launcher that narrows each rank's visible
+            # devices (HIP_VISIBLE_DEVICES) leaves device 0 = this rank's GPU
+            pkg.comm_init(world, rank, box[0], device=local_rank % max(1, pkg.device_count()))
         r0, r1 = pkg.partition_rows(n, world, rank)
     else:
         r0, r1 = 0, n
