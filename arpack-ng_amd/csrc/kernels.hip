@@ -380,7 +380,10 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
         return;
     }
     if (phase == kFinFoldCoef2) {  // a folded park's second sweep (host path)
-        for (int k = t; k < jm; k += nt) coef[2 * cstride + k] = s_sum[k];
+        for (int k = t; k < jm; k += nt) {
+            coef[2 * cstride + k] = s_sum[k];
+            if (hld) hcol[(int64_t)(j - 1) * hld + k] += s_sum[k];  // daxpy into h(1:j,j)
+        }
         if (t == 0) {
             st->alpha += s_sum[jm - 1];
             if (j == 1 || rstart) st->beta = 0.0;
@@ -401,7 +404,7 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
             st->fold = s_take;
             s_rec[2 * (j - 1)] = st->alpha;
             s_rec[2 * (j - 1) + 1] = st->beta;
-            if (s_take)
+            if (s_take && !hld)  // (Arnoldi: H s below, in parallel)
                 for (int k = 0; k < jm; ++k) {
                     double tk = s_rec[2 * k] * s_sum[k];
                     if (k > 0) tk = fma(s_rec[2 * k + 1], s_sum[k - 1], tk);
@@ -412,6 +415,23 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
     }
     __syncthreads();
     const int take = s_take;
+    if (pfold && take && hld) {
+        // Arnoldi: t = H_j s with the full upper-Hessenberg records (column q of
+        // H: hcol rows 0..q, subdiagonal H(q+1,q) = rec[2q+3]); this step's
+        // column is h + s, read before the daxpy below adds s to it
+        for (int i = t; i < jm; i += nt) {
+            double ti = 0.0;
+            for (int q = i > 0 ? i - 1 : 0; q < jm; ++q) {
+                double hiq;
+                if (q == jm - 1) hiq = hcol[(int64_t)q * hld + i] + s_sum[i];
+                else if (i <= q) hiq = hcol[(int64_t)q * hld + i];
+                else hiq = s_rec[2 * q + 3];
+                ti = fma(hiq, s_sum[q], ti);
+            }
+            coef[3 * cstride + i] = ti;
+        }
+        __syncthreads();
+    }
     if (take) {
         for (int k = t; k < jm; k += nt) {
             coef[take * cstride + k] = s_sum[k];
@@ -750,6 +770,7 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
         return e;
+    if (ncv <= 64 && (e = hipHostMalloc(&ws.host_hcol, sizeof(double) * (size_t)ncv * ncv))) return e;
     memset(ws.st_host, 0, sizeof(LzState));
     {   // test hook: exercise the (rare) second DGKS refinement on every step
         const char* e = getenv("AHIP_FORCE_DGKS2");
@@ -771,6 +792,7 @@ void ws_destroy(Workspace& ws) {
     if (ws.st) (void)hipFree(ws.st);
     if (ws.st_host) (void)hipHostFree(ws.st_host);
     if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
+    if (ws.host_hcol) (void)hipHostFree(ws.host_hcol);
     ws = Workspace{};
 }
 

@@ -23,13 +23,19 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _solve(tmp_path, fixture, fold):
-    out = tmp_path / f"{fixture}_fold{fold}.npz"
-    env = dict(os.environ, AHIP_FOLD=str(fold), AHIP_FORCE_DGKS2="0")
-    r = subprocess.run([sys.executable, os.path.join(HERE, "dgks_worker.py"), fixture, "free", str(out)],
+def _solve_env(tmp_path, fixture, extra, how="free"):
+    tag = "_".join("%s%s" % kv for kv in sorted(extra.items()))
+    out = tmp_path / f"{fixture}_{how}_{tag}.npz"
+    env = dict(os.environ, AHIP_FORCE_DGKS2="0")
+    env.update(extra)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "dgks_worker.py"), fixture, how, str(out)],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return dict(np.load(out))
+
+
+def _solve(tmp_path, fixture, fold):
+    return _solve_env(tmp_path, fixture, dict(AHIP_FOLD=str(fold)))
 
 
 @pytest.mark.parametrize("fixture", ["g3_anderson3d", "g4_banded", "g5_anderson2d_sa",
@@ -68,3 +74,38 @@ def test_folded_widest_basis(pkg):
     np.testing.assert_allclose(np.sort(d), dw, rtol=0, atol=1e-10 * np.abs(dw).max())
     r = np.linalg.norm(A @ z - z * d, axis=0)
     assert np.all(r <= 1e-8 * np.abs(dw).max()), r
+
+
+@pytest.mark.parametrize("fixture", ["n2_dnsimp_tol", "n3_convdiff_lm", "n5_convdiff_li",
+                                     "n7_convdiff_real"])
+def test_folded_arnoldi(tmp_path, golden, fixture):
+    """dnaupd: the fold's t = H s uses the full Hessenberg records.  Same restart
+    cycles and OP*x count as the unfolded engine and the reference's cycles;
+    Ritz values within the fixtures' pseudospectral bound (test_gpu_ns.py)."""
+    from test_gpu_ns import _mat, _ritz_ok
+    g = golden(fixture)
+    env0 = dict(AHIP_FOLD_NS="0")
+    fo = _solve(tmp_path, fixture, 1)
+    un = _solve_env(tmp_path, fixture, env0)
+    for k in ("iters", "nopx", "info"):
+        assert int(fo[k]) == int(un[k]), k
+    assert int(fo["iters"]) == int(g["iparam"][2])
+    assert abs(int(fo["nrorth"]) - int(un["nrorth"])) <= 2
+    nconv = int(g["iparam"][4])
+    ref = g["ritzr"][:nconv] + 1j * g["ritzi"][:nconv]
+    _ritz_ok(_mat(g["spec"]), fo["d"], ref, str(g["which"]), float(g["tol"]))
+
+
+def test_folded_arnoldi_forced_refinement(tmp_path, golden):
+    """Every step takes the second DGKS refinement (the parked folded step's
+    host path, kFinFoldCoef2 with the Hessenberg daxpy): the reference's
+    cycles and OP*x count, and the forced RCI driver's."""
+    fixture = "n7_convdiff_real"
+    g = golden(fixture)
+    fo = _solve_env(tmp_path, fixture, dict(AHIP_FORCE_DGKS2="1"), "free")
+    rc = _solve_env(tmp_path, fixture, dict(AHIP_FORCE_DGKS2="1"), "rci")
+    assert int(fo["nitref"]) > 0
+    for k in ("iters", "nopx", "nitref", "nrorth", "info"):
+        assert int(fo[k]) == int(rc[k]), k
+    assert int(fo["iters"]) == int(g["iparam"][2]) and int(fo["nopx"]) == int(g["iparam"][8])
+    np.testing.assert_array_equal(fo["d"], rc["d"])
