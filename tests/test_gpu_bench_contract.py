@@ -1,0 +1,46 @@
+"""GPU: bench.py's output contract -- stdout carries exactly ONE JSON line
+(rank 0's), also when RCCL (its version banner) and gloo (a connect message
+per rank) are initialised, and for N > 1 ranks under torch.distributed.run.
+Small operator sizes; the N > 1 case rehearses on one GPU through the
+host-staged transport (every rank on device 0)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--rows", "300000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+         "--no-full-storage"]
+
+
+def _one_json(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, lines[:5]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "dtype", "config", "roofline"):
+        assert k in d, k
+    assert d["value"] > 0 and d["steps"] == 2
+    return d
+
+
+def test_single_rank_with_rccl_communicator():
+    r = subprocess.run([sys.executable, "bench.py", *SMALL, "--force-dist"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _one_json(r.stdout)
+    assert d["n_gpus"] == 1
+
+
+def test_two_ranks_one_json_line():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", "29531", "bench.py", "--gpus", "2", "--host-transport",
+                        *SMALL], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _one_json(r.stdout)
+    assert d["n_gpus"] == 2 and "REHEARSAL" in d["config"]["parallelism"]
