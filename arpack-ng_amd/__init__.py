@@ -569,6 +569,16 @@ class ZCSR:
             raise RuntimeError("gen_zrandom failed")
         return cls(h.value)
 
+    def matvec(self, x):
+        """y = A x for a host complex vector (through HBM; arpack_hip_zcsr_spmv --
+        the XCD column-split kernel when the operator qualifies)."""
+        xv = np.ascontiguousarray(x, np.complex128).view(np.float64)
+        xb, yb = DeviceBuffer(2 * self.n), DeviceBuffer(2 * self.n)
+        xb.write(xv)
+        if lib().arpack_hip_zcsr_spmv(self.h, _ptr(xb), _ptr(yb)) != 0:
+            raise RuntimeError("zcsr spmv failed")
+        return yb.numpy().view(np.complex128).copy()
+
     def download(self):
         rp = np.zeros(self.n + 1, np.int64)
         col = np.zeros(self.nnz, np.int32)

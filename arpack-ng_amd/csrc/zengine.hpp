@@ -42,7 +42,26 @@ struct ZCsr {
     const int32_t* col = nullptr;
     const double* val = nullptr;  // interleaved complex
     bool owned = false;
+    // XCD column split (zsplit.hip, zcsr_build_split): the columns cut into 8
+    // slices of sw; slice s's entries as a CSR of their own (int32 row offsets
+    // s_rp[s*(n+1) + r] relative to s_base[s]), slice-relative columns (16 bit
+    // when sw <= 65536), partial products y_s in s_y (8 x n complex)
+    bool split = false;
+    int64_t s_w = 0;
+    bool s_col16 = true;
+    int32_t* s_rp = nullptr;
+    int64_t* s_base = nullptr;  // 9 (device)
+    void* s_col = nullptr;
+    double* s_val = nullptr;
+    double* s_y = nullptr;
 };
+// Build the XCD column split of A when it pays (n >= 2^18: x larger than one
+// XCD's L2; >= 32 entries a row: the partials' 256 B a row stay small against
+// the row's stream); AHIP_ZSPLIT=0 disables.  0: built, 1: not applicable, < 0: error.
+int zcsr_build_split(ZCsr& A);
+void zcsr_free_split(ZCsr& A);
+// y = A x through the split (8 slice launches in one grid + the fixed-order combine)
+void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Ws& ws);
 // Launchers over the component type R of the interleaved complex vectors

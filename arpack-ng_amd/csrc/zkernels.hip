@@ -440,6 +440,7 @@ void ws_destroy(Ws& ws) {
 }
 
 void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y) {
+    if (A.split) return zcsr_split_spmv(s, A, x, y);  // zsplit.hip
     hipLaunchKernelGGL(k_zcsr, dim3(grid(A.n * 64, 65536)), dim3(kB), 0, s, A.n, A.rowptr, A.col,
                        reinterpret_cast<const double2*>(A.val), reinterpret_cast<const double2*>(x),
                        reinterpret_cast<double2*>(y));

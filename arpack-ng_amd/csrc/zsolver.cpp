@@ -978,7 +978,16 @@ int arpack_hip_zcsr_create(arpack_hip_zcsr** out, int64_t n, int64_t nnz, const 
     (void)hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault);
     (void)hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault);
     (void)hipMemcpy(v, val, sizeof(double) * 2 * nnz, hipMemcpyDefault);
-    Z->A = ahip::zdev::ZCsr{n, nnz, rp, c, v, true};
+    Z->A.n = n;
+    Z->A.nnz = nnz;
+    Z->A.rowptr = rp;
+    Z->A.col = c;
+    Z->A.val = v;
+    Z->A.owned = true;
+    if (ahip::zdev::zcsr_build_split(Z->A) < 0) {  // XCD column split when it pays
+        arpack_hip_zcsr_destroy(Z);
+        return -1;
+    }
     *out = Z;
     return 0;
 }
@@ -989,12 +998,17 @@ int arpack_hip_gen_zrandom(arpack_hip_zcsr** out, int64_t n, int per_row, uint32
         delete Z;
         return -1;
     }
+    if (ahip::zdev::zcsr_build_split(Z->A) < 0) {
+        arpack_hip_zcsr_destroy(Z);
+        return -1;
+    }
     *out = Z;
     return 0;
 }
 
 void arpack_hip_zcsr_destroy(arpack_hip_zcsr* Z) {
     if (!Z) return;
+    ahip::zdev::zcsr_free_split(Z->A);
     if (Z->A.owned) {
         (void)hipFree((void*)Z->A.rowptr);
         (void)hipFree((void*)Z->A.col);

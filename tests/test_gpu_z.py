@@ -102,3 +102,23 @@ def test_zrandom_generator_bitwise(pkg):
         rp, col, val = M.zrandom(n, per, seed, 100.0)
         drp, dcol, dval = pkg.ZCSR.random(n, per, seed, 100.0).download()
         assert np.array_equal(rp, drp) and np.array_equal(col, dcol) and np.array_equal(val, dval)
+
+
+@pytest.mark.parametrize("n,per,seed", [(300000, 64, 7), (100000, 64, 7), (524289, 40, 3)])
+def test_zcsr_spmv_xcd_split(pkg, n, per, seed):
+    """Complex CSR SpMV: the XCD column-split kernel (zsplit.hip; n >= 2^18 and
+    >= 32 entries a row -- the first and third case, the third with 32-bit
+    slice columns since n/8 > 65536) and the wave-per-row kernel (second case)
+    against SciPy's product of the downloaded operator (different summation
+    orders: relative 1e-13)."""
+    import scipy.sparse as sp
+    Z = pkg.ZCSR.random(n, per, seed, 100.0)
+    rp, col, val = Z.download()
+    A = sp.csr_matrix((val, col, rp), shape=(n, n))
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    y = Z.matvec(x)
+    yref = A @ x
+    assert np.abs(y - yref).max() <= 1e-13 * np.abs(yref).max()
+    Z2 = pkg.ZCSR.from_arrays(rp, col, val)  # the arpack_hip_zcsr_create path
+    assert np.array_equal(Z2.matvec(x), y)
