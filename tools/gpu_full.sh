@@ -1,6 +1,6 @@
 # Full GPU suite + bench at the driver's settings, each step under its own limit.
 set -o pipefail
-TAG=${1:-r02c}
+TAG=${1:-full}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > gpurun_out/${TAG}_gputests.log 2>&1 || { tail -30 gpurun_out/${TAG}_gputests.log; exit 1; }

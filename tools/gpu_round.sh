@@ -1,7 +1,7 @@
 # Round profile set of the folded build: new fold tests, bench at the driver's
 # settings, kernel trace + PMC passes (tools/profile_round.sh), config sweep.
 set -o pipefail
-TAG=${1:-r02r}
+TAG=${1:-round}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_fold.py > gpurun_out/${TAG}_fold_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_fold_tests.log; exit 1; }

@@ -1,7 +1,7 @@
 # Rank-share cycle rates of the folded build (scaling estimate) and the cost of
 # the distributed machinery on a 1-rank RCCL communicator.
 set -o pipefail
-TAG=${1:-r02f}
+TAG=${1:-shares}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 for rows in 10000000 5000000 2500000 1250000; do
