@@ -7,10 +7,11 @@ iterations per second of the MI355X engine's dsaupd on the north-star operator
         nev = 10, ncv = 30, fp64, generated directly in HBM (synthetic data).
 
 A "step" is ONE implicit-restart cycle = one increment of iparam(3): np = 20
-Lanczos steps (CSR SpMV + classical Gram-Schmidt + DGKS against V) followed by
-the host shift selection and the on-device V*Q update (dsapps).  The whole loop
-runs on the GPU through arpack_hip_dsaupd_csr_cycles (the engine parks every K
-cycles so exactly K cycles sit inside the timed region).
+Lanczos steps (CSR SpMV + classical Gram-Schmidt + DGKS against V, the DGKS
+sweep folded into the next step's passes: two passes over V per step, DESIGN.md
+§2) followed by the host shift selection and the on-device V*Q update (dsapps).
+The whole loop runs on the GPU through arpack_hip_dsaupd_csr_cycles (the engine
+parks every K cycles so exactly K cycles sit inside the timed region).
 
 OP: the operator is symmetric (dsaupd's contract), so by default the CSR is
 declared symmetric and the SpMV streams only its upper triangle
