@@ -640,11 +640,13 @@ class ZRci:
         o = int(self.ipntr[k]) - 1
         return self.workd[o:o + self.n]
 
-    def eupd(self, rvec=True, howmny="A", sigma=0j):
-        """zneupd_c: returns (d, Z (n x nconv), nconv)."""
+    def eupd(self, rvec=True, howmny="A", sigma=0j, z=None):
+        """zneupd_c: returns (d, Z (n x nconv), nconv); `z` may be self.v (Z = V,
+        as the reference's drivers call it)."""
         nconv = int(self.iparam[4])
         d = np.zeros(self.nev + 1, self.ct)
-        z = np.zeros((self.nev + 1) * self.n, self.ct)
+        if z is None:
+            z = np.zeros((self.nev + 1) * self.n, self.ct)
         select = np.zeros(self.ncv, np.int32)
         workev = np.zeros(2 * self.ncv, self.ct)
         info = np.zeros(1, np.int32)
@@ -660,7 +662,7 @@ class ZRci:
           self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data, _ip(info))
         if info[0] < 0:
             raise ArpackError("zneupd", int(info[0]))
-        return d[:nconv], z.reshape(self.nev + 1, self.n)[:nconv].T, nconv
+        return d[:nconv], z[:nconv * self.n].reshape(nconv, self.n).T, nconv
 
     @property
     def ritz(self):

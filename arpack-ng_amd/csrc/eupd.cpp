@@ -244,14 +244,16 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
                                  a.stream);
             dev::ger_cols(a.stream, n, nconv, a.d_resid, ws.coef, zd, ldzd);
         }
+        // V first, then Z: with Z = V (the reference's drivers pass v for z) the
+        // purified Ritz vectors must be what V(:,1:nconv) holds on return
+        if (a.host_mode)  // the reference leaves V * Q in V (dorm2r in place)
+            (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
         if (!zdev) {
             (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
                                    sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
             (void)hipFreeAsync(zd, a.stream);
         }
-        if (a.host_mode)  // the reference leaves V * Q in V (dorm2r in place)
-            (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
-                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
         a.sync();
     }
     return 0;

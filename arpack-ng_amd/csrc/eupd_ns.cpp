@@ -300,14 +300,16 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out
         (void)hipMemcpy2DAsync(zd, sizeof(R) * ldzd, a.d_v, sizeof(R) * a.d_ld,
                                sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
     }
+    // V first, then Z: a caller may pass Z = V (the reference's drivers do),
+    // and the reference then leaves the Ritz vectors in V(:,1:nconv)
+    if (a.host_mode)  // the reference leaves V*Qh (the Schur basis) in V
+        (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, ncv, hipMemcpyDeviceToHost, a.stream);
     if (!zdev) {
         (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
                                sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
         (void)hipFreeAsync(zd, a.stream);
     }
-    if (a.host_mode)  // the reference leaves V*Qh (the Schur basis) in V
-        (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
-                               sizeof(R) * n, ncv, hipMemcpyDeviceToHost, a.stream);
     a.sync();
     return 0;
 }

@@ -815,7 +815,11 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
         zd = reinterpret_cast<R*>(z);
         ldzd = ldz;
     } else {
-        (void)hipMalloc(&zd, sizeof(CT) * (size_t)ldc * nconv);
+        if (hipMalloc(&zd, sizeof(CT) * (size_t)ldc * nconv) != hipSuccess) {
+            zdev::ws_destroy(ws);
+            a.release();
+            return -9999;
+        }
     }
     if (howmny == 'A') {
         zdev::gemm(ws, n, a.d_v, ldc, nconv, nconv, X.data(), zd, ldzd);
@@ -824,13 +828,14 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
         (void)hipMemcpy2DAsync(zd, sizeof(CT) * ldzd, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, nconv,
                                hipMemcpyDeviceToDevice, a.stream);
     }
+    // V first, then Z: a caller may pass Z = V (the reference's drivers do)
+    if (a.host_mode)
+        (void)hipMemcpy2DAsync(v, sizeof(CT) * ldv, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, ncv,
+                               hipMemcpyDeviceToHost, a.stream);
     if (!zdevp) {
         (void)hipMemcpy2DAsync(z, sizeof(CT) * ldz, zd, sizeof(CT) * ldc, sizeof(CT) * n, nconv,
                                hipMemcpyDeviceToHost, a.stream);
     }
-    if (a.host_mode)
-        (void)hipMemcpy2DAsync(v, sizeof(CT) * ldv, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, ncv,
-                               hipMemcpyDeviceToHost, a.stream);
     a.sync();
     if (!zdevp) (void)hipFree(zd);
     zdev::ws_destroy(ws);

@@ -90,3 +90,49 @@ def test_dnaupd_modes(pkg, golden, name):
     lam, ref = dr + 1j * di, g["dr"] + 1j * g["di"]
     for x in ref:
         assert np.abs(lam - x).min() <= 1e-9 * np.abs(ref).max(), (x, lam)
+
+
+# Z = V: the reference's drivers pass v for z (TESTS/bug_58_double.f:294,
+# EXAMPLES/NONSYM/dndrv2.f), and the reference then leaves the Ritz vectors in
+# V(:,1:nconv). The vectors must be the ones a separate Z receives, bit for bit.
+@pytest.mark.parametrize("name", ["m2_sym_std_si", "m7_ns_std_si"])
+def test_eupd_z_aliases_v(pkg, golden, name):
+    g = golden(name)
+    n = int(g["n"])
+    out = []
+    for alias in (False, True):
+        c = _caller(g, name)
+        cls = pkg.SymRci if name in SYM else pkg.NsRci
+        s = cls(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat=c.bmat,
+                mode=c.mode, mxiter=300, v0=g["v0"])
+        _drive(s, c, n)
+        zarg = s.v if alias else None
+        if name in SYM:
+            d, z, nconv = s.eupd(sigma=float(g["sigma"]), z=zarg)
+        else:
+            d, _, z, nconv = s.eupd(sigmar=float(g["sigma"]), z=zarg)
+        out.append((d.copy(), np.array(z[:nconv * n]).copy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def test_zneupd_z_aliases_v(pkg, golden):
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+    from oracle import matrices as M
+    g = golden("z3_zrandom_si")
+    rp, col, val = M.zrandom(*(int(x) for x in g["spec"][1:4]), float(g["spec"][4]))
+    n = len(rp) - 1
+    A = sp.csr_matrix((val, col, rp), shape=(n, n))
+    lu = spl.splu(A.tocsc())
+    out = []
+    for alias in (False, True):
+        s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
+                     mxiter=int(g["mxiter"]), v0=g["v0"])
+        while (ido := s.aupd()) in (-1, 1):
+            s.slice(1)[:] = lu.solve(s.slice(0).copy())
+        assert ido == 99
+        d, z, nconv = s.eupd(sigma=complex(g["sigma"]), z=s.v if alias else None)
+        out.append((d.copy(), z.copy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
