@@ -449,6 +449,10 @@ int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int ncl
 }
 
 void sstats_c(void) { g_stats = Stats{}; }
+// dstatn / cstatn (SRC/dstatn.f, SRC/cstatn.f): the same counters; the family
+// timers they also clear read 0 in this build (see stat_c)
+void sstatn_c(void) { g_stats = Stats{}; }
+void cstatn_c(void) { g_stats = Stats{}; }
 
 void stat_c(int* nopx, int* nbx, int* nrorth, int* nitref, int* nrstrt, float* tsaupd,
             float* tsaup2, float* tsaitr, float* tseigt, float* tsgets, float* tsapps,

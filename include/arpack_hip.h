@@ -177,6 +177,8 @@ void dseupd_(a_int* rvec, char const* howmny, a_int* select, double* d, double* 
 
 /* ---- statistics / debug (ICB/stat_c.h, ICB/debug_c.h; stat.h:8-21) ---------- */
 void sstats_c(void);
+void sstatn_c(void);
+void cstatn_c(void);
 void stat_c(a_int* nopx, a_int* nbx, a_int* nrorth, a_int* nitref, a_int* nrstrt,
             float* tsaupd, float* tsaup2, float* tsaitr, float* tseigt, float* tsgets,
             float* tsapps, float* tsconv, float* tnaupd, float* tnaup2, float* tnaitr,

@@ -25,7 +25,7 @@ def test_reference_icb_names_covered():
     for fam in ("ds", "dn", "zn", "ss", "sn", "cn"):  # all twelve ICB entry points
         for s in (fam + "aupd_c", fam + "eupd_c", fam + "aupd_", fam + "eupd_"):
             assert s in names, s
-    for s in ("stat_c", "debug_c", "sstats_c"):
+    for s in ("stat_c", "debug_c", "sstats_c", "sstatn_c", "cstatn_c"):
         assert s in names
 
 
@@ -63,3 +63,63 @@ def test_ilp64_library_exports_reference_abi():
 def test_version_and_no_gpu_probe(pkg):
     assert "gfx950" in pkg.version()
     assert pkg.device_count() >= 0
+
+
+CPP_CALLER = r"""
+#include <complex>
+#include <vector>
+#include "arpack.hpp"
+#include "debug_c.hpp"
+#include "stat_c.hpp"
+template <class R> void sym() {
+    a_int ido = 0, info = 0, ip[11] = {}, pt[14] = {};
+    std::vector<R> r(8), v(64), w(24), l(64), d(2), z(16);
+    std::vector<a_int> sel(8);
+    arpack::saupd(ido, arpack::bmat::identity, 8, arpack::which::largest_algebraic, 2, R(0),
+                  r.data(), 4, v.data(), 8, ip, pt, w.data(), l.data(), 48, info);
+    arpack::seupd(1, arpack::howmny::ritz_vectors, sel.data(), d.data(), z.data(), 8, R(0),
+                  arpack::bmat::identity, 8, arpack::which::largest_algebraic, 2, R(0), r.data(), 4,
+                  v.data(), 8, ip, pt, w.data(), l.data(), 48, info);
+    arpack::naupd(ido, arpack::bmat::identity, 8, arpack::which::largest_real, 2, R(0), r.data(),
+                  4, v.data(), 8, ip, pt, w.data(), l.data(), 48, info);
+    arpack::neupd(1, arpack::howmny::ritz_vectors, sel.data(), d.data(), d.data(), z.data(), 8,
+                  R(0), R(0), w.data(), arpack::bmat::identity, 8, arpack::which::largest_real, 2,
+                  R(0), r.data(), 4, v.data(), 8, ip, pt, w.data(), l.data(), 48, info);
+    std::vector<std::complex<R>> c(64);
+    std::vector<R> rw(4);
+    arpack::naupd(ido, arpack::bmat::identity, 8, arpack::which::largest_magnitude, 2, R(0),
+                  c.data(), 4, c.data(), 8, ip, pt, c.data(), c.data(), 48, rw.data(), info);
+    arpack::neupd(0, arpack::howmny::ritz_vectors, sel.data(), c.data(), c.data(), 8,
+                  std::complex<R>(0), c.data(), arpack::bmat::identity, 8,
+                  arpack::which::largest_magnitude, 2, R(0), c.data(), 4, c.data(), 8, ip, pt,
+                  c.data(), c.data(), 48, rw.data(), info);
+}
+int main() {
+    sym<float>();
+    sym<double>();
+    a_int a[5];
+    float t[26];
+    stat_c(a[0], a[1], a[2], a[3], a[4], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], t[8],
+           t[9], t[10], t[11], t[12], t[13], t[14], t[15], t[16], t[17], t[18], t[19], t[20], t[21],
+           t[22], t[23], t[24], t[25]);
+    sstatn_c();
+    cstatn_c();
+    debug_c(6, -6, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1);
+    return 0;
+}
+"""
+
+
+def test_cpp_caller_compiles_and_links(pkg, tmp_path):
+    """A C++ caller of the reference's C++ binding (ICB/arpack.hpp, debug_c.hpp,
+    stat_c.hpp; the pattern of TESTS/icb_arpack_cpp.cpp) builds unchanged
+    against include/ and links libarpack_hip.so (every overload instantiated)."""
+    import subprocess
+    src = tmp_path / "caller.cpp"
+    src.write_text(CPP_CALLER)
+    lib = os.path.join(ROOT, "arpack-ng_amd")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-O1", "-I",
+                        os.path.join(ROOT, "include"), str(src), "-L", lib, "-larpack_hip",
+                        "-Wl,-rpath," + lib, "-o", str(tmp_path / "caller")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -1,6 +1,7 @@
 """GPU: the reference's own test programs (TESTS/bug_142.f, bug_142_gen.f,
-bug_58_double.f, bug_1323.f, bug_79_double_complex.f, dnsimp.f) linked against
-libarpack_hip.so instead of the reference library.
+bug_58_double.f, bug_1323.f, bug_79_double_complex.f, dnsimp.f, and the ICB
+tests icb_arpack_c.c, icb_arpack_cpp.cpp, bug_1315_double.c, bug_1315_single.c)
+linked against libarpack_hip.so instead of the reference library.
 
 The programs are compiled from the reference's sources by oracle/Makefile
 (`reftests`, in the container: the sources do not exist on the GPU box) into
@@ -31,6 +32,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "oracle", "_ref", "tests")
 GOLD = os.path.join(ROOT, "tests", "golden", "reftests")
 TESTS = ["bug_142", "bug_142_gen", "bug_58_double", "bug_1323", "bug_79_double_complex", "dnsimp"]
+# the C / C++ ICB tests, compiled against include/arpack.h / arpack.hpp (the
+# reference's ICB layer is not built here): their own acceptance checks --
+# analytic eigenvalues of diagonal operators, exit status 0 -- are the oracle
+ICB_TESTS = ["icb_arpack_c", "icb_arpack_cpp", "bug_1315_double", "bug_1315_single"]
 
 ROW = re.compile(r"^\s*Row\s+\d+:\s+(.*)$")
 COUNTS = {"nconv": r"converged Ritz values is\s+(\d+)",
@@ -101,3 +106,13 @@ def test_reference_program(name, tmp_path):
         assert abs(counts["nconv"] - ref_counts["nconv"]) <= 1, (counts, ref_counts)
     else:
         assert counts == ref_counts, (name, counts, ref_counts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ICB_TESTS)
+def test_reference_icb_program(name, tmp_path):
+    exe = os.path.join(BIN, name + "_hip")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/tests not built (make -C oracle reftests, needs /root/reference)")
+    r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout[-3000:], r.stderr[-2000:])
