@@ -149,7 +149,9 @@ def test_reference_program(name, tmp_path):
 
 # EXAMPLES/{SIMPLE,SYM,NONSYM,COMPLEX,SVD,BAND}: every driver of the reference,
 # all four precisions. They run at tol = 0 (machine precision), where the
-# restart count is rounding-driven: OP*x and cycles within
+# restart count is rounding-driven (the reference's own count
+# moves under a one-ulp change of the start vector, test_reference_sensitivity.py):
+# OP*x and cycles within
 # 15% (double) / 25% (single) of the reference's, converged count equal, the
 # Ritz values and residuals as _compare says. (znbdr2 / cnbdr2 end in info = -9
 # in the reference -- a zero start vector -- and must end the same way here.)
