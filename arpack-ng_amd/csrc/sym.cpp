@@ -557,12 +557,23 @@ void SolverT<R>::sapps(int kev, int npk) {
 template <class R>
 void SolverT<R>::vq_device(int kev, int kplusp, double sigmak, double betak) {
     const double* q = workl + iq;
-    std::vector<double> qbuf((size_t)kplusp * (kev + 1));  // compact, ld = kplusp
+    // Q(:,1:kev+1) compact (ld = kplusp). ncv <= 64: staged in the pinned
+    // ws.host_hcol (ncv^2 >= kplusp (kev+1)), so the copy is asynchronous and
+    // the kFinNorm finalize queues behind V*Q without a host wait; the buffer
+    // is free again at the read_state() sync that follows every restart (its
+    // next writer is the folded Arnoldi cycle's H upload in saitr).
+    const size_t m = (size_t)kplusp * (kev + 1);
+    std::vector<double> qvec;
+    double* qbuf = ws.host_hcol;
+    if (!qbuf) {
+        qvec.resize(m);
+        qbuf = qvec.data();
+    }
     for (int c = 0; c <= kev && c < kplusp; ++c)
         for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
-    ck(hipMemcpyAsync(ws.q, qbuf.data(), sizeof(double) * qbuf.size(), hipMemcpyHostToDevice, a.stream));
+    ck(hipMemcpyAsync(ws.q, qbuf, sizeof(double) * m, hipMemcpyHostToDevice, a.stream));
     dev::vq_update(ws, n, a.d_v, a.d_ld, kplusp, kev, sigmak, betak, a.d_resid);
-    a.sync();  // qbuf lifetime
+    if (!ws.host_hcol) a.sync();  // pageable qvec: its lifetime
 }
 
 template <class R>

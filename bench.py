@@ -195,10 +195,24 @@ def main():
     # the timed region, the remaining cycles run on a fresh solve (pre-allocated;
     # its start vector and initial factorisation are timed too), so K is always
     # exactly K restart cycles.
-    def timed_run():
+    def warm_solve(w):
+        """A solve after w untimed restart cycles, and the cycles it has done
+        (a solve that converges inside the warmup is replaced by a fresh one)."""
         s = solver(0.0, 300)
         assert cycles(s, 0) == 98                # getv0 + initial nev-step factorization
-        cycles(s, args.warmup)                   # warmup cycles
+        done = 0
+        while w > 0:
+            if cycles(s, w) == 98:
+                done += w
+                break
+            w -= int(s.iparam[2]) - done         # converged after that many more cycles
+            s = solver(0.0, 300)
+            assert cycles(s, 0) == 98
+            done = 0
+        return s, done
+
+    def timed_run():
+        s, wdone = warm_solve(args.warmup)       # warmup cycles
         spare = solver(0.0, 300)
         pkg.synchronize()
         if dist:
@@ -207,7 +221,7 @@ def main():
         t0 = time.perf_counter()
         ido = cycles(s, args.steps)              # the timed region: nothing but the solve
         cur, nopx, nsolves = s, 0, 1
-        left = 0 if ido == 98 else args.steps - (int(s.iparam[2]) - args.warmup)
+        left = 0 if ido == 98 else args.steps - (int(s.iparam[2]) - wdone)
         while True:
             nopx += pkg.stats()["nopx"] - it0    # dstats restarts with every solve
             if left <= 0:
@@ -244,9 +258,7 @@ def main():
         pk = args.steps
         if ido != 98:
             del s
-            s = solver(0.0, 300)
-            cycles(s, 0)
-            cycles(s, args.warmup)
+            s, _ = warm_solve(min(args.warmup, 5))
             pk = min(args.steps, 10)
         pkg.profile(True)
         pkg.profile_read()
