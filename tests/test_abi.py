@@ -123,3 +123,17 @@ def test_cpp_caller_compiles_and_links(pkg, tmp_path):
                         "-Wl,-rpath," + lib, "-o", str(tmp_path / "caller")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_stat_resets_without_gpu(pkg):
+    """sstats_c / sstatn_c / cstatn_c (ICB/stat_c.h) clear the counters stat_c reads;
+    no GPU call involved."""
+    import ctypes
+    L = pkg.lib()
+    for f in ("sstats_c", "sstatn_c", "cstatn_c"):
+        getattr(L, f)()
+        ints = [ctypes.c_int(7) for _ in range(5)]
+        flts = [ctypes.c_float(7.0) for _ in range(26)]
+        L.stat_c(*[ctypes.byref(x) for x in ints + flts])
+        assert [x.value for x in ints] == [0] * 5, f
+        assert [x.value for x in flts] == [0.0] * 26, f
