@@ -36,6 +36,8 @@ TESTS = ["bug_142", "bug_142_gen", "bug_58_double", "bug_1323", "bug_79_double_c
 # the C / C++ ICB tests, compiled against include/arpack.h / arpack.hpp (the
 # reference's ICB layer is not built here): their own acceptance checks --
 # analytic eigenvalues of diagonal operators, exit status 0 -- are the oracle
+# (each also built as the reference's INTERFACE64 build compiles it, against the
+# ILP64 library)
 ICB_TESTS = ["icb_arpack_c", "icb_arpack_cpp", "bug_1315_double", "bug_1315_single"]
 
 ROW = re.compile(r"^\s*Row\s+\d+:\s+(.*)$")
@@ -167,9 +169,10 @@ def test_reference_example(name, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("abi", ["hip", "hip64"])  # hip64: a_int = int64_t, libarpack_hip64.so
 @pytest.mark.parametrize("name", ICB_TESTS)
-def test_reference_icb_program(name, tmp_path):
-    exe = os.path.join(BIN, name + "_hip")
+def test_reference_icb_program(name, abi, tmp_path):
+    exe = os.path.join(BIN, name + "_" + abi)
     if not os.path.exists(exe):
         pytest.skip("oracle/_ref/tests not built (make -C oracle reftests, needs /root/reference)")
     r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120)
