@@ -804,6 +804,12 @@ def comm_destroy():
     lib().arpack_hip_comm_destroy()
 
 
+def comm_failed() -> bool:
+    """True once a collective of the engine's communicator failed
+    (arpack_hip_comm_failed); the solves then end with info = -9999."""
+    return lib().arpack_hip_comm_failed() != 0
+
+
 def partition_rows(n: int, nranks: int, rank: int):
     """Contiguous balanced row blocks (PARPACK/TESTS/MPI/icb_parpack_c.c:60-77)."""
     base, rem = divmod(n, nranks)

@@ -245,10 +245,23 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         }
     }
     if (csr) S->pause_budget = max_cycles;
+    // a failed collective (RCCL / transport error) ends the solve with
+    // info = -9999 at the next return to the caller: the ranks' sums no longer
+    // agree.  Every rank's communicator reports the failure of a collective it
+    // took part in, so the ranks stop at the same return.
+    auto comm_broken = [&]() {
+        if (!S->dist || !comm_failed(S->dist->comm)) return false;
+        S->a.sync();
+        *info = -9999;
+        *ido = 99;
+        g_sym.erase(v);
+        return true;
+    };
     for (;;) {
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
+        if (r.ido != -1 && r.ido != 1 && comm_broken()) return;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
             // it); a row-distributed SpMV also holds its halo exchange: marker mode
@@ -266,10 +279,12 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park
             // the caller may free or reuse its arrays before resuming: drain
             S->a.sync();
+            if (comm_broken()) return;
             *ido = r.ido;
             return;
         }
         // hand the request to the caller
+        if ((r.ido == -1 || r.ido == 1) && comm_broken()) return;
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
             S->a.d2h_workd(r.x, n);
             if (r.ido == 1 && r.bx >= 0 && S->mode >= 3) S->a.d2h_workd(r.bx, n);
@@ -283,6 +298,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         return;
     }
     // ido = 99: dsaupd post-processing (SRC/dsaupd.f:613-627)
+    if (comm_broken()) return;
     *ido = 99;
     iparam[2] = S->mxiter;
     iparam[4] = S->np;

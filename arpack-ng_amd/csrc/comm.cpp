@@ -14,6 +14,9 @@ namespace ahip {
 struct Comm {
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1, device = 0;
+    uint64_t gen = 0;          // distinguishes communicators created at the same address
+    double* d_flag = nullptr;  // device scratch of dist_all_ok (allocated at init)
+    int failed = 0;            // sticky: a collective or the transport reported an error
     // host-staged transport (arpack_hip_comm_init_host): the launcher's own
     // collectives move the scalars and halos through host memory
     arpack_hip_host_allreduce_fn h_allreduce = nullptr;
@@ -23,27 +26,76 @@ struct Comm {
 };
 
 static Comm* g_comm = nullptr;
+static uint64_t g_gen = 0;
 
 Comm* comm_get() { return g_comm; }
 int comm_rank(const Comm* c) { return c ? c->rank : 0; }
 int comm_size(const Comm* c) { return c ? c->nranks : 1; }
+uint64_t comm_gen(const Comm* c) { return c ? c->gen : 0; }
+bool comm_alive(const Comm* c, uint64_t gen) { return c && c == g_comm && c->gen == gen; }
+double* comm_flag(const Comm* c) { return c ? c->d_flag : nullptr; }
 
-void comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream) {
-    if (!c) return;
+// Record an RCCL / HIP failure of a collective: the communicator is marked
+// failed and the engine's drivers turn that into info = -9999 at their next
+// return (a failed collective leaves the ranks' sums inconsistent, so the solve
+// cannot continue).
+static void note(const Comm* c, bool ok) {
+    if (!ok) const_cast<Comm*>(c)->failed = 1;
+}
+
+int comm_failed(const Comm* c) {
+    if (!c) return 0;
+    if (!c->failed && c->nccl) {
+        ncclResult_t a = ncclSuccess;
+        if (ncclCommGetAsyncError(c->nccl, &a) != ncclSuccess ||
+            (a != ncclSuccess && a != ncclInProgress))
+            const_cast<Comm*>(c)->failed = 1;
+    }
+    return c->failed;
+}
+
+int comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream) {
+    if (!c) return 0;
     if (c->h_allreduce) {
         auto* m = const_cast<Comm*>(c);
         m->h_buf.resize((size_t)count);
-        (void)hipMemcpyAsync(m->h_buf.data(), dev, sizeof(double) * count, hipMemcpyDeviceToHost,
-                             stream);
-        (void)hipStreamSynchronize(stream);
+        bool ok = hipMemcpyAsync(m->h_buf.data(), dev, sizeof(double) * count,
+                                 hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                  hipStreamSynchronize(stream) == hipSuccess;
+        // the transport is collective: call it even after a local failure so the
+        // other ranks are not left waiting; the failure is recorded
         c->h_allreduce(m->h_buf.data(), count, c->h_ctx);
-        (void)hipMemcpyAsync(dev, m->h_buf.data(), sizeof(double) * count, hipMemcpyHostToDevice,
-                             stream);
-        (void)hipStreamSynchronize(stream);
-        return;
+        ok = ok &&
+             hipMemcpyAsync(dev, m->h_buf.data(), sizeof(double) * count, hipMemcpyHostToDevice,
+                            stream) == hipSuccess &&
+             hipStreamSynchronize(stream) == hipSuccess;
+        note(c, ok);
+        return ok ? 0 : -1;
     }
-    if (!c->nccl) return;
-    (void)ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, c->nccl, stream);
+    if (!c->nccl) return 0;
+    const bool ok =
+        ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, c->nccl, stream) == ncclSuccess;
+    note(c, ok);
+    return ok ? 0 : -1;
+}
+
+static Comm* comm_new(int nranks, int rank, int device) {
+    auto* c = new Comm;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    c->gen = ++g_gen;
+    if (hipMalloc(&c->d_flag, sizeof(double)) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+static void comm_free(Comm* c) {
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->d_flag) (void)hipFree(c->d_flag);
+    delete c;
 }
 
 }  // namespace ahip
@@ -58,16 +110,16 @@ int arpack_hip_comm_unique_id(char* out) {
 }
 
 int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
-    auto* c = new ahip::Comm;
-    c->rank = rank;
-    c->nranks = nranks;
-    c->device = device;
+    auto* c = ahip::comm_new(nranks, rank, device);
+    if (!c) return -2;
     {   // a 1-rank communicator is real too, so the distributed path runs on one GPU
         ncclUniqueId uid;
         std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
         if (ncclCommInitRank(&c->nccl, nranks, uid, rank) != ncclSuccess) {
-            delete c;
+            c->nccl = nullptr;
+            ahip::comm_free(c);
             return -1;
         }
     }
@@ -80,10 +132,8 @@ int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn
                               arpack_hip_host_halo_fn halo, void* ctx, int device) {
     if (!allreduce || !halo || nranks < 1 || rank < 0 || rank >= nranks) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
-    auto* c = new ahip::Comm;
-    c->rank = rank;
-    c->nranks = nranks;
-    c->device = device;
+    auto* c = ahip::comm_new(nranks, rank, device);
+    if (!c) return -2;
     c->h_allreduce = allreduce;
     c->h_halo = halo;
     c->h_ctx = ctx;
@@ -94,18 +144,19 @@ int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn
 
 void arpack_hip_comm_destroy(void) {
     if (!ahip::g_comm) return;
-    if (ahip::g_comm->nccl) (void)ncclCommDestroy(ahip::g_comm->nccl);
-    delete ahip::g_comm;
+    ahip::comm_free(ahip::g_comm);
     ahip::g_comm = nullptr;
 }
+
+int arpack_hip_comm_failed(void) { return ahip::comm_failed(ahip::g_comm); }
 
 int arpack_hip_comm_rank(void) { return ahip::comm_rank(ahip::g_comm); }
 int arpack_hip_comm_size(void) { return ahip::comm_size(ahip::g_comm); }
 
 // In-place SUM allreduce of a device buffer (test hook for the RCCL plumbing).
 int arpack_hip_comm_allreduce(double* dev, int count) {
-    ahip::comm_allreduce_sum(ahip::g_comm, dev, count, nullptr);
-    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+    const int rc = ahip::comm_allreduce_sum(ahip::g_comm, dev, count, nullptr);
+    return rc == 0 && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
 }  // extern "C"
@@ -119,13 +170,19 @@ static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s, bool h
     const int64_t hlo = r > 0 && !hi_only ? D.halo_lo : 0, hhi = r < P - 1 ? D.halo_hi : 0;
     std::vector<double> b((size_t)(slo + shi + hlo + hhi));
     double *bsl = b.data(), *bsh = bsl + slo, *brl = bsh + shi, *brh = brl + hlo;
-    if (slo) (void)hipMemcpyAsync(bsl, D.x_mid(), 8 * slo, hipMemcpyDeviceToHost, s);
-    if (shi) (void)hipMemcpyAsync(bsh, D.x_mid() + D.nloc - shi, 8 * shi, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    c->h_halo(bsl, slo, brl, hlo, bsh, shi, brh, hhi, c->h_ctx);
-    if (hlo) (void)hipMemcpyAsync(D.x_ext, brl, 8 * hlo, hipMemcpyHostToDevice, s);
-    if (hhi) (void)hipMemcpyAsync(D.x_mid() + D.nloc, brh, 8 * hhi, hipMemcpyHostToDevice, s);
-    (void)hipStreamSynchronize(s);
+    bool ok = true;
+    if (slo) ok = ok && hipMemcpyAsync(bsl, D.x_mid(), 8 * slo, hipMemcpyDeviceToHost, s) == hipSuccess;
+    if (shi)
+        ok = ok && hipMemcpyAsync(bsh, D.x_mid() + D.nloc - shi, 8 * shi, hipMemcpyDeviceToHost, s) ==
+                       hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    c->h_halo(bsl, slo, brl, hlo, bsh, shi, brh, hhi, c->h_ctx);  // collective: always joined
+    if (hlo) ok = ok && hipMemcpyAsync(D.x_ext, brl, 8 * hlo, hipMemcpyHostToDevice, s) == hipSuccess;
+    if (hhi)
+        ok = ok && hipMemcpyAsync(D.x_mid() + D.nloc, brh, 8 * hhi, hipMemcpyHostToDevice, s) ==
+                       hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    note(c, ok);
 }
 
 // Forward "spill" of the symmetric-storage SpMV: send nsend doubles to rank+1,
@@ -137,17 +194,21 @@ void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, 
     const int64_t ns = r < P - 1 ? nsend : 0, nr = r > 0 ? nrecv : 0;
     if (c->h_halo) {
         std::vector<double> b((size_t)(ns + nr));
-        if (ns) (void)hipMemcpyAsync(b.data(), send, 8 * ns, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
+        bool ok = true;
+        if (ns) ok = hipMemcpyAsync(b.data(), send, 8 * ns, hipMemcpyDeviceToHost, s) == hipSuccess;
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
         c->h_halo(nullptr, 0, b.data() + ns, nr, b.data(), ns, nullptr, 0, c->h_ctx);
-        if (nr) (void)hipMemcpyAsync(recv, b.data() + ns, 8 * nr, hipMemcpyHostToDevice, s);
-        (void)hipStreamSynchronize(s);
+        if (nr)
+            ok = ok && hipMemcpyAsync(recv, b.data() + ns, 8 * nr, hipMemcpyHostToDevice, s) == hipSuccess;
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
+        note(c, ok);
         return;
     }
-    (void)ncclGroupStart();
-    if (ns) (void)ncclSend(send, (size_t)ns, ncclDouble, r + 1, c->nccl, s);
-    if (nr) (void)ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, c->nccl, s);
-    (void)ncclGroupEnd();
+    bool ok = ncclGroupStart() == ncclSuccess;
+    if (ns) ok = ncclSend(send, (size_t)ns, ncclDouble, r + 1, c->nccl, s) == ncclSuccess && ok;
+    if (nr) ok = ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, c->nccl, s) == ncclSuccess && ok;
+    ok = ncclGroupEnd() == ncclSuccess && ok;
+    note(c, ok);
 }
 
 // hi_only: the symmetric-storage SpMV reads x only at and above its own rows,
@@ -156,18 +217,19 @@ void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only) {
     if (!c || c->nranks == 1) return;
     if (c->h_halo) return comm_halo_host(c, D, s, hi_only);
     const int r = c->rank, P = c->nranks;
-    (void)ncclGroupStart();
+    bool ok = ncclGroupStart() == ncclSuccess;
+    auto chk = [&](ncclResult_t e) { ok = ok && e == ncclSuccess; };
     if (r > 0) {
-        if (D.send_lo) (void)ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, c->nccl, s);
-        if (D.halo_lo && !hi_only)
-            (void)ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, c->nccl, s);
+        if (D.send_lo) chk(ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, c->nccl, s));
+        if (D.halo_lo && !hi_only) chk(ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, c->nccl, s));
     }
     if (r < P - 1) {
         if (D.send_hi && !hi_only)
-            (void)ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, c->nccl, s);
-        if (D.halo_hi) (void)ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, c->nccl, s);
+            chk(ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, c->nccl, s));
+        if (D.halo_hi) chk(ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, c->nccl, s));
     }
-    (void)ncclGroupEnd();
+    chk(ncclGroupEnd());
+    note(c, ok);
 }
 
 }  // namespace ahip

@@ -177,19 +177,63 @@ int grid_of(int64_t n) {
     return (int)(g < 1 ? 1 : g);
 }
 
-// counts[0..rows) -> rowptr[0..rows] (exclusive scan, rowptr[rows] = nnz)
+// counts[0..rows) -> rowptr[0..rows] (exclusive scan, rowptr[rows] = nnz).
+// Returns nnz, or -2 when the scan's scratch cannot be allocated / any HIP call
+// fails (the caller frees its buffers and reports the error).
 int64_t scan_counts(int64_t rows, int64_t* counts_then_rowptr_tmp, int64_t* rowptr) {
     void* tmp = nullptr;
     size_t bytes = 0;
-    (void)hipMemset(counts_then_rowptr_tmp + rows, 0, sizeof(int64_t));
-    (void)hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1);
-    (void)hipMalloc(&tmp, bytes);
-    (void)hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1);
-    (void)hipDeviceSynchronize();
+    if (hipMemset(counts_then_rowptr_tmp + rows, 0, sizeof(int64_t)) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1) !=
+            hipSuccess ||
+        hipMalloc(&tmp, bytes) != hipSuccess)
+        return -2;
+    const bool ok =
+        hipcub::DeviceScan::ExclusiveSum(tmp, bytes, counts_then_rowptr_tmp, rowptr, rows + 1) ==
+            hipSuccess &&
+        hipDeviceSynchronize() == hipSuccess;
     (void)hipFree(tmp);
     int64_t nnz = 0;
-    (void)hipMemcpy(&nnz, rowptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost);
+    if (!ok || hipMemcpy(&nnz, rowptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return -2;
     return nnz;
+}
+
+// Count -> scan -> fill of a generated operator: `count(cnt)` writes the row
+// counts, `fill(rp, col, val)` the entries.  Every allocation and launch is
+// checked; on failure nothing leaks and -2 is returned.
+template <class Count, class Fill>
+int build_generated(int64_t rows, Count count, Fill fill, int64_t** rp_out, int32_t** col_out,
+                    double** val_out, int64_t* nnz_out) {
+    int64_t *cnt = nullptr, *rp = nullptr;
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    auto fail = [&]() {
+        (void)hipFree(cnt);
+        (void)hipFree(rp);
+        (void)hipFree(col);
+        (void)hipFree(val);
+        return -2;
+    };
+    if (hipMalloc(&cnt, sizeof(int64_t) * (rows + 1)) != hipSuccess ||
+        hipMalloc(&rp, sizeof(int64_t) * (rows + 1)) != hipSuccess)
+        return fail();
+    count(cnt);
+    if (hipGetLastError() != hipSuccess) return fail();
+    const int64_t nnz = scan_counts(rows, cnt, rp);
+    (void)hipFree(cnt);
+    cnt = nullptr;
+    if (nnz < 0) return fail();
+    if (hipMalloc(&col, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) != hipSuccess ||
+        hipMalloc(&val, sizeof(double) * (nnz > 0 ? nnz : 1)) != hipSuccess)
+        return fail();
+    fill(rp, col, val);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fail();
+    *rp_out = rp;
+    *col_out = col;
+    *val_out = val;
+    *nnz_out = nnz;
+    return 0;
 }
 
 // LDS x-window tables, then the SELL-64 layout over them (default kernel);
@@ -229,13 +273,18 @@ int arpack_hip_csr_create(arpack_hip_csr** out, int64_t n, int64_t nnz, const in
     int64_t* rp = nullptr;
     int32_t* c = nullptr;
     double* v = nullptr;
-    if (hipMalloc(&rp, sizeof(int64_t) * (n + 1)) || hipMalloc(&c, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) ||
-        hipMalloc(&v, sizeof(double) * (nnz > 0 ? nnz : 1)))
+    bool ok = hipMalloc(&rp, sizeof(int64_t) * (n + 1)) == hipSuccess &&
+              hipMalloc(&c, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) == hipSuccess &&
+              hipMalloc(&v, sizeof(double) * (nnz > 0 ? nnz : 1)) == hipSuccess &&
+              hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault) == hipSuccess;
+    if (ok && nnz > 0)
+        ok = hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault) == hipSuccess &&
+             hipMemcpy(v, val, sizeof(double) * nnz, hipMemcpyDefault) == hipSuccess;
+    if (!ok) {
+        (void)hipFree(rp);
+        (void)hipFree(c);
+        (void)hipFree(v);
         return -1;
-    (void)hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault);
-    if (nnz > 0) {
-        (void)hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault);
-        (void)hipMemcpy(v, val, sizeof(double) * nnz, hipMemcpyDefault);
     }
     *out = finish(n, n, nnz, rp, c, v);
     return 0;
@@ -243,6 +292,7 @@ int arpack_hip_csr_create(arpack_hip_csr** out, int64_t n, int64_t nnz, const in
 
 void arpack_hip_csr_destroy(arpack_hip_csr* A) {
     if (!A) return;
+    ahip_dist_detach_csr(A->dist);
     (void)hipFree(A->rowptr);
     (void)hipFree(A->col);
     (void)hipFree(A->val);
@@ -269,10 +319,12 @@ int arpack_hip_csr_info(const arpack_hip_csr* A, int64_t* n, int64_t* nnz) {
 }
 
 int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* col, double* val) {
-    (void)hipMemcpy(rowptr, A->rowptr, sizeof(int64_t) * (A->A.n + 1), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(col, A->col, sizeof(int32_t) * A->A.nnz, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(val, A->val, sizeof(double) * A->A.nnz, hipMemcpyDeviceToHost);
-    return 0;
+    const bool ok =
+        hipMemcpy(rowptr, A->rowptr, sizeof(int64_t) * (A->A.n + 1), hipMemcpyDeviceToHost) == hipSuccess &&
+        (A->A.nnz == 0 ||
+         (hipMemcpy(col, A->col, sizeof(int32_t) * A->A.nnz, hipMemcpyDeviceToHost) == hipSuccess &&
+          hipMemcpy(val, A->val, sizeof(double) * A->A.nnz, hipMemcpyDeviceToHost) == hipSuccess));
+    return ok ? 0 : -1;
 }
 
 int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
@@ -288,7 +340,15 @@ static void csr_full_storage(arpack_hip_csr* A) {
 }
 
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
+    // one rank's block of a distributed operator: the symmetric SpMV changes the
+    // exchange pattern (hi-only halo + forward spill), so the switch -- either
+    // way -- is collective, and every rank falls back to full storage if any
+    // rank's plan failed
+    bool stale = false;
+    const ahip::Comm* c = ahip_csr_dist_comm(A, &stale);
+    if (stale) return -3;  // its communicator was destroyed: no agreement possible
     if (!on) {
+        if (c && !ahip::dist_all_ok(c, 1)) return -2;
         csr_full_storage(A);
         return 0;
     }
@@ -296,10 +356,7 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     if (!A->symsell)
         rc = ahip::dev::csr_build_symsell(A->A, A->ncols, A->sym_coff, A->sym_spill_in,
                                           A->sym_spill_out, &A->symsell);
-    // one rank's block of a distributed operator: the symmetric SpMV changes the
-    // exchange pattern (hi-only halo + forward spill), so the switch is collective
-    // and every rank falls back to full storage if any rank's plan failed
-    if (A->dist_comm && !ahip::dist_all_ok(A->dist_comm, rc == 0)) {
+    if (c && !ahip::dist_all_ok(c, rc == 0)) {
         csr_full_storage(A);
         return rc != 0 ? rc : -2;
     }
@@ -359,17 +416,21 @@ double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, 
 static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, double disorder = 0.0,
                    uint32_t seed = 0) {
     const int64_t n = dim == 2 ? m * m : m * m * m;
-    int64_t *cnt = nullptr, *rp = nullptr;
-    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, cnt);
-    const int64_t nnz = scan_counts(n, cnt, rp);
-    (void)hipFree(cnt);
+    int64_t *rp = nullptr, nnz = 0;
     int32_t* col = nullptr;
     double* val = nullptr;
-    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim, scale, disorder,
-                       seed, rp, col, val);
-    (void)hipDeviceSynchronize();
+    const int rc = build_generated(
+        n,
+        [&](int64_t* cnt) {
+            hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim,
+                               cnt);
+        },
+        [&](int64_t* rp_, int32_t* col_, double* val_) {
+            hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim,
+                               scale, disorder, seed, rp_, col_, val_);
+        },
+        &rp, &col, &val, &nnz);
+    if (rc != 0) return rc;
     *out = finish(n, n, nnz, rp, col, val);
     return 0;
 }
@@ -382,17 +443,21 @@ int arpack_hip_gen_convdiff2d(arpack_hip_csr** out, int64_t m, double rho) {
     const double h = 1.0 / (double)(m + 1), h2 = h * h;
     const double dd = 4.0 / h2, dl = -1.0 / h2 - 0.5 * rho / h, du = -1.0 / h2 + 0.5 * rho / h;
     const double offy = -1.0 / (1.0 / (double)((m + 1) * (m + 1)));
-    int64_t *cnt = nullptr, *rp = nullptr;
-    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, 2, cnt);
-    const int64_t nnz = scan_counts(n, cnt, rp);
-    (void)hipFree(cnt);
+    int64_t *rp = nullptr, nnz = 0;
     int32_t* col = nullptr;
     double* val = nullptr;
-    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_cd_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dd, dl, du, offy,
-                       rp, col, val);
-    (void)hipDeviceSynchronize();
+    const int rc = build_generated(
+        n,
+        [&](int64_t* cnt) {
+            hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, 2,
+                               cnt);
+        },
+        [&](int64_t* rp_, int32_t* col_, double* val_) {
+            hipLaunchKernelGGL(ahip::gen::k_cd_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dd, dl,
+                               du, offy, rp_, col_, val_);
+        },
+        &rp, &col, &val, &nnz);
+    if (rc != 0) return rc;
     *out = finish(n, n, nnz, rp, col, val);
     return 0;
 }
@@ -405,21 +470,24 @@ int arpack_hip_gen_banded_sym(arpack_hip_csr** out, int64_t n, int64_t r0, int64
                               int bandwidth, int per_row) {
     if (r1 <= r0 || r1 > n || bandwidth < 2) return -1;
     const int64_t rows = r1 - r0;
-    int64_t *cnt = nullptr, *rp = nullptr;
-    if (hipMalloc(&cnt, sizeof(int64_t) * (rows + 1)) || hipMalloc(&rp, sizeof(int64_t) * (rows + 1))) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_band_count, dim3(grid_of(rows)), dim3(256), 0, nullptr, n, r0, r1, seed,
-                       bandwidth, per_row, cnt);
-    const int64_t nnz = scan_counts(rows, cnt, rp);
-    (void)hipFree(cnt);
+    int64_t *rp = nullptr, nnz = 0;
     int32_t* col = nullptr;
     double* val = nullptr;
-    if (hipMalloc(&col, sizeof(int32_t) * nnz) || hipMalloc(&val, sizeof(double) * nnz)) return -1;
-    hipLaunchKernelGGL(ahip::gen::k_band_fill, dim3(grid_of(rows)), dim3(256), 0, nullptr, n, r0, r1, seed,
-                       bandwidth, per_row, rp, col, val);
-    (void)hipDeviceSynchronize();
+    const int rc = build_generated(
+        rows,
+        [&](int64_t* cnt) {
+            hipLaunchKernelGGL(ahip::gen::k_band_count, dim3(grid_of(rows)), dim3(256), 0, nullptr, n,
+                               r0, r1, seed, bandwidth, per_row, cnt);
+        },
+        [&](int64_t* rp_, int32_t* col_, double* val_) {
+            hipLaunchKernelGGL(ahip::gen::k_band_fill, dim3(grid_of(rows)), dim3(256), 0, nullptr, n,
+                               r0, r1, seed, bandwidth, per_row, rp_, col_, val_);
+        },
+        &rp, &col, &val, &nnz);
+    if (rc != 0) return rc;
     *out = finish(rows, n, nnz, rp, col, val);
     (*out)->row_begin = r0;
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return 0;
 }
 
 }  // extern "C"
@@ -447,15 +515,18 @@ __global__ void k_col_span(int64_t nnz, const int32_t* col, int* mn, int* mx) {
 
 int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax) {
     int* d = nullptr;
-    if (hipMalloc(&d, 2 * sizeof(int))) return -1;
+    if (hipMalloc(&d, 2 * sizeof(int)) != hipSuccess) return -1;
     const int init[2] = {0x7fffffff, -1};
-    (void)hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice);
-    if (A->A.nnz > 0)
+    int h[2];
+    bool ok = hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess;
+    if (ok && A->A.nnz > 0) {
         hipLaunchKernelGGL(k_col_span, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz, A->col, d,
                            d + 1);
-    int h[2];
-    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    ok = ok && hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
     (void)hipFree(d);
+    if (!ok) return -1;
     *cmin = h[0];
     *cmax = h[1];
     return 0;
@@ -464,7 +535,7 @@ int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax) {
 int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     if (A->A.nnz > 0 && shift != 0)
         hipLaunchKernelGGL(k_shift_cols, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz, A->col, shift);
-    (void)hipDeviceSynchronize();
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
     A->ncols = ncols;
     if (A->win) (void)hipFree(A->win);
     if (A->sell) (void)hipFree(A->sell);

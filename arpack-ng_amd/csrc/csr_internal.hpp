@@ -7,6 +7,7 @@
 namespace ahip {
 struct Comm;
 }
+struct arpack_hip_dist;
 
 struct arpack_hip_csr {
     ahip::dev::Csr A;
@@ -25,13 +26,19 @@ struct arpack_hip_csr {
     int64_t sym_coff = 0, sym_spill_in = 0, sym_spill_out = 0;
     // set by arpack_hip_dist_create: the CSR is one rank's block of a row-
     // distributed operator, so a storage-mode switch must be agreed by all ranks
-    const ahip::Comm* dist_comm = nullptr;
+    // (cleared by arpack_hip_dist_destroy)
+    arpack_hip_dist* dist = nullptr;
 };
 
 namespace ahip {
 // collective over the ranks of c: 1 if every rank passes ok_local != 0
 int dist_all_ok(const Comm* c, int ok_local);
 }
+
+// the live communicator of A's distribution (nullptr if A is not distributed
+// or, with *stale = true, if that communicator has been destroyed)
+const ahip::Comm* ahip_csr_dist_comm(const arpack_hip_csr* A, bool* stale);
+void ahip_dist_detach_csr(arpack_hip_dist* D);
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV
 // analysis for an x vector of length ncols; 0 on success

@@ -32,18 +32,19 @@ void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
 
 int dist_all_ok(const Comm* c, int ok_local) {
     if (!c || comm_size(c) == 1) return ok_local != 0;
-    double h = ok_local ? 0.0 : 1.0, *d = nullptr;  // SUM of failures
-    if (hipMalloc(&d, sizeof(double))) return 0;  // (cannot happen on a sane device)
-    (void)hipMemcpy(d, &h, sizeof(double), hipMemcpyHostToDevice);
-    comm_allreduce_sum(c, d, 1, nullptr);
-    (void)hipMemcpy(&h, d, sizeof(double), hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    return h == 0.0;
+    // the communicator's own device double: no allocation that could fail on
+    // one rank only, so every rank always joins the collective
+    double h = ok_local ? 0.0 : 1.0, *d = comm_flag(c);  // SUM of failures
+    bool ok = hipMemcpy(d, &h, sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    if (comm_allreduce_sum(c, d, 1, nullptr) != 0) ok = false;
+    ok = ok && hipMemcpy(&h, d, sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+    return ok && h == 0.0;
 }
 }  // namespace ahip
 
 struct arpack_hip_dist {
     ahip::DistOp D;
+    arpack_hip_csr* csr = nullptr;  // the operator block it remapped (cleared if freed first)
 };
 
 extern "C" {
@@ -90,11 +91,17 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     tab[4 * r + 2] = (double)cmin;
     tab[4 * r + 3] = (double)cmax;
     double* d = nullptr;
-    if (hipMalloc(&d, sizeof(double) * tab.size())) return -1;
-    (void)hipMemcpy(d, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice);
-    comm_allreduce_sum(c, d, (int)tab.size(), nullptr);
-    (void)hipMemcpy(tab.data(), d, sizeof(double) * tab.size(), hipMemcpyDeviceToHost);
+    int ok_tab = hipMalloc(&d, sizeof(double) * tab.size()) == hipSuccess;
+    if (!dist_all_ok(c, ok_tab)) {
+        if (d) (void)hipFree(d);
+        return -1;
+    }
+    ok_tab = hipMemcpy(d, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice) == hipSuccess;
+    if (comm_allreduce_sum(c, d, (int)tab.size(), nullptr) != 0) ok_tab = 0;
+    if (hipMemcpy(tab.data(), d, sizeof(double) * tab.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        ok_tab = 0;
     (void)hipFree(d);
+    if (!dist_all_ok(c, ok_tab)) return -1;
     int64_t plan[4];
     const int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
     if (rc != 0) return rc;
@@ -108,6 +115,7 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     o.send_lo = plan[2];
     o.send_hi = plan[3];
     o.comm = c;
+    o.comm_gen = comm_gen(c);
     const int64_t next = o.halo_lo + nloc + o.halo_hi;
     // local column indices relative to x_ext; a failure on any rank fails the
     // call on every rank (the later collectives would otherwise mismatch)
@@ -129,9 +137,11 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     // and every rank's plan succeeds (arpack_hip_csr_set_symmetric is collective
     // from here on); otherwise every rank runs the full-storage SpMV (the remap
     // above already reset the kernel)
-    A->dist_comm = c;
-    if (dist_all_ok(c, was_sym)) (void)arpack_hip_csr_set_symmetric(A, 1);
     o.A = &A->A;
+    D->csr = A;
+    if (A->dist) A->dist->csr = nullptr;  // a re-distributed block: the old handle lets go
+    A->dist = D;
+    if (dist_all_ok(c, was_sym)) (void)arpack_hip_csr_set_symmetric(A, 1);
     *out = D;
     return 0;
 }
@@ -147,6 +157,7 @@ int arpack_hip_dist_rows(arpack_hip_dist** out, int64_t nloc, int64_t row0, int6
     D->D.row0 = row0;
     D->D.nloc = nloc;
     D->D.comm = c;
+    D->D.comm_gen = comm_gen(c);
     *out = D;
     return 0;
 }
@@ -162,6 +173,7 @@ int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y) {
 
 void arpack_hip_dist_destroy(arpack_hip_dist* D) {
     if (!D) return;
+    if (D->csr) D->csr->dist = nullptr;  // the CSR is a plain (unsharded) operator again
     (void)hipFree(D->D.x_ext);
     delete D;
 }
@@ -178,3 +190,24 @@ int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* ha
 }  // extern "C"
 
 const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D) { return &D->D; }
+
+// Called by arpack_hip_csr_destroy: the distribution loses its operator.
+void ahip_dist_detach_csr(arpack_hip_dist* D) {
+    if (!D) return;
+    D->csr = nullptr;
+    D->D.A = nullptr;
+}
+
+// The communicator of the distribution A belongs to, if that communicator is
+// still the live one; stale (comm destroyed) -> *stale = true.
+const ahip::Comm* ahip_csr_dist_comm(const arpack_hip_csr* A, bool* stale) {
+    *stale = false;
+    if (!A->dist) return nullptr;
+    const ahip::DistOp& o = A->dist->D;
+    if (!ahip::comm_alive(o.comm, o.comm_gen)) {
+        *stale = true;
+        return nullptr;
+    }
+    return o.comm;
+}
+

@@ -19,8 +19,16 @@ struct Comm;  // RCCL communicator (comm.cpp)
 Comm* comm_get();
 int comm_rank(const Comm*);
 int comm_size(const Comm*);
-// in-place SUM allreduce of `count` doubles on `stream`
-void comm_allreduce_sum(const Comm*, double* dev, int count, hipStream_t stream);
+// in-place SUM allreduce of `count` doubles on `stream`; 0, or -1 after an
+// RCCL / HIP / transport error (also recorded: comm_failed)
+int comm_allreduce_sum(const Comm*, double* dev, int count, hipStream_t stream);
+// nonzero once a collective of c failed (sticky; also polls RCCL's async error)
+int comm_failed(const Comm* c);
+// generation of a communicator and whether (c, gen) is still the live one
+uint64_t comm_gen(const Comm* c);
+bool comm_alive(const Comm* c, uint64_t gen);
+// one device double owned by the communicator (dist_all_ok's scratch)
+double* comm_flag(const Comm* c);
 
 // Distributed operator: the local CSR (columns relative to the start of x_ext)
 // plus the halo plan.
@@ -31,6 +39,7 @@ struct DistOp {
     double* x_ext = nullptr;            // device, halo_lo + nloc + halo_hi
     const dev::Csr* A = nullptr;        // local rows, local (x_ext) column indices
     const Comm* comm = nullptr;
+    uint64_t comm_gen = 0;              // generation of comm at creation
     double* x_mid() const { return x_ext + halo_lo; }
 };
 

@@ -111,7 +111,7 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
         dev::dots(ws, n, 0, a.d_v, a.d_ld, a.d_workd, a.d_workd, -1);
         if (dist && dist->comm) {
             dev::finalize(ws, 1, dev::kFinRaw, 0, 0, -1);
-            comm_allreduce_sum(dist->comm, ws.sums, 1, a.stream);
+            if (comm_allreduce_sum(dist->comm, ws.sums, 1, a.stream) != 0) return -9999;
             dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1, true);
         } else {
             dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);

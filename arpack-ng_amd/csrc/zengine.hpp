@@ -36,6 +36,13 @@ struct Ws {
     int hld = 0;
     double* rec = nullptr;   // ncv + 1
 };
+// widest basis of the device-resident complex step: its finalize keeps 2 doubles
+// per complex slot (j + 1 <= ncv + 1 slots) in dynamic LDS next to ~100 B of
+// static state, within the 64 KB a workgroup may allocate
+constexpr int kMaxDevStepNcv = 4000;
+// The split operator's partial products s_y belong to the operator: one SpMV
+// at a time per ZCsr (the engine's stream); concurrent SpMVs on the same ZCsr
+// from different streams need separate operators.
 struct ZCsr {
     int64_t n = 0, nnz = 0;
     const int64_t* rowptr = nullptr;

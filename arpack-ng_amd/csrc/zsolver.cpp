@@ -259,7 +259,14 @@ Task ZSolverT<R>::naitr(int k, int npk, int& iinfo) {
         const char* e = getenv("AHIP_ZHOST");
         return !(e && e[0] == '1');
     }();
-    if (bmat == 'I' && dev_steps) {
+    // the device finalize stages 2 doubles per complex slot in dynamic LDS
+    // (16 (j+1) B, 64 KB a workgroup): wider bases take the host-driven step
+    static const int dev_max_ncv = [] {  // AHIP_ZDEV_MAXNCV: test hook for the switch
+        const char* e = getenv("AHIP_ZDEV_MAXNCV");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v < zdev::kMaxDevStepNcv ? v : zdev::kMaxDevStepNcv;
+    }();
+    if (bmat == 'I' && dev_steps && ncv <= dev_max_ncv) {
         co_await naitr_dev(k, npk, iinfo);
         if (iinfo > 0) co_return;
     } else
@@ -976,23 +983,25 @@ int arpack_hip_zcsr_create(arpack_hip_zcsr** out, int64_t n, int64_t nnz, const 
     int32_t* c = nullptr;
     double* v = nullptr;
     if (hipMalloc(&rp, sizeof(int64_t) * (n + 1)) || hipMalloc(&c, sizeof(int32_t) * (nnz ? nnz : 1)) ||
-        hipMalloc(&v, sizeof(double) * 2 * (nnz ? nnz : 1))) {
+        hipMalloc(&v, sizeof(double) * 2 * (nnz ? nnz : 1)) ||
+        hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault) ||
+        (nnz && (hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault) ||
+                 hipMemcpy(v, val, sizeof(double) * 2 * nnz, hipMemcpyDefault)))) {
+        (void)hipFree(rp);
+        (void)hipFree(c);
+        (void)hipFree(v);
         delete Z;
         return -1;
     }
-    (void)hipMemcpy(rp, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDefault);
-    (void)hipMemcpy(c, col, sizeof(int32_t) * nnz, hipMemcpyDefault);
-    (void)hipMemcpy(v, val, sizeof(double) * 2 * nnz, hipMemcpyDefault);
     Z->A.n = n;
     Z->A.nnz = nnz;
     Z->A.rowptr = rp;
     Z->A.col = c;
     Z->A.val = v;
     Z->A.owned = true;
-    if (ahip::zdev::zcsr_build_split(Z->A) < 0) {  // XCD column split when it pays
-        arpack_hip_zcsr_destroy(Z);
-        return -1;
-    }
+    // XCD column split when it pays; optional: if it cannot be built (e.g. no
+    // memory for the slices) it is freed and the wave-per-row kernel serves A
+    (void)ahip::zdev::zcsr_build_split(Z->A);
     *out = Z;
     return 0;
 }
@@ -1003,10 +1012,7 @@ int arpack_hip_gen_zrandom(arpack_hip_zcsr** out, int64_t n, int per_row, uint32
         delete Z;
         return -1;
     }
-    if (ahip::zdev::zcsr_build_split(Z->A) < 0) {
-        arpack_hip_zcsr_destroy(Z);
-        return -1;
-    }
+    (void)ahip::zdev::zcsr_build_split(Z->A);  // optional, as in arpack_hip_zcsr_create
     *out = Z;
     return 0;
 }

@@ -226,11 +226,13 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * full-storage kernel.  y is then not bitwise reproducible run to run
  * (transposed terms are summed in LDS in schedule order).  on == 0 restores
  * the full-storage kernel.  For a row-distributed operator (after
- * arpack_hip_dist_create) the call is COLLECTIVE with on = 1: the halo and
- * spill exchanges differ between the modes, so every rank must call it; the
- * ranks agree (one allreduce) and if any rank's plan fails every rank keeps
- * the full-storage kernel and returns nonzero (its own plan error, or -2 when
- * only another rank's plan failed). */
+ * arpack_hip_dist_create, until arpack_hip_dist_destroy) the call is
+ * COLLECTIVE, with on = 1 and with on = 0: the halo and spill exchanges differ
+ * between the modes, so every rank must call it; the ranks agree (one
+ * allreduce) and if any rank's plan fails every rank keeps the full-storage
+ * kernel and returns nonzero (its own plan error, or -2 when only another
+ * rank's plan failed); -3 if the distribution's communicator has been
+ * destroyed. */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
@@ -295,6 +297,12 @@ void arpack_hip_comm_destroy(void);
 int arpack_hip_comm_rank(void);
 int arpack_hip_comm_size(void);
 int arpack_hip_comm_allreduce(double* dev, int count); /* in-place SUM (test hook) */
+/* Nonzero once a collective of the engine's communicator failed (an RCCL call
+ * returned an error, RCCL reported an asynchronous error, or a HIP copy of the
+ * host-staged transport failed).  The solve entry points then return with
+ * info = -9999 at their next return to the caller on every rank whose
+ * communicator saw the failure. */
+int arpack_hip_comm_failed(void);
 /* Host-staged transport in place of RCCL: the engine stages every allreduce
  * (in-place SUM of `count` host doubles) and every halo exchange (send my first
  * nsl / last nsh local entries to rank-1 / rank+1, receive nrl / nrh entries
