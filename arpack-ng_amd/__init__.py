@@ -121,6 +121,12 @@ def _declare(L):
     L.arpack_hip_zcsr_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.arpack_hip_zcsr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_zcsr_spmv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.arpack_hip_zshift_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_double,
+                                           C.c_double, C.c_double, _I]
+    L.arpack_hip_zshift_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_zshift_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, _PD]
+    L.arpack_hip_zshift_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD] * 3
+    L.arpack_hip_znaupd_zshift.argtypes = L.arpack_hip_znaupd_zcsr.argtypes
     L.arpack_hip_profile.argtypes = [_I]
     L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
     L.arpack_hip_synchronize.restype = C.c_int
@@ -587,6 +593,50 @@ class ZCSR:
         return rp, col, val
 
 
+class ZShift:
+    """Shift-invert operator y = (A - sigma I)^{-1} x on the GPU (BiCGStab over the
+    complex CSR operator; arpack_hip_zshift_*): znaupd's mode-3 OP (SRC/znaupd.f:27),
+    the caller-side solve the reference's drivers do with zgttrf/zgttrs
+    (EXAMPLES/COMPLEX/zndrv2.f:179,250)."""
+
+    def __init__(self, A: "ZCSR", sigma=0j, rtol=1e-12, maxit=200):
+        self.A = A  # keeps the operator alive
+        self.sigma = complex(sigma)
+        h = C.c_void_p()
+        rc = lib().arpack_hip_zshift_create(C.byref(h), A.h, self.sigma.real, self.sigma.imag,
+                                            float(rtol), int(maxit))
+        if rc != 0:
+            raise RuntimeError("arpack_hip_zshift_create failed (%d)" % rc)
+        self.h = h.value
+        self.n = A.n
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_zshift_destroy(self.h)
+        except Exception:
+            pass
+
+    def solve(self, x):
+        """y = (A - sigma I)^{-1} x for a host complex vector; returns (y, iters, relres)."""
+        xv = np.ascontiguousarray(x, np.complex128).view(np.float64)
+        xb, yb = DeviceBuffer(2 * self.n), DeviceBuffer(2 * self.n)
+        xb.write(xv)
+        rr = C.c_double()
+        it = lib().arpack_hip_zshift_solve(self.h, _ptr(xb), _ptr(yb), C.byref(rr))
+        if it == -2:
+            raise RuntimeError("zshift solve: HIP error")
+        return yb.numpy().view(np.complex128).copy(), it, rr.value
+
+    def stats(self):
+        a, b, c = C.c_longlong(), C.c_longlong(), C.c_longlong()
+        d, e, f = C.c_double(), C.c_double(), C.c_double()
+        lib().arpack_hip_zshift_stats(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d),
+                                      C.byref(e), C.byref(f))
+        return dict(solves=a.value, iters=b.value, failures=c.value, max_relres=d.value,
+                    ms=e.value, bytes_per_iter=f.value)
+
+
 class ZRci:
     """znaupd/zneupd state (SRC/znaupd.f, SRC/zneupd.f): complex128 arrays,
     ipntr(14), lworkl = 3*ncv^2 + 5*ncv, rwork(ncv).  Host arrays; the caller
@@ -633,6 +683,19 @@ class ZRci:
                                      _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
                                      self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data,
                                      _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
+    def aupd_zshift(self, S: "ZShift"):
+        """Whole loop on the GPU in mode 3 (construct with mode=3): OP =
+        (A - sigma I)^{-1} by the device solve S (arpack_hip_znaupd_zshift)."""
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_znaupd_zshift(S.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                       self.which.encode(), self.nev, C.byref(tol),
+                                       self.resid.ctypes.data, self.ncv, self.v.ctypes.data,
+                                       self.n, _ip(self.iparam), _ip(self.ipntr),
+                                       self.workd.ctypes.data, self.workl.ctypes.data,
+                                       self.lworkl, self.rwork.ctypes.data, _ip(self.info))
         self.tol = tol.value
         return int(self.ido[0])
 

@@ -67,8 +67,10 @@ struct ZCsr {
 // the row's stream); AHIP_ZSPLIT=0 disables.  0: built, 1: not applicable, < 0: error.
 int zcsr_build_split(ZCsr& A);
 void zcsr_free_split(ZCsr& A);
-// y = A x through the split (8 slice launches in one grid + the fixed-order combine)
-void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
+// y = A x through the split (8 slice launches in one grid + the fixed-order combine);
+// gate (device int, may be null): the kernels return at once while *gate != 0
+void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y,
+                     const int* gate = nullptr);
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Ws& ws);
 // Launchers over the component type R of the interleaved complex vectors
@@ -107,7 +109,7 @@ void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int whi
 void step_finalize(const Ws& ws, int m, dev::FinPhase ph, int j, int rstart, int gate);
 template <class R>
 void step_zero_if(const Ws& ws, int64_t n, R* r);
-void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y);
+void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate = nullptr);
 int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift);
 }  // namespace zdev
 

@@ -183,7 +183,9 @@ __global__ void k_zger(int64_t n, int k, const typename C2<R>::T* __restrict__ x
 __global__ __launch_bounds__(kB) void k_zcsr(int64_t n, const int64_t* __restrict__ rp,
                                              const int32_t* __restrict__ col,
                                              const double2* __restrict__ val,
-                                             const double2* __restrict__ x, double2* __restrict__ y) {
+                                             const double2* __restrict__ x, double2* __restrict__ y,
+                                             const int* __restrict__ gate) {
+    if (gate && *gate) return;  // a finished Krylov solve (zsolve.hip) skips its queued products
     const int lane = threadIdx.x & 63;
     const int64_t wid = ((int64_t)blockIdx.x * kB + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * kB) >> 6;
@@ -439,11 +441,11 @@ void ws_destroy(Ws& ws) {
     ws = Ws{};
 }
 
-void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y) {
-    if (A.split) return zcsr_split_spmv(s, A, x, y);  // zsplit.hip
+void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
+    if (A.split) return zcsr_split_spmv(s, A, x, y, gate);  // zsplit.hip
     hipLaunchKernelGGL(k_zcsr, dim3(grid(A.n * 64, 65536)), dim3(kB), 0, s, A.n, A.rowptr, A.col,
                        reinterpret_cast<const double2*>(A.val), reinterpret_cast<const double2*>(x),
-                       reinterpret_cast<double2*>(y));
+                       reinterpret_cast<double2*>(y), gate);
 }
 
 int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift) {

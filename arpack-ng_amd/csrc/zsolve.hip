@@ -1,0 +1,358 @@
+// Device BiCGStab for the shift-invert operator y = (A - sigma I)^{-1} b of the
+// complex engine (mode 3, SRC/znaupd.f:27; see zsolve.hpp for the design).
+//
+// One iteration (k = 0, 1, ...), complex inner products (a, b) = a^H b:
+//
+//   w = A p                      zcsr_spmv (XCD split)          gated
+//   v = w - sigma p;   P0 <- partials of rh^H v               k_bi_v
+//   alpha = rho_k / (rh^H v);   s = r - alpha v               k_bi_s   (reduces P0)
+//   w = A s                      zcsr_spmv                      gated
+//   t = w - sigma s;   P0 <- partials of t^H s, t^H t         k_bi_t
+//   omega = (t^H s)/(t^H t);  y += alpha p + omega s;
+//   r = s - omega t;   P1 <- partials of rh^H r, r^H r        k_bi_xr  (reduces P0)
+//   rho_{k+1} = rh^H r;  stop if ||r|| <= rtol ||b||;
+//   else p = r + (rho_{k+1}/rho_k)(alpha/omega)(p - omega v)  k_bi_p   (reduces P1)
+//
+// Every block of a reducing kernel sums the previous kernel's per-block
+// partials itself, in one fixed order (so all blocks hold the same scalars, and
+// results are reproducible run to run); block 0 records the scalars in the
+// device state for the later kernels.  A kernel never writes the partial
+// buffer it reads (P0 / P1 alternate).  When k_bi_p decides to stop it sets
+// st.done, and every later kernel of the chunk -- the SpMVs included -- returns
+// at once.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/arpack_hip.h"
+#include "zcommon.hpp"
+#include "zsolve.hpp"
+
+namespace ahip::zdev {
+
+namespace {
+using namespace zc;
+constexpr int kT = 256;      // threads a block
+constexpr int kMaxBlk = 512;  // blocks of the vector kernels (partials per slot)
+
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
+    const double d = b.x * b.x + b.y * b.y;
+    return make_double2((a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d);
+}
+
+// per-thread accumulators -> one partial per slot for this block
+template <int NS>
+__device__ __forceinline__ void put_partials(const double (&acc)[NS], double* __restrict__ part,
+                                             int nblk) {
+    __shared__ double red[kT / 64][NS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const double v = wsum(acc[q]);
+        if (lane == 0) red[wave][q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+        const int q = threadIdx.x;
+        part[(int64_t)q * nblk + blockIdx.x] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+    }
+}
+
+// fixed-order total of NS slots of per-block partials (every block, same result)
+template <int NS>
+__device__ __forceinline__ void totals(const double* __restrict__ part, int nblk, double (&out)[NS]) {
+    __shared__ double red[kT / 64][NS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        double a = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kT) a += part[(int64_t)q * nblk + b];
+        a = wsum(a);
+        if (lane == 0) red[wave][q] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NS; ++q) out[q] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+}
+
+__global__ __launch_bounds__(kT) void k_bi_init(int64_t n, const double2* __restrict__ b,
+                                                double2* __restrict__ r, double2* __restrict__ rh,
+                                                double2* __restrict__ p, double2* __restrict__ y,
+                                                double* __restrict__ part, int nblk) {
+    double acc[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 bi = b[i];
+        r[i] = bi;
+        rh[i] = bi;
+        p[i] = bi;
+        y[i] = make_double2(0.0, 0.0);
+        acc[0] += bi.x * bi.x + bi.y * bi.y;
+    }
+    put_partials<1>(acc, part, nblk);
+}
+
+__global__ __launch_bounds__(kT) void k_bi_init_fin(const double* __restrict__ part, int nblk,
+                                                    BiState* __restrict__ st) {
+    double t[1];
+    totals<1>(part, nblk, t);
+    if (threadIdx.x == 0) {
+        st->done = t[0] == 0.0 ? 1 : 0;  // b = 0: y = 0 is exact
+        st->breakdown = 0;
+        st->iters = 0;
+        st->pad = 0;  // failed flag
+        st->rho[0][0] = t[0];
+        st->rho[0][1] = 0.0;
+        st->bnorm2 = t[0];
+        st->rnorm2 = t[0];
+    }
+}
+
+// v = w - sigma p; partials of rh^H v
+__global__ __launch_bounds__(kT) void k_bi_v(int64_t n, const double2* __restrict__ w,
+                                             const double2* __restrict__ p,
+                                             const double2* __restrict__ rh, double2* __restrict__ v,
+                                             double2 sigma, const BiState* __restrict__ st,
+                                             double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 pi = p[i], wi = w[i];
+        const double2 sp = cmul(sigma, pi);
+        const double2 vi = make_double2(wi.x - sp.x, wi.y - sp.y);
+        v[i] = vi;
+        const double2 d = cmulc(rh[i], vi);
+        acc[0] += d.x;
+        acc[1] += d.y;
+    }
+    put_partials<2>(acc, part, nblk);
+}
+
+// alpha = rho_k / (rh^H v); s = r - alpha v
+__global__ __launch_bounds__(kT) void k_bi_s(int64_t n, const double2* __restrict__ r,
+                                             const double2* __restrict__ v, double2* __restrict__ s,
+                                             BiState* __restrict__ st, int k,
+                                             const double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double t[2];
+    totals<2>(part, nblk, t);
+    const double2 d = make_double2(t[0], t[1]);
+    const double2 rho = make_double2(st->rho[k & 1][0], st->rho[k & 1][1]);
+    const bool bd = d.x == 0.0 && d.y == 0.0;
+    const double2 alpha = bd ? make_double2(0.0, 0.0) : cdiv(rho, d);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->alpha[0] = alpha.x;
+        st->alpha[1] = alpha.y;
+        if (bd) st->breakdown = 1;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 ri = r[i], av = cmul(alpha, v[i]);
+        s[i] = make_double2(ri.x - av.x, ri.y - av.y);
+    }
+}
+
+// t = w - sigma s; partials of t^H s (complex), t^H t
+__global__ __launch_bounds__(kT) void k_bi_t(int64_t n, const double2* __restrict__ w,
+                                             const double2* __restrict__ s, double2* __restrict__ t,
+                                             double2 sigma, const BiState* __restrict__ st,
+                                             double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 si = s[i], wi = w[i];
+        const double2 ss = cmul(sigma, si);
+        const double2 ti = make_double2(wi.x - ss.x, wi.y - ss.y);
+        t[i] = ti;
+        const double2 d = cmulc(ti, si);
+        acc[0] += d.x;
+        acc[1] += d.y;
+        acc[2] += ti.x * ti.x + ti.y * ti.y;
+    }
+    put_partials<3>(acc, part, nblk);
+}
+
+// omega = (t^H s)/(t^H t); y += alpha p + omega s; r = s - omega t;
+// partials of rh^H r (complex), r^H r
+__global__ __launch_bounds__(kT) void k_bi_xr(int64_t n, double2* __restrict__ y,
+                                              const double2* __restrict__ p,
+                                              const double2* __restrict__ s,
+                                              const double2* __restrict__ t,
+                                              double2* __restrict__ r,
+                                              const double2* __restrict__ rh,
+                                              BiState* __restrict__ st,
+                                              const double* __restrict__ part_in,
+                                              double* __restrict__ part_out, int nblk) {
+    if (st->done) return;
+    double tt[3];
+    totals<3>(part_in, nblk, tt);
+    // t = 0 (s = 0 exactly): omega = 0, y += alpha p, r = s -- the next test stops
+    const double2 omega = tt[2] > 0.0 ? make_double2(tt[0] / tt[2], tt[1] / tt[2])
+                                      : make_double2(0.0, 0.0);
+    const double2 alpha = make_double2(st->alpha[0], st->alpha[1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->omega[0] = omega.x;
+        st->omega[1] = omega.y;
+    }
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 si = s[i];
+        const double2 ap = cmul(alpha, p[i]), os = cmul(omega, si), ot = cmul(omega, t[i]);
+        const double2 yi = y[i];
+        y[i] = make_double2(yi.x + ap.x + os.x, yi.y + ap.y + os.y);
+        const double2 ri = make_double2(si.x - ot.x, si.y - ot.y);
+        r[i] = ri;
+        const double2 d = cmulc(rh[i], ri);
+        acc[0] += d.x;
+        acc[1] += d.y;
+        acc[2] += ri.x * ri.x + ri.y * ri.y;
+    }
+    put_partials<3>(acc, part_out, nblk);
+}
+
+// rho_{k+1} = rh^H r, convergence test; p = r + beta (p - omega v)
+__global__ __launch_bounds__(kT) void k_bi_p(int64_t n, const double2* __restrict__ r,
+                                             double2* __restrict__ p,
+                                             const double2* __restrict__ v,
+                                             BiState* __restrict__ st, int k, double rtol2,
+                                             const double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double tt[3];
+    totals<3>(part, nblk, tt);
+    const double2 rho1 = make_double2(tt[0], tt[1]);
+    const double2 rho0 = make_double2(st->rho[k & 1][0], st->rho[k & 1][1]);
+    const double2 alpha = make_double2(st->alpha[0], st->alpha[1]);
+    const double2 omega = make_double2(st->omega[0], st->omega[1]);
+    const bool conv = tt[2] <= rtol2 * st->bnorm2;
+    const bool stop = conv || st->breakdown || (omega.x == 0.0 && omega.y == 0.0) ||
+                      (rho1.x == 0.0 && rho1.y == 0.0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rho[(k + 1) & 1][0] = rho1.x;
+        st->rho[(k + 1) & 1][1] = rho1.y;
+        st->rnorm2 = tt[2];
+        if (stop) {
+            st->iters = k + 1;
+            st->pad = conv ? 0 : 1;
+            st->done = 1;
+        }
+    }
+    if (stop) return;
+    const double2 beta = cmul(cdiv(rho1, rho0), cdiv(alpha, omega));
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double2 pi = p[i], ov = cmul(omega, v[i]), ri = r[i];
+        const double2 q = cmul(beta, make_double2(pi.x - ov.x, pi.y - ov.y));
+        p[i] = make_double2(ri.x + q.x, ri.y + q.y);
+    }
+}
+
+}  // namespace
+
+int zshift_create(ZShift& S, const ZCsr* A, std::complex<double> sigma, double rtol, int maxit) {
+    S = ZShift{};
+    S.A = A;
+    S.sigma = sigma;
+    S.rtol = rtol;
+    S.maxit = maxit;
+    S.n = A->n;
+    int64_t g = (S.n + kT - 1) / kT;
+    S.nblk = (int)(g < 1 ? 1 : (g > kMaxBlk ? kMaxBlk : g));
+    const size_t vb = 16 * (size_t)(S.n > 0 ? S.n : 1);
+    hipError_t e = hipSuccess;
+    double** vecs[] = {&S.r, &S.rh, &S.p, &S.v, &S.s, &S.t, &S.w};
+    for (double** q : vecs)
+        if (e == hipSuccess) e = hipMalloc(q, vb);
+    if (e == hipSuccess) e = hipMalloc(&S.part, sizeof(double) * 2 * 4 * (size_t)S.nblk);
+    if (e == hipSuccess) e = hipMalloc(&S.st, sizeof(BiState));
+    if (e == hipSuccess) e = hipHostMalloc(&S.st_host, sizeof(BiState));
+    if (e == hipSuccess) e = hipEventCreate(&S.ev0);
+    if (e == hipSuccess) e = hipEventCreate(&S.ev1);
+    if (e != hipSuccess) {
+        zshift_destroy(S);
+        return (int)e;
+    }
+    std::memset(S.st_host, 0, sizeof(BiState));
+    return 0;
+}
+
+void zshift_destroy(ZShift& S) {
+    double* vecs[] = {S.r, S.rh, S.p, S.v, S.s, S.t, S.w, S.part};
+    for (double* q : vecs)
+        if (q) (void)hipFree(q);
+    if (S.st) (void)hipFree(S.st);
+    if (S.st_host) (void)hipHostFree(S.st_host);
+    if (S.ev0) (void)hipEventDestroy(S.ev0);
+    if (S.ev1) (void)hipEventDestroy(S.ev1);
+    S = ZShift{};
+}
+
+double zshift_iter_bytes(const ZShift& S) {
+    const double n = (double)S.n, nnz = (double)S.A->nnz;
+    const double spmv = 20.0 * nnz + 8.0 * (n + 1) + 32.0 * n;  // val+col, rowptr, x, y
+    return 2.0 * spmv + 336.0 * n;  // + v, s, t, (y, r), p passes (21 complex n-vectors)
+}
+
+int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double* relres) {
+    using D2 = double2;
+    const int64_t n = S.n;
+    const int nb = S.nblk;
+    double* P0 = S.part;
+    double* P1 = S.part + 4 * (size_t)nb;
+    const D2 sig = make_double2(S.sigma.real(), S.sigma.imag());
+    auto* y2 = reinterpret_cast<D2*>(y);
+    auto V = [](double* q) { return reinterpret_cast<D2*>(q); };
+    const int* gate = &S.st->done;
+    if (hipEventRecord(S.ev0, strm) != hipSuccess) return -2;
+    hipLaunchKernelGGL(k_bi_init, dim3(nb), dim3(kT), 0, strm, n, reinterpret_cast<const D2*>(b),
+                       V(S.r), V(S.rh), V(S.p), y2, P0, nb);
+    hipLaunchKernelGGL(k_bi_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
+    const double rtol2 = S.rtol * S.rtol;
+    int k = 0, chunk = S.chunk > 0 ? S.chunk : 4;
+    bool done = false;
+    while (k < S.maxit) {
+        const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
+        for (int q = 0; q < m; ++q, ++k) {
+            zcsr_spmv(strm, *S.A, S.p, S.w, gate);
+            hipLaunchKernelGGL(k_bi_v, dim3(nb), dim3(kT), 0, strm, n, V(S.w), V(S.p), V(S.rh),
+                               V(S.v), sig, S.st, P0, nb);
+            hipLaunchKernelGGL(k_bi_s, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.v), V(S.s), S.st,
+                               k, P0, nb);
+            zcsr_spmv(strm, *S.A, S.s, S.w, gate);
+            hipLaunchKernelGGL(k_bi_t, dim3(nb), dim3(kT), 0, strm, n, V(S.w), V(S.s), V(S.t), sig,
+                               S.st, P0, nb);
+            hipLaunchKernelGGL(k_bi_xr, dim3(nb), dim3(kT), 0, strm, n, y2, V(S.p), V(S.s), V(S.t),
+                               V(S.r), V(S.rh), S.st, P0, P1, nb);
+            hipLaunchKernelGGL(k_bi_p, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.p), V(S.v), S.st,
+                               k, rtol2, P1, nb);
+        }
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(S.st_host, S.st, sizeof(BiState), hipMemcpyDeviceToHost, strm) !=
+                hipSuccess ||
+            hipStreamSynchronize(strm) != hipSuccess)
+            return -2;
+        if (S.st_host->done) {
+            done = true;
+            break;
+        }
+        chunk = 2;  // past the expected count: small chunks, little gated waste
+    }
+    if (hipEventRecord(S.ev1, strm) != hipSuccess || hipEventSynchronize(S.ev1) != hipSuccess)
+        return -2;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) == hipSuccess) S.ms_total += ms;
+    const BiState& h = *S.st_host;
+    const int iters = done ? h.iters : S.maxit;
+    const double rr = h.bnorm2 > 0.0 ? std::sqrt(h.rnorm2 / h.bnorm2) : 0.0;
+    if (relres) *relres = rr;
+    S.n_solves += 1;
+    S.n_iters += iters;
+    if (rr > S.max_relres) S.max_relres = rr;
+    // the next solve enqueues this one's count first (operators repeat: the
+    // shift-invert solves of one Arnoldi run take the same number of steps)
+    S.chunk = iters > 0 ? iters : 1;
+    if (!done || h.pad || (h.bnorm2 > 0.0 && !(h.rnorm2 <= S.rtol * S.rtol * h.bnorm2))) {
+        S.n_fail += 1;
+        return -1;
+    }
+    return iters;
+}
+
+}  // namespace ahip::zdev

@@ -17,6 +17,7 @@
 
 #include "../../include/arpack_hip.h"
 #include "zengine.hpp"
+#include "zsolve.hpp"
 
 namespace ahip {
 
@@ -507,8 +508,9 @@ template <class R>
 static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                    std::complex<R>* resid, int ncv, std::complex<R>* v, int ldv, int* iparam,
                    int* ipntr, std::complex<R>* workd, std::complex<R>* workl, int lworkl,
-                   R* rwork, int* info, const zdev::ZCsr* csr) {
+                   R* rwork, int* info, const zdev::ZCsr* csr, zdev::ZShift* zs = nullptr) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
+    if (zs) csr = zs->A;  // free-running shift-invert: OP = (A - sigma I)^{-1} on the device
     if (kShadow && csr) {
         *info = -9999;
         *ido = 99;
@@ -539,7 +541,8 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         else if (lworkl < 3 * ncv * ncv + 5 * ncv) ierr = -7;
         else if (mode < 1 || mode > 3) ierr = -10;
         else if (mode == 1 && bmat[0] == 'G') ierr = -11;
-        if (csr && (mode != 1 || csr->n != n)) ierr = ierr ? ierr : -11;
+        if (csr && ((zs ? mode != 3 || bmat[0] != 'I' : mode != 1) || csr->n != n))
+            ierr = ierr ? ierr : -11;
         if (ierr != 0) {
             *info = ierr;
             *ido = 99;
@@ -620,7 +623,20 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
         if (S->csr && (r.ido == -1 || r.ido == 1)) {
-            if constexpr (!kShadow) zdev::zcsr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+            if constexpr (!kShadow) {
+                if (!zs) {
+                    zdev::zcsr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+                } else if (zdev::zshift_apply(*zs, S->a.stream, S->op_x, S->op_y, nullptr) < 0) {
+                    // mode 3 (bmat = 'I': B x = x for ido = 1 too): the solve broke
+                    // down or missed its tolerance -- OP is not what the
+                    // caller asked for, so the Arnoldi run stops
+                    S->a.sync();
+                    *info = -9999;
+                    *ido = 99;
+                    g_z.erase(v);
+                    return;
+                }
+            }
             continue;
         }
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
@@ -1053,6 +1069,54 @@ void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* Z, int* ido, char const* bmat
                             int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl, double* rwork, int* info) {
     ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr, (cd*)workd,
                  (cd*)workl, lworkl, rwork, info, &Z->A);
+}
+
+// ---- device shift-invert operator (zsolve.hip) ----
+struct arpack_hip_zshift {
+    ahip::zdev::ZShift S;
+};
+
+int arpack_hip_zshift_create(arpack_hip_zshift** out, const arpack_hip_zcsr* A, double sigma_re,
+                             double sigma_im, double rtol, int maxit) {
+    if (!A || !(rtol > 0.0) || maxit < 1) return -1;
+    auto* Z = new arpack_hip_zshift;
+    if (ahip::zdev::zshift_create(Z->S, &A->A, cd(sigma_re, sigma_im), rtol, maxit) != 0) {
+        delete Z;
+        return -2;
+    }
+    *out = Z;
+    return 0;
+}
+
+void arpack_hip_zshift_destroy(arpack_hip_zshift* Z) {
+    if (!Z) return;
+    ahip::zdev::zshift_destroy(Z->S);
+    delete Z;
+}
+
+int arpack_hip_zshift_solve(arpack_hip_zshift* Z, const double* x, double* y, double* relres) {
+    return ahip::zdev::zshift_apply(Z->S, nullptr, x, y, relres);
+}
+
+int arpack_hip_zshift_stats(const arpack_hip_zshift* Z, long long* solves, long long* iters,
+                            long long* failures, double* max_relres, double* ms,
+                            double* bytes_per_iter) {
+    const auto& S = Z->S;
+    *solves = S.n_solves;
+    *iters = S.n_iters;
+    *failures = S.n_fail;
+    *max_relres = S.max_relres;
+    *ms = S.ms_total;
+    *bytes_per_iter = ahip::zdev::zshift_iter_bytes(S);
+    return 0;
+}
+
+void arpack_hip_znaupd_zshift(arpack_hip_zshift* Z, int* ido, char const* bmat, int n,
+                              char const* which, int nev, double* tol, a_dcomplex* resid, int ncv,
+                              a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                              a_dcomplex* workl, int lworkl, double* rwork, int* info) {
+    ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr,
+                 (cd*)workd, (cd*)workl, lworkl, rwork, info, nullptr, &Z->S);
 }
 
 }  // extern "C"

@@ -63,7 +63,9 @@ __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
                                                      const CT* __restrict__ scol,
                                                      const double2* __restrict__ sval,
                                                      const double2* __restrict__ x,
-                                                     double2* __restrict__ yp) {
+                                                     double2* __restrict__ yp,
+                                                     const int* __restrict__ gate) {
+    if (gate && *gate) return;  // a finished Krylov solve (zsolve.hip) skips its queued products
     typedef double dv2 __attribute__((ext_vector_type(2)));
     const int s = (int)(blockIdx.x % kSlices);  // the XCD this workgroup runs on
     const int64_t q = blockIdx.x / kSlices, nq = gridDim.x / kSlices;
@@ -91,7 +93,9 @@ __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
     }
 }
 
-__global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, double2* __restrict__ y) {
+__global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, double2* __restrict__ y,
+                                 const int* __restrict__ gate) {
+    if (gate && *gate) return;
     for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
         double2 a[kSlices];
 #pragma unroll
@@ -182,17 +186,18 @@ int zcsr_build_split(ZCsr& A) {
     return 0;
 }
 
-void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y) {
+void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
     const auto* x2 = reinterpret_cast<const double2*>(x);
     auto* yp = reinterpret_cast<double2*>(A.s_y);
     const int g = 1024;  // 128 workgroups a slice (tools/zspmv_split.hip)
     if (A.s_col16)
         hipLaunchKernelGGL(k_zsplit_spmv<uint16_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
-                           (const uint16_t*)A.s_col, (const double2*)A.s_val, x2, yp);
+                           (const uint16_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
     else
         hipLaunchKernelGGL(k_zsplit_spmv<int32_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
-                           (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp);
-    hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y));
+                           (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
+    hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y),
+                       gate);
 }
 
 }  // namespace ahip::zdev

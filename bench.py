@@ -89,22 +89,71 @@ def pmc_traffic(kernel_substr: str):
     return v["traffic_bytes"], os.path.basename(files[-1])
 
 
-def cpu_baseline(args):
-    """The reference on the host cores (rank 0, N=1 only), bounded sample."""
-    threads = min(16, len(os.sched_getaffinity(0)))
+def cpu_share():
+    """Host cores for the CPU reference: the box's nproc, this process's affinity
+    set, and the cgroup CPU quota (a GPU box's CPU share is a quota on a larger
+    machine; more threads than the quota only oversubscribe it).  Threads used =
+    min(affinity, quota); without a readable quota, min(affinity,
+    OMP_NUM_THREADS) when the environment sets it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for f in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(f) as fh:
+                parts = fh.read().split()
+            if f.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif f.endswith("quota_us") and parts and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                    quota = int(parts[0]) / int(fh.read().split()[0])
+            if quota:
+                break
+        except (OSError, ValueError, IndexError):
+            continue
+    threads = aff
+    if quota:
+        threads = max(1, min(aff, int(quota)))
+    elif os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = max(1, min(aff, int(os.environ["OMP_NUM_THREADS"])))
+    return dict(nproc=os.cpu_count(), affinity=aff, cgroup_quota=quota, threads=threads)
+
+
+def cpu_baseline(args, cycles):
+    """The reference on the host cores (rank 0, N=1 only): restart cycles
+    1..`cycles` of the same tol=eps solve the GPU's steady-state figure times,
+    and (unless --no-cpu-ttc) the reference's full time-to-converge solve."""
+    share = cpu_share()
+    threads = share["threads"]
     cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--seed",
            str(args.seed), "--bandwidth", str(args.bandwidth), "--per-row", str(args.per_row),
-           "--threads", str(threads)]
+           "--threads", str(threads), "--cycles", str(cycles)]
+    if not args.no_cpu_ttc:
+        cmd.append("--ttc")
     try:
-        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         cb = json.loads(line)
-        return dict(value=cb["iters_per_s"], unit="iters/s", cores=threads, kind="reference",
-                    sample=cb["sample"], lanczos_steps_per_s=cb["lanczos_steps_per_s"],
-                    cycle_s=cb["cycle_s"])
+        out = dict(value=cb["iters_per_s"], unit="iters/s", cores=threads, kind="reference",
+                   sample=cb["sample"], lanczos_steps_per_s=cb["lanczos_steps_per_s"],
+                   cycle_s=cb["cycle_s"], per_cycle_s=cb["per_cycle_s"], cycles=cb["cycles"],
+                   host=share)
+        if "time_to_converge" in cb:
+            out["time_to_converge"] = cb["time_to_converge"]
+        return out
     except Exception as e:  # report, never fake
-        return dict(value=None, unit="iters/s", cores=threads, kind="reference",
+        return dict(value=None, unit="iters/s", cores=threads, kind="reference", host=share,
                     sample="failed: %s" % (str(e)[:200]))
+
+
+def ref_model_bytes(n, nnz, kev, kplusp):
+    """SURVEY.md §8(d)'s byte model of the REFERENCE's arithmetic (full-CSR SpMV
+    with int32 columns, four V passes per Lanczos step -- CGS + DGKS, taken on
+    ~100% of steps here -- and dsapps' V*Q) for one restart cycle k = kev ->
+    kplusp: returns (SpMV bytes per product, bytes per cycle)."""
+    spmv = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n
+    steps = sum(spmv + 32.0 * n * j + 48.0 * n for j in range(kev + 1, kplusp + 1))
+    apps = 8.0 * n * (kplusp + kev + 1) + 16.0 * n
+    return spmv, steps + apps
 
 
 def main():
@@ -120,6 +169,10 @@ def main():
     ap.add_argument("--ncv", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttc", action="store_true")
+    ap.add_argument("--no-cpu-ttc", action="store_true",
+                    help="skip the reference's full time-to-converge solve on the host (~45 s)")
+    ap.add_argument("--steady-cycles", type=int, default=3,
+                    help="restart cycles 1..k of one solve timed on GPU and CPU alike")
     ap.add_argument("--no-full-storage", action="store_true",
                     help="skip the secondary full-storage measurement of --storage sym")
     ap.add_argument("--host-transport", action="store_true",
@@ -280,13 +333,43 @@ def main():
     # full-size GPU test checks this case against the reference (11 cycles,
     # 187 OP*x).  Generated on the host (80 MB) and sliced per rank.
     ttc = None
-    if not args.no_ttc:
+    steady = None
+    v0 = None
+    if not args.no_ttc or args.steady_cycles > 0:
         iseed = np.array([1, 3, 5, 7], np.int32)
         v0 = np.empty(n, np.float64)
         pkg.lib().arpack_hip_kit_dlarnv(iseed.ctypes.data_as(pkg.C.POINTER(pkg.C.c_int)), n,
                                         v0.ctypes.data_as(pkg.C.POINTER(pkg.C.c_double)))
+    # ---- steady state over IDENTICAL cycles: restart cycles 1..k of the tol = eps
+    # solve from the reference's first draw -- the very cycles the CPU baseline
+    # times -- each parked and drained; np of each cycle from the OP*x counts
+    if args.steady_cycles > 0:
+        s3 = pkg.SymRci(nloc, nev, ncv, "LA", 0.0, mxiter=300, device=True, v0=v0[r0:r1])
+        assert cycles(s3, 0) == 98
+        pkg.synchronize()
+        if dist:
+            dist.barrier()
+        nops = []
+        t = time.perf_counter()
+        for _ in range(args.steady_cycles):
+            o0 = pkg.stats()["nopx"]
+            if cycles(s3, 1) != 98:
+                break
+            nops.append(pkg.stats()["nopx"] - o0)
+        pkg.synchronize()
+        secs = time.perf_counter() - t
+        if dist:
+            tt = torch.tensor([secs], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            secs = float(tt.item())
+        if len(nops) == args.steady_cycles:
+            steady = dict(cycles="1..%d" % len(nops), seconds=secs, iters_per_s=len(nops) / secs,
+                          ms_per_cycle=1e3 * secs / len(nops), lanczos_steps=nops,
+                          lanczos_steps_per_s=sum(nops) / secs,
+                          start="dlarnv iseed=(1,3,5,7), tol = eps")
+        del s3
+    if not args.no_ttc:
         s2 = pkg.SymRci(nloc, nev, ncv, "LA", 1e-6, mxiter=300, device=True, v0=v0[r0:r1])
-        del v0
         pkg.synchronize()
         if dist:
             dist.barrier()
@@ -302,6 +385,7 @@ def main():
                    nopx=int(s2.iparam[8]), info=int(s2.info[0]), tol=1e-6,
                    start="dlarnv iseed=(1,3,5,7): the reference's first solve in a fresh process")
         del s2
+    del v0
 
     if prof is None:
         prof = {k: (0.0, 0.0, 0) for k in ("spmv", "cgs_dots", "update", "vq", "place",
@@ -360,6 +444,16 @@ def main():
                                     "same K cycles (events kept out of the timed region)",
                      "read_stream_measured": READ_STREAM_GBS,
                      "frac_of_read_stream": (achieved / READ_STREAM_GBS) if achieved else None,
+                     "bytes_model": ("engine bytes: what the dominant kernel must move in "
+                                     "ITS storage -- upper triangle only, 10 B per stored entry "
+                                     "(8 B value + 2 B window-relative column), x and y 8n each, "
+                                     "+ 4n (the row map) + combine slots; not the reference's "
+                                     "12 B per entry of the full CSR (see reference_model)"
+                                     if storage == "sym" else
+                                     "engine bytes: full CSR in SELL-64 slices, 10 B per stored "
+                                     "entry (8 B value + 2 B window-relative column), x and y 8n "
+                                     "each, + 4n row map"),
+                     "reference_model": None,
                      "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
@@ -368,13 +462,36 @@ def main():
         "storage": storage,
         "full_storage": full_storage,
     }
+    # SURVEY.md §8(d)'s byte model of the reference's arithmetic on the same
+    # product / cycle, divided by OUR times: an "effective" rate that can exceed
+    # the HBM peak, because the engine moves fewer bytes (upper-triangle storage,
+    # 16-bit columns, two V passes a step instead of four)
+    rs, rc = ref_model_bytes(n, nnz, nev, ncv)
+    out["roofline"]["reference_model"] = {
+        "spmv_bytes": rs, "cycle_bytes": rc,
+        "spmv_effective_gbs": rs / (spmv_avg_ms * 1e-3) / 1e9 if cnt else None,
+        "cycle_effective_gbs": (rc / (steady["ms_per_cycle"] * 1e-3) / 1e9) if steady else None,
+        "cycle": "k = %d -> %d (the steady cycles 1..k, np = %d)" % (nev, ncv, ncv - nev),
+        "definition": "SpMV 12 nnz + 4(n+1) + 16n; per Lanczos step j: + 32 n j (CGS + DGKS "
+                      "over V(:,1:j)) + 48 n; per cycle + 8n(kplusp + kev + 1) + 16n (V*Q)"}
+    if steady:
+        out["steady_state"] = steady
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del A
-        out["cpu_baseline"] = cpu_baseline(args)
+        out["cpu_baseline"] = cpu_baseline(args, args.steady_cycles if steady else 1)
+        cb = out["cpu_baseline"]
+        if steady and cb.get("value"):
+            steady["cpu_iters_per_s"] = cb["value"]
+            steady["speedup_same_cycles"] = steady["iters_per_s"] / cb["value"]
+        if ttc and cb.get("time_to_converge"):
+            ttc["cpu_seconds"] = cb["time_to_converge"]["seconds"]
+            ttc["speedup"] = cb["time_to_converge"]["seconds"] / ttc["seconds"]
+            ttc["cpu_same_solve"] = (cb["time_to_converge"]["iters"] == ttc["iters"] and
+                                     cb["time_to_converge"]["nopx"] == ttc["nopx"])
         if out["cpu_baseline"].get("value"):
             out["speedup_vs_cpu"] = iters_per_s / out["cpu_baseline"]["value"]
             # per Lanczos step (OP*x): the GPU's timed cycles run the adapted np
-            # of the solve (nev grows), the CPU sample a first cycle of np = 20
+            # of the solve (nev grows), the CPU sample cycles 1..k of np = 20
             out["speedup_vs_cpu_lanczos_steps"] = \
                 (nopx / elapsed) / out["cpu_baseline"]["lanczos_steps_per_s"]
     if rank == 0:

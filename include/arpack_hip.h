@@ -286,6 +286,36 @@ void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* A, int* ido, char const* bmat
                             a_dcomplex* workd, a_dcomplex* workl, int lworkl, double* rwork,
                             int* info);
 
+/* Shift-invert operator on the device: y = (A - sigma I)^{-1} x by BiCGStab on
+ * the complex CSR operator (complex128; products on the XCD-split SpMV, scalar
+ * recurrences on the device).  The caller-side solve of znaupd's mode 3
+ * (SRC/znaupd.f:27: OP = inv[A - sigma M] M, here M = I), which the reference's
+ * drivers do with a banded LU (EXAMPLES/COMPLEX/zndrv2.f:179,250 zgttrf/zgttrs).
+ * Stops when ||r|| <= rtol ||x|| (r the recursively updated residual) or after
+ * maxit iterations.  A solve object serves one stream at a time. */
+typedef struct arpack_hip_zshift arpack_hip_zshift;
+int arpack_hip_zshift_create(arpack_hip_zshift** S, const arpack_hip_zcsr* A, double sigma_re,
+                             double sigma_im, double rtol, int maxit);
+void arpack_hip_zshift_destroy(arpack_hip_zshift* S);
+/* x, y device pointers (interleaved complex, y != x); synchronous.  Returns the
+ * iterations (>= 0; *relres = ||r||/||x||), -1 if BiCGStab broke down or missed
+ * rtol within maxit, -2 on a HIP error. */
+int arpack_hip_zshift_solve(arpack_hip_zshift* S, const double* x, double* y, double* relres);
+/* Totals over the solves so far: solves, iterations, failures, worst final
+ * relative residual, device time (ms, hipEvents around each solve) and the
+ * algorithmic HBM bytes of one iteration (two CSR products at 20 B a stored
+ * entry + rowptr + x/y, plus the fused vector passes). */
+int arpack_hip_zshift_stats(const arpack_hip_zshift* S, long long* solves, long long* iters,
+                            long long* failures, double* max_relres, double* ms,
+                            double* bytes_per_iter);
+/* znaupd in mode 3 (iparam[6] = 3, bmat = 'I') with OP = (A - sigma I)^{-1}
+ * served on the GPU by S; returns with ido = 99.  A failed solve ends the run
+ * with info = -9999. */
+void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, int n,
+                              char const* which, int nev, double* tol, a_dcomplex* resid, int ncv,
+                              a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                              a_dcomplex* workl, int lworkl, double* rwork, int* info);
+
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
  * rows) and PARPACK/SRC/MPI/pdsaitr.f.  One process per GPU; the communicator

@@ -7,10 +7,12 @@ generator and copied to host memory) driven through the reference RCI loop with
 a multithreaded OpenMP CSR SpMV as the user OP (oracle/csr_omp.c).  We time the
 reference from the OP*x request that opens restart cycle 1 (request #12: one
 getv0 request + nev0 = 10 initial Lanczos steps precede it) to the request that
-opens cycle 2 (#32), i.e. exactly one implicit-restart cycle (np = 20 Lanczos
-steps + dseigt/dsgets/dsapps), then stop.  Run as a subprocess:
+opens cycle k + 1 (#12 + 20 k), i.e. exactly k implicit-restart cycles (np = 20
+Lanczos steps + dseigt/dsgets/dsapps each), then stop; bench.py times the same
+cycles of the same solve on the GPU.  --ttc adds the reference's full solve at
+tol 1e-6 (the bench's time-to-converge case).  Run as a subprocess:
 
-    python -m oracle.cpu_baseline --n 10000000 --threads 16
+    python -m oracle.cpu_baseline --n 10000000 --threads 16 [--cycles 3] [--ttc]
 prints one JSON line.
 """
 from __future__ import annotations
@@ -59,6 +61,11 @@ def main():
     ap.add_argument("--nev", type=int, default=10)
     ap.add_argument("--ncv", type=int, default=30)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--cycles", type=int, default=3,
+                    help="restart cycles 1..k timed (np = ncv - nev Lanczos steps each)")
+    ap.add_argument("--ttc", action="store_true",
+                    help="also time the reference's full solve at --ttc-tol (time to converge)")
+    ap.add_argument("--ttc-tol", type=float, default=1e-6)
     args = ap.parse_args()
     os.environ["OPENBLAS_NUM_THREADS"] = str(args.threads)
     os.environ["OMP_NUM_THREADS"] = str(args.threads)
@@ -98,6 +105,11 @@ def main():
     P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     nreq = 0
     stamps = {}
+    np_ = ncv - nev
+    # request #1 is getv0's, #2..#(nev+1) the initial factorisation, then cycle c
+    # (np = ncv - nev steps while no Ritz value has converged, as in the GPU's
+    # verified count of the same solve) opens at request 2 + nev + (c - 1) np
+    opens = [2 + nev + c * np_ for c in range(args.cycles + 1)]
     t_start = time.time()
     while True:
         L.dsaupd_(P(ido), b"I", C.byref(C.c_int(n)), b"LA", C.byref(C.c_int(nev)), C.byref(tol),
@@ -108,20 +120,30 @@ def main():
             break
         nreq += 1
         stamps[nreq] = time.time()
-        if nreq == 1 + nev + (ncv - nev) + 1:  # request opening cycle 2
+        if nreq == opens[-1]:  # the request opening cycle k + 1
             break
         x = workd[ipntr[0] - 1: ipntr[0] - 1 + n]
         workd[ipntr[1] - 1: ipntr[1] - 1 + n] = op(x)
-    c0, c1 = 1 + nev + 1, 1 + nev + (ncv - nev) + 1
-    cycle_s = stamps[c1] - stamps[c0]
-    steps = ncv - nev
-    print(json.dumps(dict(
-        cycle_s=cycle_s, iters_per_s=1.0 / cycle_s, lanczos_steps_per_s=steps / cycle_s,
-        threads=args.threads, setup_s=stamps[c0] - t_start, gen_download_s=t_gen,
-        nnz=int(len(col)), n=n, kind="reference",
-        sample=f"1 implicit-restart cycle (np={steps} Lanczos steps + dsapps) of the bench "
-               f"workload, reference Fortran dsaupd_ + OpenBLAS, OpenMP CSR OP, "
-               f"{args.threads} threads")))
+    per_cycle = [stamps[opens[c + 1]] - stamps[opens[c]] for c in range(args.cycles)]
+    cycle_s = sum(per_cycle) / len(per_cycle)
+    out = dict(
+        cycle_s=cycle_s, iters_per_s=1.0 / cycle_s, lanczos_steps_per_s=np_ / cycle_s,
+        per_cycle_s=per_cycle, cycles="1..%d" % args.cycles, threads=args.threads,
+        setup_s=stamps[opens[0]] - t_start, gen_download_s=t_gen, nnz=int(len(col)), n=n,
+        kind="reference",
+        sample=f"restart cycles 1..{args.cycles} (np={np_} Lanczos steps + dsapps each) of the "
+               f"bench workload's tol=eps solve from dlarnv(1,3,5,7), reference Fortran dsaupd_ "
+               f"+ OpenBLAS, OpenMP CSR OP, {args.threads} threads")
+    del v, workd, workl
+    if args.ttc:
+        t = time.time()
+        r = ref.dsaupd_solve(lambda x, *_: op(x), n, nev, ncv, "LA", args.ttc_tol,
+                             v0=dlarnv_fast(n), mxiter=300, rvec=False)
+        out["time_to_converge"] = dict(seconds=time.time() - t, iters=int(r["iparam"][2]),
+                                       nopx=int(r["stats"]["nopx"]), info=int(r["info"]),
+                                       nconv=int(r.get("nconv", 0)), tol=args.ttc_tol,
+                                       start="dlarnv iseed=(1,3,5,7), info=1")
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

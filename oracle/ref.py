@@ -336,3 +336,18 @@ def csr_matvec(rowptr64, col32, val, nthreads=0):
                           x.ctypes.data, y.ctypes.data, nthreads)
         return y.copy()
     return op
+
+
+def csr_matvec_c128(rowptr64, col32, val, nthreads=0):
+    """Return op(x) -> A x using the OpenMP CSR kernel (complex128, interleaved)."""
+    lib_ = csr_omp()
+    n = len(rowptr64) - 1
+    vv = np.ascontiguousarray(val, np.complex128)
+    y = np.empty(n, np.complex128)
+
+    def op(x, *_):
+        x = np.ascontiguousarray(x, np.complex128)
+        lib_.csr_spmv_c128(n, rowptr64.ctypes.data, col32.ctypes.data, vv.ctypes.data,
+                           x.ctypes.data, y.ctypes.data, nthreads)
+        return y.copy()
+    return op

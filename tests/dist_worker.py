@@ -12,7 +12,8 @@ is the one the 8-GPU job runs.
 CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
       declared symmetric: upper-triangle SpMV + forward spill exchange; also
       checks one distributed SpMV against SciPy), ns_csr (pdnaupd_csr_cycles),
-      sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather).
+      sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather),
+      lap3d (FIXTURE m<m>_cap<k>: config 4's 3-D Laplacian, capped run).
 Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
 import os
 import sys
@@ -100,6 +101,26 @@ def sym_mixed(pkg, out, rank, world):
     del D
 
 
+def lap3d(pkg, out, rank, world, m, cap):
+    """BASELINE config 4's family at a rehearsal size: the 3-D 7-pt Laplacian
+    m^3 sharded by row blocks (z-slabs: the halo is one m x m plane per side,
+    PARPACK/EXAMPLES/MPI/pdsdrv1.f's decomposition), dsaupd LA, nev 10, ncv 30,
+    tol 1e-10, v0 = dlarnv(1,3,5,7) sliced per rank, capped at `cap` cycles."""
+    from oracle.cpu_baseline import dlarnv_fast
+    rp, col, val = M.laplace3d(m)
+    n = len(rp) - 1
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    nloc = r1 - r0
+    A = pkg.CSR.from_arrays(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]])
+    D = pkg.DistOp(A, n, r0)
+    s = pkg.SymRci(nloc, 10, 30, "LA", 1e-10, mxiter=cap, v0=dlarnv_fast(n)[r0:r1], device=True)
+    assert pkg.pdsaupd_cycles(s, D, -1) == 99
+    np.savez(os.path.join(out, "rank%d.npz" % rank), iparam=s.iparam.copy(), info=s.info.copy(),
+             ritz=np.asarray(s.ritz), halo=np.array(list(D.info().values())),
+             failed=np.array([pkg.comm_failed()]))
+    del D
+
+
 def main():
     case, fixture, out = sys.argv[1], sys.argv[2], sys.argv[3]
     info0 = len(sys.argv) > 4 and sys.argv[4] == "info0"
@@ -109,8 +130,12 @@ def main():
     dist.init_process_group("gloo")
     pkg = load_pkg()
     pkg.comm_init_host(world, rank, device=0)
-    if case in ("spmv_chain", "sym_mixed"):
-        (spmv_chain if case == "spmv_chain" else sym_mixed)(pkg, out, rank, world)
+    if case in ("spmv_chain", "sym_mixed", "lap3d"):
+        if case == "lap3d":  # FIXTURE = "m<m>_cap<cycles>"
+            m, cap = (int(t[1:]) if t[0] == "m" else int(t[3:]) for t in fixture.split("_"))
+            lap3d(pkg, out, rank, world, m, cap)
+        else:
+            (spmv_chain if case == "spmv_chain" else sym_mixed)(pkg, out, rank, world)
         dist.barrier()
         pkg.comm_destroy()
         dist.destroy_process_group()

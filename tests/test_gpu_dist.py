@@ -182,3 +182,63 @@ def test_symmetric_storage_mode_agreed(tmp_path):
     np.testing.assert_allclose(np.sort(r2[0]["d"]), np.sort(r1[0]["d"]), rtol=1e-10)
     A = sp.load_npz(tmp_path / "sym_mixed_-_1_0" / "A.npz")
     assert _resid(A, _z(r2), r2[0]["d"]) <= 1e-8
+
+
+_LAP = {}
+
+
+def _lap3d_reference(m, cap):
+    """The reference (oracle/_ref dsaupd_) on the same capped config-4-family run."""
+    if (m, cap) not in _LAP:
+        from oracle import ref
+        from oracle.cpu_baseline import dlarnv_fast
+        rp, col, val = M.laplace3d(m)
+        A = M.to_scipy(rp, col, val)
+        n = A.shape[0]
+        r = ref.dsaupd_solve(lambda x, *_: A @ x, n, 10, 30, "LA", 1e-10, v0=dlarnv_fast(n),
+                             mxiter=cap, rvec=False, return_state=True)
+        o5 = int(r["ipntr"][5]) - 1
+        _LAP[(m, cap)] = (r, r["workl"][o5:o5 + 30].copy())
+    return _LAP[(m, cap)]
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_lap3d_config4_family_ranks(tmp_path, P):
+    """BASELINE config 4's operator family (3-D 7-pt Laplacian, row-block /
+    z-slab sharding) at m = 60 (n = 216,000) over P host-transport ranks,
+    capped at 6 restart cycles: every rank reports the reference's info,
+    cycles and OP*x, and the ncv Ritz values in workl agree with the
+    reference's to 1e-10 relative; each interior rank exchanges one m x m plane
+    with each neighbour."""
+    m, cap = 60, 6
+    ref, ritz = _lap3d_reference(m, cap)
+    ranks = _run(tmp_path, "lap3d", "m%d_cap%d" % (m, cap), P)
+    for r in ranks:
+        assert not bool(r["failed"][0])
+        assert int(r["info"][0]) == ref["info"]
+        for k in (2, 4, 8):
+            assert int(r["iparam"][k]) == int(ref["iparam"][k]), (P, k)
+        got, want = np.sort(r["ritz"]), np.sort(ritz)
+        assert np.all(np.abs(got - want) <= 1e-10 * np.maximum(1.0, np.abs(want)))
+    h = ranks[1]["halo"]  # {halo_lo, halo_hi, send_lo, send_hi}
+    assert h[0] == m * m and (P == 2 or h[1] == m * m)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("P", [4, 8])
+def test_sym_csr_many_ranks(tmp_path, golden, P):
+    """The 4- and 8-way row-block plans end to end (host-transport ranks on the
+    one GPU, n = 20,000 split into blocks of 2,500-5,000 rows): the reference's
+    cycles and eigenvalues on g4, the Ritz vectors assembled from P slices."""
+    g = golden("g4_banded")
+    spec = g["spec"]
+    rp, col, val = M.banded_sym(*[int(x) for x in spec[1:]])
+    A = M.to_scipy(rp, col, val)
+    ranks = _run(tmp_path, "sym_csr", "g4_banded", P)
+    for r in ranks:
+        assert int(r["info"][0]) == 0
+        assert int(r["iparam"][2]) == int(g["iparam"][2]), (P, r["iparam"][2])
+        np.testing.assert_array_equal(r["d"], ranks[0]["d"])
+    np.testing.assert_allclose(np.sort(ranks[0]["d"]), np.sort(g["d"]), rtol=1e-10)
+    assert _resid(A, _z(ranks), ranks[0]["d"]) <= 1e-8
+

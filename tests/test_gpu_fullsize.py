@@ -64,13 +64,13 @@ def test_north_star_full_size(pkg, reference, storage):
         assert r <= 10 * TOL * abs(dv[k]), (k, r, dv[k])
 
 
-def _ref_capped(case, cap):
+def _ref_capped(case, cap, *extra):
     import tempfile
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "ref.npz")
         threads = min(16, len(os.sched_getaffinity(0)))
         r = subprocess.run([sys.executable, "-m", "oracle.fullsize_ref", "--case", case, "--mxiter",
-                            str(cap), "--threads", str(threads), "--out", out], cwd=ROOT,
+                            str(cap), "--threads", str(threads), "--out", out, *extra], cwd=ROOT,
                            capture_output=True, text=True, timeout=400)
         assert r.returncode == 0, r.stderr[-2000:]
         print(r.stdout.strip())
@@ -124,3 +124,73 @@ def test_c5_znaupd_zrandom_full_size(pkg):
     if int(s.iparam[4]):
         d, _, nconv = s.eupd(rvec=False)
         assert _close(d[:nconv], ref["d"], 1e-10)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("storage", ["full", "sym"])
+def test_c2_dsaupd_laplace2d_full_size(pkg, storage):
+    """BASELINE config 2 at full size (2-D 5-pt Laplacian m = 1000, n = 1e6, LA,
+    nev 10, ncv 30), capped at 6 restart cycles, tol 1e-10: same info, cycles,
+    OP*x and DGKS count as the reference, all ncv Ritz values in workl within
+    1e-10 relative -- with the full-storage SpMV and with the bench's
+    symmetric-storage SpMV (upper triangle)."""
+    cap = 6
+    ref = _ref_capped("c2", cap, "--tol", "1e-10")
+    A = pkg.CSR.laplace2d(1000)
+    if storage == "sym":
+        A.set_symmetric(True)
+    n = A.n
+    s = pkg.SymRci(n, 10, 30, "LA", 1e-10, mxiter=cap, v0=dlarnv_fast(n), device=True)
+    s.aupd_csr(A)
+    assert int(s.info[0]) == int(ref["info"])
+    for k in (2, 4, 8):
+        assert int(s.iparam[k]) == int(ref["iparam"][k]), k
+    o5 = int(s.ipntr[5]) - 1
+    assert _close(s.workl[o5:o5 + 30], ref["ritz"], 1e-10)
+
+
+@pytest.mark.timeout(600)
+def test_c4_dsaupd_laplace3d_full_size(pkg):
+    """BASELINE config 4's operator on one GPU (3-D 7-pt Laplacian m = 215,
+    n = 9,938,375; the 8-GPU row-block run shards exactly this), LA, nev 10,
+    ncv 30, tol 1e-10, capped at 3 restart cycles: same info, cycles and OP*x,
+    all ncv Ritz values within 1e-10 relative of the reference's."""
+    cap = 3
+    ref = _ref_capped("c4", cap, "--tol", "1e-10")
+    A = pkg.CSR.laplace3d(215)
+    n = A.n
+    s = pkg.SymRci(n, 10, 30, "LA", 1e-10, mxiter=cap, v0=dlarnv_fast(n), device=True)
+    s.aupd_csr(A)
+    assert int(s.info[0]) == int(ref["info"])
+    for k in (2, 4, 8):
+        assert int(s.iparam[k]) == int(ref["iparam"][k]), k
+    o5 = int(s.ipntr[5]) - 1
+    assert _close(s.workl[o5:o5 + 30], ref["ritz"], 1e-10)
+
+
+@pytest.mark.timeout(600)
+def test_c5_znaupd_shift_invert_full_size(pkg):
+    """BASELINE config 5 as stated: znaupd in shift-invert mode 3 (sigma = 0,
+    SRC/znaupd.f:27) on the random complex operator n = 5e5, 100 nnz/row, LM,
+    nev 10, ncv 40, capped at 2 restart cycles.  OP = (A - sigma I)^{-1} by the
+    device BiCGStab (csrc/zsolve.hip) here and by the host BiCGStab
+    (oracle/krylov.py over the OpenMP complex CSR product) under the reference,
+    both to rtol 1e-13: same info, cycles and OP*x, all ncv Ritz values of OP
+    within 1e-9 relative (the two solves agree to ~1e-13, not bitwise)."""
+    cap = 2
+    ref = _ref_capped("c5si", cap, "--rtol", "1e-13")
+    Z = pkg.ZCSR.random(500_000, 100, 5, 100.0)
+    n = Z.n
+    S = pkg.ZShift(Z, 0j, rtol=1e-13, maxit=200)
+    s = pkg.ZRci(n, 10, 40, "LM", 1e-6, mode=3, mxiter=cap, v0=dlarnv_fast(2 * n).view(np.complex128))
+    assert s.aupd_zshift(S) == 99
+    assert int(s.info[0]) == int(ref["info"])
+    for k in (2, 4, 8):
+        assert int(s.iparam[k]) == int(ref["iparam"][k]), k
+    st = S.stats()
+    assert st["failures"] == 0 and st["solves"] == int(s.iparam[8])
+    print("device BiCGStab: %d solves, %.1f iterations a solve, %.2f ms a solve"
+          % (st["solves"], st["iters"] / st["solves"], st["ms"] / st["solves"]))
+    o5 = int(s.ipntr[5]) - 1
+    assert _close(s.workl[o5:o5 + 40], ref["ritz"], 1e-9)
+
