@@ -21,8 +21,6 @@ const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
 namespace ahip {
 
 Stats g_stats;
-uint64_t g_dseed = 0;
-static bool g_dseed_init = false;
 static hipStream_t g_stream = nullptr;
 static std::mutex g_mu;
 // live solves keyed by the caller's V (one registry per storage type)
@@ -55,15 +53,36 @@ uint64_t lcg_advance(uint64_t seed, uint64_t steps) {
     return (seed * p) & mask;
 }
 
-static void ensure_seed() {
-    if (!g_dseed_init) {  // SRC/dgetv0.f:202-208: iseed = (1,3,5,7) once per process
+uint64_t& getv0_seed(char family) {
+    static uint64_t seed[4];
+    static bool init[4] = {false, false, false, false};
+    const int f = family == 's' ? 1 : family == 'z' ? 2 : family == 'c' ? 3 : 0;
+    if (!init[f]) {  // SRC/dgetv0.f:202-208: iseed = (1,3,5,7) once per process
         const int is[4] = {1, 3, 5, 7};
-        g_dseed = seed48_from_iseed(is);
-        g_dseed_init = true;
+        seed[f] = seed48_from_iseed(is);
+        init[f] = true;
     }
+    return seed[f];
 }
 
-void ahip_ensure_seed() { ensure_seed(); }
+uint64_t& pgetv0_seed(char family, int rank) {
+    static uint64_t seed[4];
+    static bool init[4] = {false, false, false, false};
+    const int f = family == 's' ? 1 : family == 'z' ? 2 : family == 'c' ? 3 : 0;
+    if (!init[f]) {  // PARPACK/SRC/MPI/pdgetv0.f:234-245: igen = 1000 + 2 myid + 1
+        int igen = 1000 + 2 * rank + 1;
+        int is[4];
+        is[0] = igen / 1000;
+        igen %= 1000;
+        is[1] = igen / 100;
+        igen %= 100;
+        is[2] = igen / 10;
+        is[3] = igen % 10;
+        seed[f] = seed48_from_iseed(is);
+        init[f] = true;
+    }
+    return seed[f];
+}
 
 // dsaupd argument checks (SRC/dsaupd.f:501-543); returns ierr
 static int sym_check(char bmat, int n, la::Which which, int nev, int ncv, int lworkl, int mode,
@@ -119,7 +138,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
                      const DistOp* dist = nullptr, bool ns = false) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
     if (dist) csr = dist->A;
-    if (kShadow && (dist || csr)) {  // the float family: RCI on one GPU
+    if (kShadow && csr) {  // the float family: reverse communication (no device-CSR OP)
         *info = -9999;
         *ido = 99;
         return;
@@ -133,7 +152,6 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             for (int t = 0; t < wlen; ++t) workl[t] = (R)S->wshadow[t];
     };
     if (*ido == 0) {
-        ensure_seed();
         g_stats = Stats{};  // dstats (SRC/dstats.f)
         const la::Which w = la::parse_which(which);
         const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
@@ -448,6 +466,32 @@ void arpack_hip_pdnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, 
                           double* workl, int lworkl, int* info) {
     sym_aupd(ido, bmat, n, which, nev, &tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
              lworkl, info, nullptr, -1, ahip_dist_view(D), true);
+}
+
+// fp32 PARPACK-style RCI (ICB/parpack.h:17 pssaupd_c, :23 psnaupd_c): the float
+// engine on a row decomposition; reductions in fp64 and allreduced as for pd*.
+void arpack_hip_pssaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info) {
+    double t = tol;
+    sym_aupd(ido, bmat, n, which, nev, &t, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr, -1, ahip_dist_view(D), false);
+}
+void arpack_hip_psnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info) {
+    double t = tol;
+    sym_aupd(ido, bmat, n, which, nev, &t, resid, ncv, v, ldv, iparam, ipntr, workd, workl,
+             lworkl, info, nullptr, -1, ahip_dist_view(D), true);
+}
+
+// PARPACK's start vector for info = 0 (PARPACK/SRC/MPI/pdgetv0.f:234-245)
+int arpack_hip_dist_set_seed_mode(arpack_hip_dist* D, int mode) {
+    if (!D || (mode != 0 && mode != 1)) return -1;
+    const_cast<DistOp*>(ahip_dist_view(D))->seed_mode = mode;
+    return 0;
 }
 
 void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }

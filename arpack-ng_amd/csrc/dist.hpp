@@ -40,6 +40,10 @@ struct DistOp {
     const dev::Csr* A = nullptr;        // local rows, local (x_ext) column indices
     const Comm* comm = nullptr;
     uint64_t comm_gen = 0;              // generation of comm at creation
+    // info = 0 start vector: 0 = one dlarnv stream sliced at the rank's global
+    // row offset (the same iterates for every rank count); 1 = PARPACK's
+    // per-rank stream (PARPACK/SRC/MPI/pdgetv0.f:234-245)
+    int seed_mode = 0;
     double* x_mid() const { return x_ext + halo_lo; }
 };
 

@@ -23,13 +23,18 @@ struct Stats {
 };
 extern Stats g_stats;
 
-// dgetv0's process-wide SAVEd LAPACK seed (SRC/dgetv0.f:202-208), kept as the
-// 48-bit integer the four base-4096 digits encode.
-extern uint64_t g_dseed;
+// The process-wide SAVEd LAPACK seed of each start-vector routine, kept as the
+// 48-bit integer its four base-4096 digits encode: dgetv0 (shared by dsaupd and
+// dnaupd), sgetv0, zgetv0 and cgetv0 each keep their own, initialised to
+// (1,3,5,7) on first use (SRC/dgetv0.f:202-208, sgetv0.f, zgetv0.f, cgetv0.f).
+// family: 'd', 's', 'z', 'c'.
+uint64_t& getv0_seed(char family);
+// PARPACK's p?getv0 seed (PARPACK/SRC/MPI/pdgetv0.f:225-246): per process rank,
+// the digits of 1000 + 2 rank + 1, SAVEd per family like the serial one.
+uint64_t& pgetv0_seed(char family, int rank);
 uint64_t seed48_from_iseed(const int iseed[4]);
 void iseed_from_seed48(uint64_t s, int iseed[4]);
 uint64_t lcg_advance(uint64_t seed, uint64_t steps);  // seed * a^steps mod 2^48
-void ahip_ensure_seed();  // iseed = (1,3,5,7) once per process
 
 // Caller-visible arrays in one place. `dev_*` are what the kernels use: the
 // caller's own buffers in device-pointer mode, engine-owned mirrors in

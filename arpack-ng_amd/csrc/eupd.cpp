@@ -296,6 +296,17 @@ void dseupd_(int* rvec, char const* howmny, int* select, double* d, double* z, i
 }
 
 // single-precision family (ICB/arpack.h:19; SRC/sseupd.f)
+// pss: the fp32 family on a row distribution (ICB/parpack.h:17-18)
+void arpack_hip_psseupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, float* d, float* z, int ldz, float sigma,
+                          char const* bmat, int n, char const* which, int nev, float tol,
+                          float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr,
+                          float* workd, float* workl, int lworkl, int* info) {
+    (void)select;
+    *info = ahip::sym_eupd(rvec != 0, howmny[0], nullptr, d, z, ldz, sigma, bmat[0], n, which, nev,
+                           tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+                           ahip_dist_view(D));
+}
 void sseupd_c(int rvec, char const* howmny, int const* select, float* d, float* z, int ldz,
               float sigma, char const* bmat, int n, char const* which, int nev, float tol,
               float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr, float* workd,

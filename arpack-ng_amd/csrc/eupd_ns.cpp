@@ -354,6 +354,19 @@ void dneupd_(int* rvec, char const* howmny, int* select, double* dr, double* di,
 }
 
 // single-precision family (ICB/arpack.h:17; SRC/sneupd.f)
+// psn (ICB/parpack.h:23-24): as pdneupd, no collective
+void arpack_hip_psneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, float* dr, float* di, float* z, int ldz,
+                          float sigmar, float sigmai, float* workev, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info) {
+    (void)D;
+    (void)select;
+    *info = ahip::ns_eupd(rvec != 0, howmny[0], nullptr, dr, di, z, ldz, sigmar, sigmai, workev,
+                          bmat[0], n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
+                          workl, lworkl);
+}
 void sneupd_c(int rvec, char const* howmny, int const* select, float* dr, float* di, float* z,
               int ldz, float sigmar, float sigmai, float* workev, char const* bmat, int n,
               char const* which, int nev, float tol, float* resid, int ncv, float* v, int ldv,

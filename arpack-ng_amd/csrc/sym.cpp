@@ -189,8 +189,17 @@ Task SolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
     R* wd = a.d_workd;
     ierr = 0;
     if (!initv) {  // dlarnv(idist=2, iseed, n, resid) — SRC/dgetv0.f:234-237
-        const uint64_t s1 = dev::larnv_uniform(ws, nn, g_dseed, a.d_resid, row0);
-        g_dseed = dist ? lcg_advance(g_dseed, (uint64_t)dist->n_global) : s1;
+        constexpr char fam = std::is_same_v<R, double> ? 'd' : 's';
+        if (dist && dist->seed_mode == 1) {
+            // PARPACK: each rank draws its n local values from its own stream
+            // (PARPACK/SRC/MPI/pdgetv0.f:234-245, 276)
+            uint64_t& sd = pgetv0_seed(fam, comm_rank(dist->comm));
+            sd = dev::larnv_uniform(ws, nn, sd, a.d_resid, 0);
+        } else {  // one stream; a rank takes its rows' slice (P-invariant start)
+            uint64_t& sd = getv0_seed(fam);
+            const uint64_t s1 = dev::larnv_uniform(ws, nn, sd, a.d_resid, row0);
+            sd = dist ? lcg_advance(sd, (uint64_t)dist->n_global) : s1;
+        }
     }
     if (itry == 1) {  // force into the range of OP (SRC/dgetv0.f:245-251)
         g_stats.nopx += 1;

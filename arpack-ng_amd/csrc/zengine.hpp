@@ -15,9 +15,13 @@
 
 namespace ahip {
 
+struct Comm;
 namespace zdev {
 struct Ws {
     hipStream_t stream = nullptr;
+    // row-distributed solve: every reduction of `dots` is allreduced over the
+    // ranks before it reaches the host (PARPACK/SRC/MPI/pznaitr.f's MPI_ALLREDUCEs)
+    const Comm* comm = nullptr;
     int nblk = 0;
     double* part = nullptr;  // 2*(ncv+2) slots x nblk
     double* sums = nullptr;
@@ -137,6 +141,8 @@ public:
     RciCtx ctx;
     std::optional<Task> root;
     const zdev::ZCsr* csr = nullptr;  // free-running OP (mode 1)
+    const DistOp* dist = nullptr;      // row block of a distributed solve (or null)
+    int64_t row0 = 0, n_global = 0;
     const R* op_x = nullptr;
     R* op_y = nullptr;
 

@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "../../include/arpack_hip.h"
+#include "dist.hpp"
 #include "zcommon.hpp"
 #include "zengine.hpp"
 
@@ -315,6 +316,7 @@ void dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, co
     }
     const int m = 2 * (j + (w ? 1 : 0));
     hipLaunchKernelGGL(k_sum_slots, dim3(m), dim3(kB), 0, ws.stream, ws.part, ws.nblk, ws.sums);
+    if (ws.comm) comm_allreduce_sum(ws.comm, ws.sums, m, ws.stream);  // the ranks' local sums
     (void)hipMemcpyAsync(ws.host, ws.sums, sizeof(double) * m, hipMemcpyDeviceToHost, ws.stream);
     (void)hipStreamSynchronize(ws.stream);
     for (int c = 0; c < m / 2; ++c) out[c] = std::complex<double>(ws.host[2 * c], ws.host[2 * c + 1]);

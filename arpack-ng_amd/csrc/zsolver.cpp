@@ -16,8 +16,11 @@
 #include <unordered_map>
 
 #include "../../include/arpack_hip.h"
+#include "dist.hpp"
 #include "zengine.hpp"
 #include "zsolve.hpp"
+
+const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
 
 namespace ahip {
 
@@ -61,7 +64,15 @@ Task ZSolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
     if (!initv) {  // zlarnv(idist=2): re/im pairs of one dlaruv stream
         dev::Workspace tmp;
         tmp.stream = a.stream;
-        g_dseed = dev::larnv_uniform(tmp, 2 * nn, g_dseed, a.d_resid, 0, 128);
+        constexpr char fam = std::is_same_v<R, double> ? 'z' : 'c';
+        if (dist && dist->seed_mode == 1) {  // PARPACK/SRC/MPI/pzgetv0.f:231-242: per rank
+            uint64_t& sd = pgetv0_seed(fam, comm_rank(dist->comm));
+            sd = dev::larnv_uniform(tmp, 2 * nn, sd, a.d_resid, 0, 128);
+        } else {  // one stream, this rank's slice of 2 n_global reals
+            uint64_t& sd = getv0_seed(fam);
+            const uint64_t s1 = dev::larnv_uniform(tmp, 2 * nn, sd, a.d_resid, 2 * row0, 128);
+            sd = dist ? lcg_advance(sd, 2 * (uint64_t)n_global) : s1;
+        }
     }
     if (itry == 1) {
         g_stats.nopx += 1;
@@ -267,7 +278,9 @@ Task ZSolverT<R>::naitr(int k, int npk, int& iinfo) {
         const int v = e ? atoi(e) : 0;
         return v > 0 && v < zdev::kMaxDevStepNcv ? v : zdev::kMaxDevStepNcv;
     }();
-    if (bmat == 'I' && dev_steps && ncv <= dev_max_ncv) {
+    // (a row-distributed solve takes the host-driven step: its reductions are
+    // the allreduced dots of zdev::dots, PARPACK/SRC/MPI/pznaitr.f:580-763)
+    if (bmat == 'I' && dev_steps && ncv <= dev_max_ncv && !dist) {
         co_await naitr_dev(k, npk, iinfo);
         if (iinfo > 0) co_return;
     } else
@@ -460,7 +473,7 @@ Task ZSolverT<R>::run() {
             std::memcpy(ritz, wl, sizeof(cd) * np);
         }
         {   // znapps: chase on the host, V*Q and resid update on the device
-            zla::znapps_host(nev, np, ritz, h, ncv, q, ncv, wl, n);
+            zla::znapps_host(nev, np, ritz, h, ncv, q, ncv, wl, n_global);
             const int kev = nev;
             const bool next = h[kev + (size_t)(kev - 1) * ncv].real() > 0.0;
             const int nz = kev + (next ? 1 : 0);
@@ -508,7 +521,8 @@ template <class R>
 static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                    std::complex<R>* resid, int ncv, std::complex<R>* v, int ldv, int* iparam,
                    int* ipntr, std::complex<R>* workd, std::complex<R>* workl, int lworkl,
-                   R* rwork, int* info, const zdev::ZCsr* csr, zdev::ZShift* zs = nullptr) {
+                   R* rwork, int* info, const zdev::ZCsr* csr, zdev::ZShift* zs = nullptr,
+                   const DistOp* dist = nullptr) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
     if (zs) csr = zs->A;  // free-running shift-invert: OP = (A - sigma I)^{-1} on the device
     if (kShadow && csr) {
@@ -525,7 +539,6 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             for (int t = 0; t < wlen; ++t) workl[t] = std::complex<R>(S->wshadow[t]);
     };
     if (*ido == 0) {
-        ahip_ensure_seed();
         g_stats = Stats{};
         const la::Which w = la::parse_which(which);
         const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
@@ -543,6 +556,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         else if (mode == 1 && bmat[0] == 'G') ierr = -11;
         if (csr && ((zs ? mode != 3 || bmat[0] != 'I' : mode != 1) || csr->n != n))
             ierr = ierr ? ierr : -11;
+        if (dist && (csr || dist->nloc != n)) ierr = ierr ? ierr : -1;
         if (ierr != 0) {
             *info = ierr;
             *ido = 99;
@@ -589,6 +603,12 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             return;
         }
         S->csr = csr;
+        S->n_global = dist ? dist->n_global : n;
+        if (dist) {  // row block of a distributed solve (PARPACK's pznaupd)
+            S->dist = dist;
+            S->row0 = dist->row0;
+            S->ws.comm = dist->comm;
+        }
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
@@ -618,10 +638,19 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         }
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) S->a.h2d_workd(2 * r.y, 2 * (int64_t)n);
     }
+    auto comm_broken = [&]() {  // a failed collective: info = -9999 (see sym_aupd)
+        if (!S->dist || !comm_failed(S->dist->comm)) return false;
+        S->a.sync();
+        *info = -9999;
+        *ido = 99;
+        g_z.erase(v);
+        return true;
+    };
     for (;;) {
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
+        if (comm_broken()) return;
         if (S->csr && (r.ido == -1 || r.ido == 1)) {
             if constexpr (!kShadow) {
                 if (!zs) {
@@ -651,6 +680,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         *ido = r.ido;
         return;
     }
+    if (comm_broken()) return;
     *ido = 99;  // SRC/znaupd.f:585-600
     iparam[2] = S->mxiter;
     iparam[4] = S->np;
@@ -1069,6 +1099,47 @@ void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* Z, int* ido, char const* bmat
                             int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl, double* rwork, int* info) {
     ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr, (cd*)workd,
                  (cd*)workl, lworkl, rwork, info, &Z->A);
+}
+
+// ---- PARPACK-style complex RCI (ICB/parpack.h:30-33 pcnaupd_c / pznaupd_c
+//      with n = LOCAL rows; PARPACK/SRC/MPI/pznaupd.f decomposition) ----
+void arpack_hip_pznaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, a_dcomplex* resid, int ncv,
+                          a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                          a_dcomplex* workl, int lworkl, double* rwork, int* info) {
+    ahip::z_aupd(ido, bmat, n, which, nev, &tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr,
+                 (cd*)workd, (cd*)workl, lworkl, rwork, info, nullptr, nullptr, ahip_dist_view(D));
+}
+void arpack_hip_pcnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, a_fcomplex* resid, int ncv,
+                          a_fcomplex* v, int ldv, int* iparam, int* ipntr, a_fcomplex* workd,
+                          a_fcomplex* workl, int lworkl, float* rwork, int* info) {
+    double t = tol;
+    ahip::z_aupd<float>(ido, bmat, n, which, nev, &t, (cf*)resid, ncv, (cf*)v, ldv, iparam, ipntr,
+                        (cf*)workd, (cf*)workl, lworkl, rwork, info, nullptr, nullptr,
+                        ahip_dist_view(D));
+}
+// p[cz]neupd (PARPACK/SRC/MPI/pzneupd.f): no collective -- the Schur / Ritz
+// work is replicated host work and the n-length products are row-local
+void arpack_hip_pzneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, a_dcomplex* d, a_dcomplex* z, int ldz,
+                          a_dcomplex sigma, a_dcomplex* workev, char const* bmat, int n,
+                          char const* which, int nev, double tol, a_dcomplex* resid, int ncv,
+                          a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                          a_dcomplex* workl, int lworkl, double* rwork, int* info) {
+    (void)D;
+    zneupd_c(rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol, resid, ncv,
+             v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
+}
+void arpack_hip_pcneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, a_fcomplex* d, a_fcomplex* z, int ldz,
+                          a_fcomplex sigma, a_fcomplex* workev, char const* bmat, int n,
+                          char const* which, int nev, float tol, a_fcomplex* resid, int ncv,
+                          a_fcomplex* v, int ldv, int* iparam, int* ipntr, a_fcomplex* workd,
+                          a_fcomplex* workl, int lworkl, float* rwork, int* info) {
+    (void)D;
+    cneupd_c(rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol, resid, ncv,
+             v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
 }
 
 // ---- device shift-invert operator (zsolve.hip) ----

@@ -390,6 +390,56 @@ void arpack_hip_pdneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny
                           char const* which, int nev, double tol, double* resid, int ncv,
                           double* v, int ldv, int* iparam, int* ipntr, double* workd,
                           double* workl, int lworkl, int* info);
+/* The same for the other families of ICB/parpack.h: fp32 symmetric / nonsymmetric
+ * (pssaupd_c :17, psseupd_c :18, psnaupd_c :23, psneupd_c :24) and complex
+ * (pcnaupd_c :29, pcneupd_c :30, pznaupd_c :32, pzneupd_c :33).  The complex
+ * engine on a row block takes its host-driven Arnoldi step with allreduced
+ * inner products (PARPACK/SRC/MPI/pznaitr.f); p*neupd need no collective. */
+void arpack_hip_pssaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info);
+void arpack_hip_psseupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, float* d, float* z, int ldz, float sigma,
+                          char const* bmat, int n, char const* which, int nev, float tol,
+                          float* resid, int ncv, float* v, int ldv, int* iparam, int* ipntr,
+                          float* workd, float* workl, int lworkl, int* info);
+void arpack_hip_psnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info);
+void arpack_hip_psneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, float* dr, float* di, float* z, int ldz,
+                          float sigmar, float sigmai, float* workev, char const* bmat, int n,
+                          char const* which, int nev, float tol, float* resid, int ncv, float* v,
+                          int ldv, int* iparam, int* ipntr, float* workd, float* workl,
+                          int lworkl, int* info);
+void arpack_hip_pznaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, double tol, a_dcomplex* resid, int ncv,
+                          a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                          a_dcomplex* workl, int lworkl, double* rwork, int* info);
+void arpack_hip_pzneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, a_dcomplex* d, a_dcomplex* z, int ldz,
+                          a_dcomplex sigma, a_dcomplex* workev, char const* bmat, int n,
+                          char const* which, int nev, double tol, a_dcomplex* resid, int ncv,
+                          a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
+                          a_dcomplex* workl, int lworkl, double* rwork, int* info);
+void arpack_hip_pcnaupd_c(const arpack_hip_dist* D, int* ido, char const* bmat, int n,
+                          char const* which, int nev, float tol, a_fcomplex* resid, int ncv,
+                          a_fcomplex* v, int ldv, int* iparam, int* ipntr, a_fcomplex* workd,
+                          a_fcomplex* workl, int lworkl, float* rwork, int* info);
+void arpack_hip_pcneupd_c(const arpack_hip_dist* D, int rvec, char const* howmny,
+                          int const* select, a_fcomplex* d, a_fcomplex* z, int ldz,
+                          a_fcomplex sigma, a_fcomplex* workev, char const* bmat, int n,
+                          char const* which, int nev, float tol, a_fcomplex* resid, int ncv,
+                          a_fcomplex* v, int ldv, int* iparam, int* ipntr, a_fcomplex* workd,
+                          a_fcomplex* workl, int lworkl, float* rwork, int* info);
+/* Start vector of info = 0 on a distribution: mode 0 (default) draws one dlarnv
+ * stream and gives each rank its rows' slice, so every rank count sees the
+ * single-GPU iterates; mode 1 is PARPACK's: each rank draws its local rows from
+ * its own process-persistent stream seeded with the digits of 1000 + 2 rank + 1
+ * (PARPACK/SRC/MPI/pdgetv0.f:234-245), as libparpack_hip.so sets it. */
+int arpack_hip_dist_set_seed_mode(arpack_hip_dist* D, int mode);
 /* Halo plan (host only, CPU-testable): tab = [row0, nloc, min col, max col] per
  * rank (4*P doubles, global indices); out = {halo_lo, halo_hi, send_lo, send_hi}
  * of rank r.  Returns 0, -3 (blocks not contiguous) or -4 (halo too wide). */

@@ -92,13 +92,13 @@ def _match_rows(rows, ref_rows, nval):
     return pairs
 
 
-def _compare(name, stdout, single=False, count_rtol=0.0):
+def _compare(name, stdout, single=False, count_rtol=0.0, gold=GOLD):
     """Ritz table and counters of one program run against the reference's.
     single: a single-precision family (s*, c*) -- values to 2e-4 of the row's
     magnitude, residuals <= max(10x the reference's, 1e-5); otherwise values to
     the 6 printed digits, residuals <= max(10x the reference's, 1e-12).
     count_rtol: relative slack on OP*x and restart cycles (0 = equal)."""
-    ref_rows, ref_counts = parse(open(os.path.join(GOLD, name + ".out")).read())
+    ref_rows, ref_counts = parse(open(os.path.join(gold, name + ".out")).read())
     rows, counts = parse(stdout)
     assert len(rows) == len(ref_rows), (name, rows, ref_rows)
     nval = 2 if ref_rows and len(ref_rows[0]) == 3 else 1
