@@ -65,6 +65,13 @@ struct ZCsr {
     void* s_col = nullptr;
     double* s_val = nullptr;
     double* s_y = nullptr;
+    // column-sorted tiles (zsplit.hip, default when the slice width < 2^20): the
+    // entries of each (row block of kTileRows rows, slice) sorted by column;
+    // t_idx = row_local << 20 | slice column; the block's range comes from s_rp
+    bool tile = false;
+    int64_t t_nrb = 0;
+    uint32_t* t_idx = nullptr;
+    double* t_val = nullptr;
 };
 // Build the XCD column split of A when it pays (n >= 2^18: x larger than one
 // XCD's L2; >= 32 entries a row: the partials' 256 B a row stay small against

@@ -15,6 +15,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "zcommon.hpp"
 #include "zengine.hpp"
@@ -105,6 +106,112 @@ __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, doub
     }
 }
 
+// ---- column-sorted tiles --------------------------------------------------
+// Measured (tools/zspmv_probe.hip, config-5 operator): the CSR split spends
+// 0.41 ms of which only 0.23-0.28 is its matrix stream -- the rest is the
+// random 16-byte gather, which costs the address unit one cache line per lane
+// whether or not the line is in L2 (a 64 KB gather window: 0.38 ms).  Here the
+// entries of each (row block of kTileRows rows, slice) are sorted by column, so
+// the 64 lanes of a wave gather from a few neighbouring lines of x, and every
+// product is added into the block's row sums in LDS (ds_add_f64), written once
+// as the slice's partial y: 0.226 ms, same results to 5e-16 (the LDS adds land
+// in schedule order, so y is reproducible to rounding, not bitwise).
+constexpr int kTileRows = 4096;  // 64 KB of LDS row sums: two blocks a CU
+constexpr int kTileU = 4;        // entries a lane keeps in flight
+
+__global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int32_t* __restrict__ srp,
+                                               const int64_t* __restrict__ base,
+                                               const uint32_t* __restrict__ idx,
+                                               const double2* __restrict__ val,
+                                               const double2* __restrict__ x,
+                                               double2* __restrict__ yp, const int* __restrict__ gate) {
+    if (gate && *gate) return;
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    __shared__ double ylds[2 * kTileRows];
+    const int s = (int)(blockIdx.x % kSlices);  // the XCD this block runs on
+    const int64_t r0 = (int64_t)(blockIdx.x / kSlices) * kTileRows;
+    const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
+    for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
+    __syncthreads();
+    const int32_t* rp = srp + (int64_t)s * (n + 1);
+    const int64_t e0 = base[s] + rp[r0], e1 = base[s] + rp[r0 + rows];
+    const double2* xs = x + (int64_t)s * sw;
+    int64_t e = e0 + threadIdx.x;
+    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
+        uint32_t id[kTileU];
+        dv2 v[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) {  // every load of the batch issued first
+            id[u] = __builtin_nontemporal_load(&idx[e + u * 256]);
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+        }
+        double2 xv[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) xv[u] = xs[id[u] & 0xfffffu];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) {
+            const int r = (int)(id[u] >> 20);
+            atomicAdd(&ylds[2 * r], v[u].x * xv[u].x - v[u].y * xv[u].y);
+            atomicAdd(&ylds[2 * r + 1], v[u].x * xv[u].y + v[u].y * xv[u].x);
+        }
+    }
+    for (; e < e1; e += 256) {
+        const uint32_t id = idx[e];
+        const dv2 v = reinterpret_cast<const dv2*>(val)[e];
+        const double2 xv = xs[id & 0xfffffu];
+        const int r = (int)(id >> 20);
+        atomicAdd(&ylds[2 * r], v.x * xv.x - v.y * xv.y);
+        atomicAdd(&ylds[2 * r + 1], v.x * xv.y + v.y * xv.x);
+    }
+    __syncthreads();
+    double2* y = yp + (int64_t)s * n + r0;
+    for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
+}
+
+// sort keys (slice column), the row of every entry, and the segment bounds of
+// the (slice, row block) segments in the slice-major entry order
+template <class CT>
+__global__ void k_ztile_keys(int64_t n, const int32_t* __restrict__ srp, const int64_t* __restrict__ base,
+                             const CT* __restrict__ scol, uint32_t* __restrict__ key,
+                             uint32_t* __restrict__ erow, uint32_t* __restrict__ perm) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        for (int s = 0; s < kSlices; ++s) {
+            const int32_t* rp = srp + (int64_t)s * (n + 1);
+            for (int64_t k = base[s] + rp[r]; k < base[s] + rp[r + 1]; ++k) {
+                key[k] = (uint32_t)scol[k];
+                erow[k] = (uint32_t)(r % kTileRows);
+                perm[k] = (uint32_t)k;
+            }
+        }
+    }
+}
+__global__ void k_ztile_segs(int64_t n, int64_t nrb, const int32_t* __restrict__ srp,
+                             const int64_t* __restrict__ base, int64_t* __restrict__ seg) {
+    const int64_t ns = kSlices * nrb;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= ns;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        if (q == ns) {
+            seg[q] = base[kSlices];
+            continue;
+        }
+        const int s = (int)(q / nrb);
+        const int64_t rb = q % nrb;
+        seg[q] = base[s] + srp[(int64_t)s * (n + 1) + rb * kTileRows];
+    }
+}
+__global__ void k_ztile_gather(int64_t nnz, const uint32_t* __restrict__ perm,
+                               const uint32_t* __restrict__ key_sorted, const uint32_t* __restrict__ erow,
+                               const double2* __restrict__ sval, uint32_t* __restrict__ idx,
+                               double2* __restrict__ tval) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = perm[k];
+        idx[k] = (erow[p] << 20) | key_sorted[k];
+        tval[k] = sval[p];
+    }
+}
+
 inline int grid1(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
@@ -112,6 +219,11 @@ inline int grid1(int64_t n) {
 }  // namespace
 
 void zcsr_free_split(ZCsr& A) {
+    if (A.t_idx) (void)hipFree(A.t_idx);
+    if (A.t_val) (void)hipFree(A.t_val);
+    A.t_idx = nullptr;
+    A.t_val = nullptr;
+    A.tile = false;
     if (A.s_rp) (void)hipFree(A.s_rp);
     if (A.s_base) (void)hipFree(A.s_base);
     if (A.s_col) (void)hipFree(A.s_col);
@@ -123,6 +235,73 @@ void zcsr_free_split(ZCsr& A) {
     A.s_val = nullptr;
     A.s_y = nullptr;
     A.split = false;
+}
+
+// Column-sorted tiles from the slice CSR (A.split): a stable segmented radix sort
+// of each (slice, row block) segment by column, then idx / val gathered in that
+// order; the slice CSR's columns and values are released.  0: built; 1: not
+// applicable (slice wider than 2^20 columns, AHIP_ZSPLIT=csr); < 0: error (the
+// CSR split is kept).
+static int ztile_build(ZCsr& A) {
+    static const bool off = [] {
+        const char* e = getenv("AHIP_ZSPLIT");
+        return e && std::strcmp(e, "csr") == 0;
+    }();
+    const int64_t n = A.n, nnz = A.nnz;
+    if (off || A.s_w >= (int64_t(1) << 20) || nnz <= 0 || nnz >= (int64_t(1) << 32)) return 1;
+    const int64_t nrb = (n + kTileRows - 1) / kTileRows, nseg = kSlices * nrb;
+    uint32_t *key = nullptr, *key2 = nullptr, *erow = nullptr, *perm = nullptr, *perm2 = nullptr;
+    int64_t* seg = nullptr;
+    void* tmp = nullptr;
+    size_t tmpb = 0;
+    int rc = 0;
+    auto cleanup = [&]() {
+        for (void* q : {(void*)key, (void*)key2, (void*)erow, (void*)perm, (void*)perm2, (void*)seg, tmp})
+            if (q) (void)hipFree(q);
+    };
+    const size_t eb = sizeof(uint32_t) * (size_t)nnz;
+    if (hipMalloc(&key, eb) || hipMalloc(&key2, eb) || hipMalloc(&erow, eb) || hipMalloc(&perm, eb) ||
+        hipMalloc(&perm2, eb) || hipMalloc(&seg, sizeof(int64_t) * (nseg + 1)) ||
+        hipMalloc(&A.t_idx, eb) || hipMalloc(&A.t_val, 16 * (size_t)nnz)) {
+        rc = -2;
+    } else {
+        if (A.s_col16)
+            hipLaunchKernelGGL(k_ztile_keys<uint16_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_rp,
+                               A.s_base, (const uint16_t*)A.s_col, key, erow, perm);
+        else
+            hipLaunchKernelGGL(k_ztile_keys<int32_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_rp,
+                               A.s_base, (const int32_t*)A.s_col, key, erow, perm);
+        hipLaunchKernelGGL(k_ztile_segs, dim3(grid1(nseg + 1)), dim3(256), 0, nullptr, n, nrb, A.s_rp,
+                           A.s_base, seg);
+        int bits = 1;
+        while ((int64_t(1) << bits) < A.s_w) ++bits;
+        if (hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tmpb, key, key2, perm, perm2, (int)nnz,
+                                                        (int)nseg, seg, seg + 1, 0, bits) != hipSuccess ||
+            hipMalloc(&tmp, tmpb ? tmpb : 1) != hipSuccess ||
+            hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, tmpb, key, key2, perm, perm2, (int)nnz,
+                                                        (int)nseg, seg, seg + 1, 0, bits) != hipSuccess) {
+            rc = -1;
+        } else {
+            hipLaunchKernelGGL(k_ztile_gather, dim3(grid1(nnz)), dim3(256), 0, nullptr, nnz, perm2, key2, erow,
+                               (const double2*)A.s_val, A.t_idx, (double2*)A.t_val);
+            if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+        }
+    }
+    cleanup();
+    if (rc != 0) {
+        if (A.t_idx) (void)hipFree(A.t_idx);
+        if (A.t_val) (void)hipFree(A.t_val);
+        A.t_idx = nullptr;
+        A.t_val = nullptr;
+        return rc;
+    }
+    (void)hipFree(A.s_col);  // the tiles replace the slice CSR's columns and values
+    (void)hipFree(A.s_val);
+    A.s_col = nullptr;
+    A.s_val = nullptr;
+    A.t_nrb = nrb;
+    A.tile = true;
+    return 0;
 }
 
 int zcsr_build_split(ZCsr& A) {
@@ -183,12 +362,20 @@ int zcsr_build_split(ZCsr& A) {
                            A.col, v2, A.s_rp, A.s_base, (int32_t*)A.s_col, (double2*)A.s_val);
     if (hipDeviceSynchronize() != hipSuccess) return fail(-1);
     A.split = true;
+    (void)ztile_build(A);  // optional: the CSR split stays if the tiles cannot be built
     return 0;
 }
 
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
     const auto* x2 = reinterpret_cast<const double2*>(x);
     auto* yp = reinterpret_cast<double2*>(A.s_y);
+    if (A.tile) {
+        hipLaunchKernelGGL(k_ztile, dim3((unsigned)(kSlices * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
+                           A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
+        hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y),
+                           gate);
+        return;
+    }
     const int g = 1024;  // 128 workgroups a slice (tools/zspmv_split.hip)
     if (A.s_col16)
         hipLaunchKernelGGL(k_zsplit_spmv<uint16_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
