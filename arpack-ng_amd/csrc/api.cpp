@@ -284,8 +284,25 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
             // it); a row-distributed SpMV also holds its halo exchange: marker mode
             const double by = dev::csr_bytes(*S->csr);
+            if (S->dist && S->x_ready) {
+                // overlapped: halo + SpMV on op_stream once the update pass has
+                // written x, concurrent with that pass's allreduce + finalize on
+                // a.stream (p2p communicator); a.stream waits for y
+                S->x_ready = false;
+                hipStream_t so = S->op_stream;
+                bool ok = hipStreamWaitEvent(so, S->x_ev, 0) == hipSuccess;
+                dev::prof_begin(dev::kProfSpmv, so);
+                if constexpr (!kShadow) dist_spmv(*S->dist, so, S->op_x, S->op_y, true);
+                dev::prof_end(dev::kProfSpmv, so, by);
+                ok = ok && hipEventRecord(S->y_ev, so) == hipSuccess &&
+                     hipStreamWaitEvent(S->a.stream, S->y_ev, 0) == hipSuccess;
+                if (!ok) {  // cannot order the streams: finish here, serialised
+                    (void)hipStreamSynchronize(so);
+                }
+                continue;
+            }
             if (S->dist) dev::prof_begin(dev::kProfSpmv, S->a.stream);
-            else dev::prof_arm(dev::kProfSpmv);
+            else dev::prof_arm(dev::kProfSpmv, S->a.stream);
             if constexpr (!kShadow) {
                 if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
                 else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);

@@ -13,6 +13,12 @@ namespace ahip {
 
 struct Comm {
     ncclComm_t nccl = nullptr;
+    // a second communicator (ncclCommSplit of nccl, same ranks) for the SpMV's
+    // point-to-point halo / spill exchange on its own stream, so it can run
+    // while the Gram-Schmidt allreduce of the same step is in flight on the
+    // engine's stream (operations of ONE communicator must not be issued to two
+    // streams concurrently); nullptr: everything on nccl, serialised
+    ncclComm_t nccl_p2p = nullptr;
     int rank = 0, nranks = 1, device = 0;
     uint64_t gen = 0;          // distinguishes communicators created at the same address
     double* d_flag = nullptr;  // device scratch of dist_all_ok (allocated at init)
@@ -34,6 +40,7 @@ int comm_size(const Comm* c) { return c ? c->nranks : 1; }
 uint64_t comm_gen(const Comm* c) { return c ? c->gen : 0; }
 bool comm_alive(const Comm* c, uint64_t gen) { return c && c == g_comm && c->gen == gen; }
 double* comm_flag(const Comm* c) { return c ? c->d_flag : nullptr; }
+bool comm_has_p2p(const Comm* c) { return c && c->nccl_p2p; }
 
 // Record an RCCL / HIP failure of a collective: the communicator is marked
 // failed and the engine's drivers turn that into info = -9999 at their next
@@ -93,6 +100,7 @@ static Comm* comm_new(int nranks, int rank, int device) {
 }
 
 static void comm_free(Comm* c) {
+    if (c->nccl_p2p) (void)ncclCommDestroy(c->nccl_p2p);
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     if (c->d_flag) (void)hipFree(c->d_flag);
     delete c;
@@ -122,6 +130,11 @@ int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
             ahip::comm_free(c);
             return -1;
         }
+        // collective on every rank, right here; a failure leaves the serialised
+        // path (also split for one rank, where it carries no traffic, so that the
+        // 1-rank rehearsal runs the overlapped stream schedule too)
+        if (ncclCommSplit(c->nccl, 0, rank, &c->nccl_p2p, nullptr) != ncclSuccess)
+            c->nccl_p2p = nullptr;
     }
     if (ahip::g_comm) arpack_hip_comm_destroy();
     ahip::g_comm = c;
@@ -188,7 +201,7 @@ static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s, bool h
 // Forward "spill" of the symmetric-storage SpMV: send nsend doubles to rank+1,
 // receive nrecv from rank-1 (the reverse of the x halo's hi side).
 void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
-                hipStream_t s) {
+                hipStream_t s, bool p2p) {
     if (!c || c->nranks == 1) return;
     const int r = c->rank, P = c->nranks;
     const int64_t ns = r < P - 1 ? nsend : 0, nr = r > 0 ? nrecv : 0;
@@ -204,29 +217,31 @@ void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, 
         note(c, ok);
         return;
     }
+    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
     bool ok = ncclGroupStart() == ncclSuccess;
-    if (ns) ok = ncclSend(send, (size_t)ns, ncclDouble, r + 1, c->nccl, s) == ncclSuccess && ok;
-    if (nr) ok = ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, c->nccl, s) == ncclSuccess && ok;
+    if (ns) ok = ncclSend(send, (size_t)ns, ncclDouble, r + 1, cm, s) == ncclSuccess && ok;
+    if (nr) ok = ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, cm, s) == ncclSuccess && ok;
     ok = ncclGroupEnd() == ncclSuccess && ok;
     note(c, ok);
 }
 
 // hi_only: the symmetric-storage SpMV reads x only at and above its own rows,
 // so only the hi halo travels (my first rows to rank-1, rank+1's to me).
-void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only) {
+void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only, bool p2p) {
     if (!c || c->nranks == 1) return;
     if (c->h_halo) return comm_halo_host(c, D, s, hi_only);
     const int r = c->rank, P = c->nranks;
+    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
     bool ok = ncclGroupStart() == ncclSuccess;
     auto chk = [&](ncclResult_t e) { ok = ok && e == ncclSuccess; };
     if (r > 0) {
-        if (D.send_lo) chk(ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, c->nccl, s));
-        if (D.halo_lo && !hi_only) chk(ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, c->nccl, s));
+        if (D.send_lo) chk(ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, cm, s));
+        if (D.halo_lo && !hi_only) chk(ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, cm, s));
     }
     if (r < P - 1) {
         if (D.send_hi && !hi_only)
-            chk(ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, c->nccl, s));
-        if (D.halo_hi) chk(ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, c->nccl, s));
+            chk(ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, cm, s));
+        if (D.halo_hi) chk(ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, cm, s));
     }
     chk(ncclGroupEnd());
     note(c, ok);

@@ -321,9 +321,9 @@ void prof_end(ProfClass c, hipStream_t s, double bytes);
 // one's (hipExtLaunchKernel), so the measured time is the kernels' own
 // execution -- what rocprofv3's kernel trace reports -- without marker packets
 // between the launches.  Nested spans are counted in the outermost one.
-void prof_arm(ProfClass c);
+void prof_arm(ProfClass c, hipStream_t s);
 void prof_disarm(ProfClass c, double bytes);
-bool prof_kernel_events(hipEvent_t* start, hipEvent_t* stop);
+bool prof_kernel_events(hipStream_t s, hipEvent_t* start, hipEvent_t* stop);
 void prof_collect(ProfStat out[kProfClasses]);  // synchronises, returns and resets
 
 }  // namespace ahip::dev
@@ -334,7 +334,7 @@ void prof_collect(ProfStat out[kProfClasses]);  // synchronises, returns and res
 #define AHIP_LAUNCH(K, G, B, SH, S, ...)                                                        \
     do {                                                                                       \
         hipEvent_t ahip_ev0_, ahip_ev1_;                                                       \
-        if (::ahip::dev::prof_kernel_events(&ahip_ev0_, &ahip_ev1_))                           \
+        if (::ahip::dev::prof_kernel_events((S), &ahip_ev0_, &ahip_ev1_))                      \
             hipExtLaunchKernelGGL(K, G, B, SH, S, ahip_ev0_, ahip_ev1_, 0, __VA_ARGS__);       \
         else                                                                                   \
             hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                   \

@@ -9,21 +9,21 @@
 #include "dist.hpp"
 
 namespace ahip {
-void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only);
+void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only, bool p2p);
 void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
-                hipStream_t s);
+                hipStream_t s, bool p2p);
 
-void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y) {
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p) {
     if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
     const dev::Csr& A = *D.A;
     const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val;
-    comm_halo(D.comm, D, s, sym);
+    comm_halo(D.comm, D, s, sym, p2p);
     if (sym) {
         // symmetric storage: my rows' upper entries reach the next rank's first
         // rows -- those transposed terms (the spill) travel forward and are
         // combined into the receiver's leading rows (a reverse halo)
         dev::csr_spmv_sym_main(s, A, D.x_ext, y);
-        comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s);
+        comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
         dev::csr_spmv_sym_combine(s, A, y);
         return;
     }

@@ -29,6 +29,8 @@ uint64_t comm_gen(const Comm* c);
 bool comm_alive(const Comm* c, uint64_t gen);
 // one device double owned by the communicator (dist_all_ok's scratch)
 double* comm_flag(const Comm* c);
+// the communicator has its separate point-to-point communicator (RCCL, > 1 rank)
+bool comm_has_p2p(const Comm* c);
 
 // Distributed operator: the local CSR (columns relative to the start of x_ext)
 // plus the halo plan.
@@ -49,6 +51,9 @@ struct DistOp {
 
 // y = A_loc * x for the distributed operator: copy x into x_ext (skipped when
 // the engine already placed it there), halo exchange, local SpMV.
-void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y);
+// p2p: run the halo / spill exchanges on the communicator's separate
+// point-to-point communicator (the SpMV then may run on a stream of its own,
+// concurrently with the engine stream's allreduces)
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p = false);
 
 }  // namespace ahip

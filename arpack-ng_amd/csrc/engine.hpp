@@ -155,6 +155,14 @@ private:
 public:
     const R* op_x = nullptr;  // device pointers of the pending OP request
     R* op_y = nullptr;
+    // overlapped distributed SpMV (RCCL, > 1 rank): the folded update pass
+    // records x_ev once the SpMV's input is written; the driver runs the halo +
+    // SpMV on op_stream after it, concurrently with the update's allreduce and
+    // finalize on a.stream, and a.stream waits y_ev before the next pass
+    hipStream_t op_stream = nullptr;
+    hipEvent_t x_ev = nullptr, y_ev = nullptr;
+    bool x_ready = false;
+    bool overlap_ready();  // creates the stream/events on first use
 };
 using Solver = SolverT<double>;
 

@@ -83,7 +83,7 @@ struct ProfScope {  // kernel-mode span (prof_arm) around one launcher when prof
     ProfClass c;
     hipStream_t s;
     double bytes;
-    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_arm(c); }
+    ProfScope(ProfClass cc, hipStream_t ss, double b) : c(cc), s(ss), bytes(b) { prof_arm(c, s); }
     ~ProfScope() { prof_disarm(c, bytes); }
 };
 }  // namespace

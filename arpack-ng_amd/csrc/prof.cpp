@@ -2,6 +2,7 @@
 // the stream the kernel is launched on, so the measured duration is the
 // kernel's own device time inside the timed region, not host wall time.
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "device.hpp"
@@ -20,10 +21,24 @@ std::vector<hipEvent_t> g_pool;
 std::vector<Pending> g_pending;
 hipEvent_t g_open[kProfClasses] = {};
 ProfStat g_acc[kProfClasses];
-// kernel mode: the open span (one at a time; nested spans count in the outer)
+// kernel mode: the open span (one at a time; nested spans count in the outer),
+// bound to the stream and thread that armed it: launches on other streams or
+// threads get no events and do not count in it
 int g_arm = -1, g_depth = 0;
+hipStream_t g_arm_stream = nullptr;
+std::thread::id g_arm_thread;
 hipEvent_t g_kstart = nullptr, g_kstop = nullptr;
 std::vector<hipEvent_t> g_retire;  // stop events superseded by a later launch
+
+// superseded stop events go back to the pool once their launch has completed
+void recycle_retired_locked() {
+    size_t k = 0;
+    for (hipEvent_t e : g_retire) {
+        if (hipEventQuery(e) == hipSuccess) g_pool.push_back(e);
+        else g_retire[k++] = e;
+    }
+    g_retire.resize(k);
+}
 
 hipEvent_t take() {
     if (!g_pool.empty()) {
@@ -83,7 +98,7 @@ void prof_end(ProfClass c, hipStream_t s, double bytes) {
     g_open[c] = nullptr;
 }
 
-void prof_arm(ProfClass c) {
+void prof_arm(ProfClass c, hipStream_t s) {
     if (!g_on) return;
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_arm >= 0) {
@@ -92,6 +107,8 @@ void prof_arm(ProfClass c) {
     }
     if (g_pending.size() > 4096) drain_locked();
     g_arm = c;
+    g_arm_stream = s;
+    g_arm_thread = std::this_thread::get_id();
     g_kstart = g_kstop = nullptr;
 }
 
@@ -108,13 +125,16 @@ void prof_disarm(ProfClass c, double bytes) {
     g_kstart = g_kstop = nullptr;
 }
 
-bool prof_kernel_events(hipEvent_t* start, hipEvent_t* stop) {
+bool prof_kernel_events(hipStream_t s, hipEvent_t* start, hipEvent_t* stop) {
     *start = *stop = nullptr;
     if (!g_on) return false;
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_arm < 0) return false;
+    if (g_arm < 0 || s != g_arm_stream || std::this_thread::get_id() != g_arm_thread) return false;
     if (!g_kstart) *start = g_kstart = take();
-    if (g_kstop) g_retire.push_back(g_kstop);
+    if (g_kstop) {
+        g_retire.push_back(g_kstop);
+        if (g_retire.size() > 64) recycle_retired_locked();
+    }
     *stop = g_kstop = take();
     return true;
 }

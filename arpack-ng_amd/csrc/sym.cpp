@@ -9,6 +9,7 @@
 //   Solver::getv0  SRC/dgetv0.f:119-421   (start / restart vector)
 //   Solver::sapps  SRC/dsapps.f:131-518   (shifts on T host-side, V*Q on device)
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <type_traits>
@@ -119,10 +120,39 @@ void ArraysT<R>::sync() { ck(hipStreamSynchronize(stream)); }
 template <class R>
 SolverT<R>::~SolverT() {
     // no kernel of this solve may still be writing the caller's arrays
+    if (op_stream) (void)hipStreamSynchronize(op_stream);
     if (a.stream) (void)hipStreamSynchronize(a.stream);
+    if (x_ev) (void)hipEventDestroy(x_ev);
+    if (y_ev) (void)hipEventDestroy(y_ev);
+    if (op_stream) (void)hipStreamDestroy(op_stream);
     root.reset();
     dev::ws_destroy(ws);
     a.release();
+}
+
+// The overlapped distributed SpMV (opt-in, AHIP_DIST_OVERLAP=1) needs RCCL's
+// separate p2p communicator.  Off by default: measured on a 1-rank RCCL
+// communicator at a rank's share of the north star (1.25e6 rows), the two
+// cross-stream event waits per step cost ~20 us of scheduling latency
+// (255-282 vs 301-313 cycles/s) -- about what an 8-rank allreduce + finalize
+// would hide, so the overlap cannot be shown to pay without a multi-GPU run.
+template <class R>
+bool SolverT<R>::overlap_ready() {
+    static const bool off = [] {
+        const char* e = getenv("AHIP_DIST_OVERLAP");
+        return !(e && e[0] == '1');
+    }();
+    if (off || !dist || !dist->A || !comm_has_p2p(dist->comm)) return false;
+    if (!op_stream) {
+        if (hipStreamCreateWithFlags(&op_stream, hipStreamNonBlocking) != hipSuccess) {
+            op_stream = nullptr;
+            return false;
+        }
+        if (hipEventCreateWithFlags(&x_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&y_ev, hipEventDisableTiming) != hipSuccess)
+            return false;
+    }
+    return x_ev && y_ev;
 }
 
 template <class R>
@@ -399,6 +429,10 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             if (folded) {
                 dev::fold_update(ws, nn, j, a.d_v, a.d_ld, wd + irj, a.d_resid,
                                  next_folded ? dist_x() : nullptr);
+                // the next step's SpMV input (the distributed x window) is
+                // complete here: its halo + SpMV may overlap this step's finalize
+                if (next_folded && dist_x() && overlap_ready())
+                    x_ready = hipEventRecord(x_ev, a.stream) == hipSuccess;
             } else {
                 dev::UpdateChain<R> x;
                 x.chained = chained;
