@@ -3,6 +3,7 @@
 // the launcher's control plane (bench.py: torch.distributed over gloo).
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -130,10 +131,13 @@ int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
             ahip::comm_free(c);
             return -1;
         }
-        // collective on every rank, right here; a failure leaves the serialised
-        // path (also split for one rank, where it carries no traffic, so that the
-        // 1-rank rehearsal runs the overlapped stream schedule too)
-        if (ncclCommSplit(c->nccl, 0, rank, &c->nccl_p2p, nullptr) != ncclSuccess)
+        // only for the opt-in overlapped SpMV (AHIP_DIST_OVERLAP=1; the variable
+        // must be the same on every rank): collective on every rank, right here;
+        // a failure leaves the serialised path (also split for one rank, where it
+        // carries no traffic, so the 1-rank rehearsal runs that stream schedule)
+        const char* ov = std::getenv("AHIP_DIST_OVERLAP");
+        if (ov && ov[0] == '1' &&
+            ncclCommSplit(c->nccl, 0, rank, &c->nccl_p2p, nullptr) != ncclSuccess)
             c->nccl_p2p = nullptr;
     }
     if (ahip::g_comm) arpack_hip_comm_destroy();
