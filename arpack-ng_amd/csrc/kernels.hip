@@ -475,7 +475,11 @@ __global__ void k_zero_if(int64_t n, R* r, const LzState* st) {
 }
 
 // -------------------------------------------------------------- V*Q update --
-template <class R, int MAXK, int POL = kPolNt>
+// NTS: non-temporal stores of the kev+1 new columns and r.  tools/vq_bench.hip
+// (this pass's shape, 31 columns read + 12 written, n = 1e7): plain stores
+// 0.683 ms = 5.04 TB/s -- what this kernel reaches -- non-temporal 0.610 ms
+// = 5.64 TB/s; reads alone 0.351 ms = 7.06 TB/s.
+template <class R, int MAXK, int POL = kPolNt, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t ld,
                                                       int kplusp, int kev,
                                                       const double* __restrict__ Q, int ldq,
@@ -504,22 +508,26 @@ __global__ __launch_bounds__(kBlock) void k_vq_update(int64_t n, R* V, int64_t l
             for (int k = 0; k < MAXK; ++k)
                 if (k < kplusp) vnext += v[k] * q[k];
         }
+        auto st_ = [](R* p, R x) {
+            if constexpr (NTS) __builtin_nontemporal_store(x, p);
+            else *p = x;
+        };
         for (int l = 0; l < kev; ++l) {
             const double* q = sq + l * kplusp;
             double o = 0.0;
 #pragma unroll
             for (int k = 0; k < MAXK; ++k)
                 if (k < kplusp) o += v[k] * q[k];
-            V[i + (int64_t)l * ld] = (R)o;
+            st_(V + i + (int64_t)l * ld, (R)o);
         }
         double ri = sigmak * (double)r[i];
         if (next) {
             const R vn = (R)vnext;
-            V[i + (int64_t)kev * ld] = vn;
+            st_(V + i + (int64_t)kev * ld, vn);
             ri += betak * (double)vn;
         }
         const R rs = (R)ri;
-        r[i] = rs;
+        st_(r + i, rs);
         rr += (double)rs * (double)rs;
     }
     double acc[1] = {0.0};
@@ -951,9 +959,19 @@ void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int
         AHIP_LAUNCH(kern, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld, kplusp, kev, ws.q,
                            kplusp, sigmak, betak, r, ws.part, ws.stride);
     };
-    if (kplusp <= 16) ws.v_plain ? go(k_vq_update<R, 16, kPolPlain>) : go(k_vq_update<R, 16>);
-    else if (kplusp <= 32) ws.v_plain ? go(k_vq_update<R, 32, kPolPlain>) : go(k_vq_update<R, 32>);
-    else if (kplusp <= 64) ws.v_plain ? go(k_vq_update<R, 64, kPolPlain>) : go(k_vq_update<R, 64>);
+    // AHIP_VQ_NTS=0: plain stores of the new columns (the V-load policy's
+    // plain-load case keeps plain stores: there the next pass re-reads V from
+    // the Infinity Cache)
+    static const bool nts = [] {
+        const char* e = getenv("AHIP_VQ_NTS");
+        return !(e && e[0] == '0');
+    }();
+    if (kplusp <= 16) ws.v_plain ? go(k_vq_update<R, 16, kPolPlain>)
+                      : nts ? go(k_vq_update<R, 16, kPolNt, true>) : go(k_vq_update<R, 16>);
+    else if (kplusp <= 32) ws.v_plain ? go(k_vq_update<R, 32, kPolPlain>)
+                           : nts ? go(k_vq_update<R, 32, kPolNt, true>) : go(k_vq_update<R, 32>);
+    else if (kplusp <= 64) ws.v_plain ? go(k_vq_update<R, 64, kPolPlain>)
+                           : nts ? go(k_vq_update<R, 64, kPolNt, true>) : go(k_vq_update<R, 64>);
     else  // ws.scratch: nblk * kBlock * (ncv + 1) doubles, allocated by ws_create for ncv > 64
         AHIP_LAUNCH(k_vq_update_generic<R>, dim3(g), dim3(kBlock), 0, ws.stream, n, V, ld,
                            kplusp, kev, ws.q, kplusp, sigmak, betak, r, ws.scratch, ws.part,

@@ -237,7 +237,7 @@ int main() {
     };
     const double stream = 18.0 * nnz + 4.0 * 8 * (n + 1) + 16.0 * 8 * n;  // val + colr + rps + partials
     // column-sorted tile layout (block b = rb * 8 + s), for RB = 2048 and 4096
-    for (int RB : {2048, 4096}) {
+    for (int RB : {4096, 8192}) {
         for (int sorted = 0; sorted < 2; ++sorted) {
             const int64_t nrb = (n + RB - 1) / RB;
             std::vector<int64_t> boff(8 * nrb + 1, 0);
@@ -279,7 +279,12 @@ int main() {
                     kern<<<grid, 256, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp);
                 });
             };
-            const float t1 = runt(k_ztile<1>), t4 = runt(k_ztile<4>), t8 = runt(k_ztile<8>);
+            if (lds > 65536) {
+                CK(hipFuncSetAttribute((const void*)k_ztile<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                CK(hipFuncSetAttribute((const void*)k_ztile<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                CK(hipFuncSetAttribute((const void*)k_ztile<6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            }
+            const float t1 = runt(k_ztile<2>), t4 = runt(k_ztile<4>), t8 = runt(k_ztile<6>);
             // check against the CSR-split probe (MODE 0) partials
             std::vector<double2> ya(8 * n), yb(8 * n);
             CK(hipMemcpy(ya.data(), d_yp, 16 * 8 * n, hipMemcpyDeviceToHost));
@@ -290,7 +295,7 @@ int main() {
                 err = std::max(err, std::hypot(ya[i].x - yb[i].x, ya[i].y - yb[i].y));
                 sc = std::max(sc, std::hypot(yb[i].x, yb[i].y));
             }
-            printf("tile RB %d %s: U1 %.3f  U4 %.3f  U8 %.3f ms  (max rel diff %.1e)\n", RB,
+            printf("tile RB %d %s: U2 %.3f  U4 %.3f  U6 %.3f ms  (max rel diff %.1e)\n", RB,
                    sorted ? "column-sorted" : "row order   ", t1, t4, t8, err / sc);
             CK(hipFree(d_boff));
             CK(hipFree(d_tidx));
