@@ -150,6 +150,60 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, int rb_row
     for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
 }
 
+
+// k_ztile with the next batch's index/value loads issued before this batch's
+// gathers (software pipelined) and a block of T threads
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_ztile_pipe(int64_t n, int64_t sw, int rb_rows,
+                                                  const int64_t* __restrict__ boff,
+                                                  const uint32_t* __restrict__ idx,
+                                                  const double2* __restrict__ val,
+                                                  const double2* __restrict__ x,
+                                                  double2* __restrict__ yp) {
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    extern __shared__ double ylds[];
+    const int s = (int)(blockIdx.x & 7);
+    const int64_t r0 = (int64_t)(blockIdx.x >> 3) * rb_rows;
+    const int rows = (int)((n - r0) < rb_rows ? (n - r0) : rb_rows);
+    for (int i = threadIdx.x; i < 2 * rows; i += T) ylds[i] = 0.0;
+    __syncthreads();
+    const double2* xs = x + (int64_t)s * sw;
+    const int64_t e0 = boff[blockIdx.x], e1 = boff[blockIdx.x + 1];
+    int64_t e = e0 + threadIdx.x;
+    uint32_t id[U];
+    dv2 v[U];
+    auto load = [&](int64_t b) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = b + u * T;
+            id[u] = q < e1 ? __builtin_nontemporal_load(&idx[q]) : 0u;
+            v[u] = q < e1 ? __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + q) : dv2{0.0, 0.0};
+        }
+    };
+    load(e);
+    for (; e < e1; e += U * T) {
+        uint32_t idc[U];
+        dv2 vc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { idc[u] = id[u]; vc[u] = v[u]; }
+        load(e + U * T);
+        double2 xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = xs[idc[u] & 0xffffu];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (e + u * T < e1) {
+                const int r = (int)(idc[u] >> 16);
+                atomicAdd(&ylds[2 * r], vc[u].x * xv[u].x - vc[u].y * xv[u].y);
+                atomicAdd(&ylds[2 * r + 1], vc[u].x * xv[u].y + vc[u].y * xv[u].x);
+            }
+        }
+    }
+    __syncthreads();
+    double2* y = yp + (int64_t)s * n + r0;
+    for (int i = threadIdx.x; i < rows; i += T) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
+}
+
 static uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -285,6 +339,14 @@ int main() {
                 CK(hipFuncSetAttribute((const void*)k_ztile<6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             }
             const float t1 = runt(k_ztile<2>), t4 = runt(k_ztile<4>), t8 = runt(k_ztile<6>);
+            if (RB == 4096 && sorted) {
+                const float p2 = timeit([&] { k_ztile_pipe<2, 256><<<grid, 256, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp); });
+                const float p4 = timeit([&] { k_ztile_pipe<4, 256><<<grid, 256, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp); });
+                const float q4 = timeit([&] { k_ztile_pipe<4, 512><<<grid, 512, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp); });
+                const float q2 = timeit([&] { k_ztile_pipe<2, 512><<<grid, 512, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp); });
+                const float w4 = timeit([&] { k_ztile_pipe<4, 1024><<<grid, 1024, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp); });
+                printf("pipelined RB 4096 sorted: T256 U2 %.3f U4 %.3f | T512 U2 %.3f U4 %.3f | T1024 U4 %.3f ms\n", p2, p4, q2, q4, w4);
+            }
             // check against the CSR-split probe (MODE 0) partials
             std::vector<double2> ya(8 * n), yb(8 * n);
             CK(hipMemcpy(ya.data(), d_yp, 16 * 8 * n, hipMemcpyDeviceToHost));
