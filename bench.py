@@ -77,16 +77,16 @@ def pmc_traffic(kernel_substr: str):
     summary (profiles/r*_pmc.json, written by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes of this same command, gfx950-corrected)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as fh:
-        ks = json.load(fh)["kernels"]
-    hits = [v for k, v in ks.items() if kernel_substr in k]
-    if not hits:
-        return None, None
-    v = max(hits, key=lambda e: e["launches"])
-    return v["traffic_bytes"], os.path.basename(files[-1])
+    # the newest profile set that measured this kernel (other configs' PMC
+    # summaries, e.g. the complex kernels', live beside it)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        with open(f) as fh:
+            ks = json.load(fh).get("kernels", {})
+        hits = [v for k, v in ks.items() if kernel_substr in k]
+        if hits:
+            v = max(hits, key=lambda e: e["launches"])
+            return v["traffic_bytes"], os.path.basename(f)
+    return None, None
 
 
 def cpu_share():

@@ -105,3 +105,28 @@ def test_pdnaupd_c_matches_dnaupd(pkg, golden, comm1):
     assert int(s2.iparam[2]) == int(g["iparam"][2])
     r1, r2 = s1.eupd(), s2.eupd(dist=D)
     assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
+
+
+def test_overlapped_distributed_spmv_same_solve(tmp_path):
+    """AHIP_DIST_OVERLAP=1 (opt-in): the distributed free run with the next
+    step's halo + SpMV on a second stream and a split p2p communicator must
+    give the same solve as the serialised schedule -- on a 1-rank RCCL
+    communicator (bench.py --force-dist), the time-to-converge solve's restart
+    cycles, OP*x count and converged count are equal with and without it.  Run
+    in subprocesses: the switch is read once per process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for ov in ("0", "1"):
+        env = dict(os.environ, AHIP_DIST_OVERLAP=ov)
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--force-dist",
+                            "--rows", "400000", "--steps", "3", "--warmup", "1",
+                            "--no-cpu-baseline", "--no-full-storage", "--steady-cycles", "0"],
+                           env=env, capture_output=True, text=True, timeout=300, cwd=root)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[ov] = json.loads(r.stdout.strip().splitlines()[-1])["time_to_converge"]
+    for k in ("iters", "nopx", "nconv", "info"):
+        assert res["0"][k] == res["1"][k], (k, res)

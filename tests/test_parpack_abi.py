@@ -79,3 +79,19 @@ def test_pdnorm2_collective(tmp_path):
     x = np.concatenate([(k + 1) * 1e150 * np.arange(1, 7) for k in range(2)])
     assert abs(a - np.linalg.norm(x)) <= 1e-14 * np.linalg.norm(x)
     assert abs(b - np.linalg.norm(x)) <= 1e-14 * np.linalg.norm(x)  # 3 complex = 6 reals a rank
+
+
+def test_parpack_reference_fixtures_parse():
+    """The recorded outputs of the reference's PARPACK programs
+    (tests/golden/preftests, tests/golden/make_preftests.py) hold a Ritz table
+    and the converged / cycle / OP*x counts the GPU test compares, for 1 and 2
+    ranks, and every recorded run exited 0."""
+    import json
+    from test_gpu_reftests import parse
+    gold = os.path.join(ROOT, "tests", "golden", "preftests")
+    rcs = json.load(open(os.path.join(gold, "rc.json")))
+    assert len(rcs) == 18 and all(v == 0 for v in rcs.values())
+    for key in rcs:
+        rows, counts = parse(open(os.path.join(gold, key + ".out")).read())
+        assert rows and counts["nconv"] and counts["iters"] and counts["nopx"], key
+
