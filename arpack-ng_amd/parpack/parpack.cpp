@@ -153,7 +153,6 @@ arpack_hip_dist* dist_for(MPI_Fint fcomm, int64_t nloc) {
     return D;
 }
 
-template <class T>
 void fail(a_int* ido, a_int* info) {  // no decomposition (MPI / device setup failed)
     *info = -9999;
     if (ido) *ido = 99;
@@ -213,7 +212,7 @@ void pdsaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_pdsaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
 }
@@ -223,7 +222,7 @@ void pdseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int* iparam, a_int* ipntr, double* workd, double* workl, a_int lworkl,
                a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_pdseupd_c(D, rvec, howmny, select, d, z, ldz, sigma, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, info);
 }
@@ -231,7 +230,7 @@ void pssaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_pssaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
 }
@@ -240,7 +239,7 @@ void psseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int nev, float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_psseupd_c(D, rvec, howmny, select, d, z, ldz, sigma, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, info);
 }
@@ -248,7 +247,7 @@ void pdnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_pdnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
 }
@@ -258,7 +257,7 @@ void pdneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int ncv, double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
                double* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_pdneupd_c(D, rvec, howmny, select, dr, di, z, ldz, sigmar, sigmai, workev, bmat, n,
                          which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
                          info);
@@ -267,7 +266,7 @@ void psnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_psnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
 }
@@ -277,7 +276,7 @@ void psneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int ncv, float* v, a_int ldv, a_int* iparam, a_int* ipntr, float* workd,
                float* workl, a_int lworkl, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_psneupd_c(D, rvec, howmny, select, dr, di, z, ldz, sigmar, sigmai, workev, bmat, n,
                          which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
                          info);
@@ -286,7 +285,7 @@ void pznaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                double tol, zc* resid, a_int ncv, zc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                zc* workd, zc* workl, a_int lworkl, double* rwork, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_pznaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
 }
@@ -295,7 +294,7 @@ void pzneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int nev, double tol, zc* resid, a_int ncv, zc* v, a_int ldv, a_int* iparam,
                a_int* ipntr, zc* workd, zc* workl, a_int lworkl, double* rwork, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<double>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_pzneupd_c(D, rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
 }
@@ -303,7 +302,7 @@ void pcnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const*
                float tol, cc* resid, a_int ncv, cc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                cc* workd, cc* workl, a_int lworkl, float* rwork, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(ido, info);
+    if (!D) return fail(ido, info);
     arpack_hip_pcnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
 }
@@ -312,7 +311,7 @@ void pcneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int nev, float tol, cc* resid, a_int ncv, cc* v, a_int ldv, a_int* iparam,
                a_int* ipntr, cc* workd, cc* workl, a_int lworkl, float* rwork, a_int* info) {
     arpack_hip_dist* D = dist_for(comm, n);
-    if (!D) return fail<float>(nullptr, info);
+    if (!D) return fail(nullptr, info);
     arpack_hip_pcneupd_c(D, rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
 }
