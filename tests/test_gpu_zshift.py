@@ -103,3 +103,19 @@ def test_znaupd_mode3_argument_checks(pkg):
     assert s.aupd_zshift(S) == 99 and int(s.info[0]) == -11
     s = pkg.ZRci(1999, 6, 20, "LM", 1e-10, mode=3)  # n must be the operator's
     assert s.aupd_zshift(S) == 99 and int(s.info[0]) == -11
+
+
+def test_zshift_singular_shift_fails_loudly(pkg):
+    """sigma on an eigenvalue: A - sigma I is singular, BiCGStab cannot reach
+    rtol -- the solve reports -1 (a counted failure, never a silent result) and
+    a mode-3 run served by it ends with info = -9999."""
+    rp, col, val = M.zdiag_icb(1000)  # diag (k+1)(1+i)
+    Z = pkg.ZCSR.from_arrays(rp, col, val)
+    S = pkg.ZShift(Z, 5 * (1 + 1j), rtol=1e-12, maxit=30)
+    x = np.random.default_rng(1).standard_normal(1000) + 0j
+    _, it, rr = S.solve(x)
+    assert it == -1
+    assert S.stats()["failures"] == 1
+    s = pkg.ZRci(1000, 4, 12, "LM", 1e-8, mode=3, mxiter=50)
+    assert s.aupd_zshift(S) == 99
+    assert int(s.info[0]) == -9999
