@@ -82,6 +82,12 @@ void zcsr_free_split(ZCsr& A);
 // gate (device int, may be null): the kernels return at once while *gate != 0
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y,
                      const int* gate = nullptr);
+// The slice products alone (no combine): y_s = A(:, slice s) x into A.s_y (8 x n
+// complex, slice-major), for a caller that sums them in zc::slice_sum's order
+// inside its own pass (zsolve.hip).  Returns A.s_y; nullptr (nothing launched)
+// when A is not split.
+const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x,
+                                  const int* gate = nullptr);
 hipError_t ws_create(Ws& ws, int64_t n, int ncv, hipStream_t s);
 void ws_destroy(Ws& ws);
 // Launchers over the component type R of the interleaved complex vectors

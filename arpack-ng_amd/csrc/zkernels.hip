@@ -453,11 +453,19 @@ void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const i
 int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift) {
     if (per_row < 1 || per_row > kMaxPerRow) return -1;
     int64_t *cnt = nullptr, *rp = nullptr;
-    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1))) return -1;
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    auto fail = [&]() {  // every HIP error ends here: nothing leaks, A stays empty
+        for (void* q : {(void*)cnt, (void*)rp, (void*)col, (void*)val})
+            if (q) (void)hipFree(q);
+        return -1;
+    };
+    if (hipMalloc(&cnt, sizeof(int64_t) * (n + 1)) || hipMalloc(&rp, sizeof(int64_t) * (n + 1)))
+        return fail();
     const uint32_t sm = mix32(seed);
     hipLaunchKernelGGL(k_zgen_count, dim3(grid(n, 65536)), dim3(kB), 0, nullptr, n, sm, per_row, cnt);
     std::vector<int64_t> h(n + 1);
-    (void)hipMemcpy(h.data(), cnt, sizeof(int64_t) * n, hipMemcpyDeviceToHost);
+    if (hipMemcpy(h.data(), cnt, sizeof(int64_t) * n, hipMemcpyDeviceToHost)) return fail();
     int64_t acc = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t c = h[i];
@@ -465,14 +473,15 @@ int gen_zrandom(ZCsr& A, int64_t n, int per_row, uint32_t seed, double dshift) {
         acc += c;
     }
     h[n] = acc;
-    (void)hipMemcpy(rp, h.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice);
+    if (hipMemcpy(rp, h.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice)) return fail();
     (void)hipFree(cnt);
-    int32_t* col = nullptr;
-    double* val = nullptr;
-    if (hipMalloc(&col, sizeof(int32_t) * acc) || hipMalloc(&val, sizeof(double) * 2 * acc)) return -1;
+    cnt = nullptr;
+    if (hipMalloc(&col, sizeof(int32_t) * (acc ? acc : 1)) ||
+        hipMalloc(&val, sizeof(double) * 2 * (acc ? acc : 1)))
+        return fail();
     hipLaunchKernelGGL(k_zgen_fill, dim3(grid(n, 65536)), dim3(kB), 0, nullptr, n, sm, per_row, dshift, rp,
                        col, reinterpret_cast<double2*>(val));
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return fail();
     A.n = n;
     A.nnz = acc;
     A.rowptr = rp;

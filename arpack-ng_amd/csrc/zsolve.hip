@@ -3,11 +3,11 @@
 //
 // One iteration (k = 0, 1, ...), complex inner products (a, b) = a^H b:
 //
-//   w = A p                      zcsr_spmv (XCD split)          gated
-//   v = w - sigma p;   P0 <- partials of rh^H v               k_bi_v
+//   w = A p                      split slice products           gated
+//   v = w - sigma p;   P0 <- partials of rh^H v               k_bi_v   (sums the slices)
 //   alpha = rho_k / (rh^H v);   s = r - alpha v               k_bi_s   (reduces P0)
-//   w = A s                      zcsr_spmv                      gated
-//   t = w - sigma s;   P0 <- partials of t^H s, t^H t         k_bi_t
+//   w = A s                      split slice products           gated
+//   t = w - sigma s;   P0 <- partials of t^H s, t^H t         k_bi_t   (sums the slices)
 //   omega = (t^H s)/(t^H t);  y += alpha p + omega s;
 //   r = s - omega t;   P1 <- partials of rh^H r, r^H r        k_bi_xr  (reduces P0)
 //   rho_{k+1} = rh^H r;  stop if ||r|| <= rtol ||b||;
@@ -19,7 +19,10 @@
 // device state for the later kernels.  A kernel never writes the partial
 // buffer it reads (P0 / P1 alternate).  When k_bi_p decides to stop it sets
 // st.done, and every later kernel of the chunk -- the SpMVs included -- returns
-// at once.
+// at once.  On the XCD-split operator the SpMV's combine is fused into k_bi_v /
+// k_bi_t (the 8 slice partials summed in the combine's order, zc::slice_sum: the
+// same w bit for bit, without storing and re-reading it); an unsplit operator
+// goes through zcsr_spmv and w.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -108,7 +111,16 @@ __global__ __launch_bounds__(kT) void k_bi_init_fin(const double* __restrict__ p
     }
 }
 
+// w = A x: the SpMV's output, or (SPLIT) the split operator's 8 slice partials
+// summed here in the combine's fixed order (zc::slice_sum) -- one pass less
+template <bool SPLIT>
+__device__ __forceinline__ double2 op_row(const double2* __restrict__ w, int64_t n, int64_t i) {
+    if constexpr (SPLIT) return slice_sum(w, n, i);
+    else return w[i];
+}
+
 // v = w - sigma p; partials of rh^H v
+template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_bi_v(int64_t n, const double2* __restrict__ w,
                                              const double2* __restrict__ p,
                                              const double2* __restrict__ rh, double2* __restrict__ v,
@@ -117,7 +129,7 @@ __global__ __launch_bounds__(kT) void k_bi_v(int64_t n, const double2* __restric
     if (st->done) return;
     double acc[2] = {0.0, 0.0};
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const double2 pi = p[i], wi = w[i];
+        const double2 pi = p[i], wi = op_row<SPLIT>(w, n, i);
         const double2 sp = cmul(sigma, pi);
         const double2 vi = make_double2(wi.x - sp.x, wi.y - sp.y);
         v[i] = vi;
@@ -152,6 +164,7 @@ __global__ __launch_bounds__(kT) void k_bi_s(int64_t n, const double2* __restric
 }
 
 // t = w - sigma s; partials of t^H s (complex), t^H t
+template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_bi_t(int64_t n, const double2* __restrict__ w,
                                              const double2* __restrict__ s, double2* __restrict__ t,
                                              double2 sigma, const BiState* __restrict__ st,
@@ -159,7 +172,7 @@ __global__ __launch_bounds__(kT) void k_bi_t(int64_t n, const double2* __restric
     if (st->done) return;
     double acc[3] = {0.0, 0.0, 0.0};
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const double2 si = s[i], wi = w[i];
+        const double2 si = s[i], wi = op_row<SPLIT>(w, n, i);
         const double2 ss = cmul(sigma, si);
         const double2 ti = make_double2(wi.x - ss.x, wi.y - ss.y);
         t[i] = ti;
@@ -286,6 +299,8 @@ void zshift_destroy(ZShift& S) {
 
 double zshift_iter_bytes(const ZShift& S) {
     const double n = (double)S.n, nnz = (double)S.A->nnz;
+    if (S.A->split)  // the products feed v and t directly: no w stored and re-read
+        return 2.0 * (20.0 * nnz + 8.0 * (n + 1) + 16.0 * n) + 304.0 * n;  // 19 n-vectors
     const double spmv = 20.0 * nnz + 8.0 * (n + 1) + 32.0 * n;  // val+col, rowptr, x, y
     return 2.0 * spmv + 336.0 * n;  // + v, s, t, (y, r), p passes (21 complex n-vectors)
 }
@@ -300,6 +315,13 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
     auto* y2 = reinterpret_cast<D2*>(y);
     auto V = [](double* q) { return reinterpret_cast<D2*>(q); };
     const int* gate = &S.st->done;
+    // w = A x; on a split operator only its slice partials, summed by k_bi_v / k_bi_t
+    const bool split = S.A->split;
+    auto op = [&](double* x) -> const D2* {
+        if (split) return reinterpret_cast<const D2*>(zcsr_split_partials(strm, *S.A, x, gate));
+        zcsr_spmv(strm, *S.A, x, S.w, gate);
+        return V(S.w);
+    };
     if (hipEventRecord(S.ev0, strm) != hipSuccess) return -2;
     hipLaunchKernelGGL(k_bi_init, dim3(nb), dim3(kT), 0, strm, n, reinterpret_cast<const D2*>(b),
                        V(S.r), V(S.rh), V(S.p), y2, P0, nb);
@@ -310,14 +332,14 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
     while (k < S.maxit) {
         const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
         for (int q = 0; q < m; ++q, ++k) {
-            zcsr_spmv(strm, *S.A, S.p, S.w, gate);
-            hipLaunchKernelGGL(k_bi_v, dim3(nb), dim3(kT), 0, strm, n, V(S.w), V(S.p), V(S.rh),
-                               V(S.v), sig, S.st, P0, nb);
+            const D2* w = op(S.p);
+            hipLaunchKernelGGL(split ? k_bi_v<true> : k_bi_v<false>, dim3(nb), dim3(kT), 0, strm, n,
+                               w, V(S.p), V(S.rh), V(S.v), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_s, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.v), V(S.s), S.st,
                                k, P0, nb);
-            zcsr_spmv(strm, *S.A, S.s, S.w, gate);
-            hipLaunchKernelGGL(k_bi_t, dim3(nb), dim3(kT), 0, strm, n, V(S.w), V(S.s), V(S.t), sig,
-                               S.st, P0, nb);
+            w = op(S.s);
+            hipLaunchKernelGGL(split ? k_bi_t<true> : k_bi_t<false>, dim3(nb), dim3(kT), 0, strm, n,
+                               w, V(S.s), V(S.t), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_xr, dim3(nb), dim3(kT), 0, strm, n, y2, V(S.p), V(S.s), V(S.t),
                                V(S.r), V(S.rh), S.st, P0, P1, nb);
             hipLaunchKernelGGL(k_bi_p, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.p), V(S.v), S.st,

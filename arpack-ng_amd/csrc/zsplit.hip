@@ -24,7 +24,7 @@ namespace ahip::zdev {
 
 namespace {
 using namespace zc;
-constexpr int kSlices = 8;  // = XCDs
+constexpr int kSlices = zc::kZSlices;
 constexpr int kLanes = 8;   // lanes per row (tools/zspmv_split.hip: 8 of 4/8/16)
 
 __global__ void k_zsplit_count(int64_t n, int64_t sw, const int64_t* __restrict__ rp,
@@ -97,13 +97,8 @@ __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
 __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, double2* __restrict__ y,
                                  const int* __restrict__ gate) {
     if (gate && *gate) return;
-    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
-        double2 a[kSlices];
-#pragma unroll
-        for (int s = 0; s < kSlices; ++s) a[s] = yp[(int64_t)s * n + r];
-        y[r] = make_double2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
-                            ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
-    }
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256)
+        y[r] = zc::slice_sum(yp, n, r);
 }
 
 // ---- column-sorted tiles --------------------------------------------------
@@ -366,15 +361,14 @@ int zcsr_build_split(ZCsr& A) {
     return 0;
 }
 
-void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
+const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x, const int* gate) {
+    if (!A.split) return nullptr;
     const auto* x2 = reinterpret_cast<const double2*>(x);
     auto* yp = reinterpret_cast<double2*>(A.s_y);
     if (A.tile) {
         hipLaunchKernelGGL(k_ztile, dim3((unsigned)(kSlices * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
                            A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
-        hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y),
-                           gate);
-        return;
+        return A.s_y;
     }
     const int g = 1024;  // 128 workgroups a slice (tools/zspmv_split.hip)
     if (A.s_col16)
@@ -383,6 +377,11 @@ void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, c
     else
         hipLaunchKernelGGL(k_zsplit_spmv<int32_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
                            (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
+    return A.s_y;
+}
+
+void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
+    const auto* yp = reinterpret_cast<const double2*>(zcsr_split_partials(s, A, x, gate));
     hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y),
                        gate);
 }
