@@ -53,11 +53,12 @@ struct ZCsr {
     const int32_t* col = nullptr;
     const double* val = nullptr;  // interleaved complex
     bool owned = false;
-    // XCD column split (zsplit.hip, zcsr_build_split): the columns cut into 8
+    // XCD column split (zsplit.hip, zcsr_build_split): the columns cut into s_n
     // slices of sw; slice s's entries as a CSR of their own (int32 row offsets
     // s_rp[s*(n+1) + r] relative to s_base[s]), slice-relative columns (16 bit
-    // when sw <= 65536), partial products y_s in s_y (8 x n complex)
+    // when sw <= 65536), partial products y_s in s_y (s_n x n complex)
     bool split = false;
+    int s_n = 8;  // column slices: 4 or 8 (zcsr_build_split)
     int64_t s_w = 0;
     bool s_col16 = true;
     int32_t* s_rp = nullptr;
@@ -82,8 +83,8 @@ void zcsr_free_split(ZCsr& A);
 // gate (device int, may be null): the kernels return at once while *gate != 0
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y,
                      const int* gate = nullptr);
-// The slice products alone (no combine): y_s = A(:, slice s) x into A.s_y (8 x n
-// complex, slice-major), for a caller that sums them in zc::slice_sum's order
+// The slice products alone (no combine): y_s = A(:, slice s) x into A.s_y (s_n x
+// n complex, slice-major), for a caller that sums them in zc::slice_sum's order
 // inside its own pass (zsolve.hip).  Returns A.s_y; nullptr (nothing launched)
 // when A is not split.
 const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x,

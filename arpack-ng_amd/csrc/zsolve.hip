@@ -111,16 +111,16 @@ __global__ __launch_bounds__(kT) void k_bi_init_fin(const double* __restrict__ p
     }
 }
 
-// w = A x: the SpMV's output, or (SPLIT) the split operator's 8 slice partials
+// w = A x: the SpMV's output (S = 0), or the split operator's S slice partials
 // summed here in the combine's fixed order (zc::slice_sum) -- one pass less
-template <bool SPLIT>
+template <int S>
 __device__ __forceinline__ double2 op_row(const double2* __restrict__ w, int64_t n, int64_t i) {
-    if constexpr (SPLIT) return slice_sum(w, n, i);
+    if constexpr (S > 0) return slice_sum<S>(w, n, i);
     else return w[i];
 }
 
 // v = w - sigma p; partials of rh^H v
-template <bool SPLIT>
+template <int S>
 __global__ __launch_bounds__(kT) void k_bi_v(int64_t n, const double2* __restrict__ w,
                                              const double2* __restrict__ p,
                                              const double2* __restrict__ rh, double2* __restrict__ v,
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kT) void k_bi_v(int64_t n, const double2* __restric
     if (st->done) return;
     double acc[2] = {0.0, 0.0};
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const double2 pi = p[i], wi = op_row<SPLIT>(w, n, i);
+        const double2 pi = p[i], wi = op_row<S>(w, n, i);
         const double2 sp = cmul(sigma, pi);
         const double2 vi = make_double2(wi.x - sp.x, wi.y - sp.y);
         v[i] = vi;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kT) void k_bi_s(int64_t n, const double2* __restric
 }
 
 // t = w - sigma s; partials of t^H s (complex), t^H t
-template <bool SPLIT>
+template <int S>
 __global__ __launch_bounds__(kT) void k_bi_t(int64_t n, const double2* __restrict__ w,
                                              const double2* __restrict__ s, double2* __restrict__ t,
                                              double2 sigma, const BiState* __restrict__ st,
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kT) void k_bi_t(int64_t n, const double2* __restric
     if (st->done) return;
     double acc[3] = {0.0, 0.0, 0.0};
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const double2 si = s[i], wi = op_row<SPLIT>(w, n, i);
+        const double2 si = s[i], wi = op_row<S>(w, n, i);
         const double2 ss = cmul(sigma, si);
         const double2 ti = make_double2(wi.x - ss.x, wi.y - ss.y);
         t[i] = ti;
@@ -316,7 +316,8 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
     auto V = [](double* q) { return reinterpret_cast<D2*>(q); };
     const int* gate = &S.st->done;
     // w = A x; on a split operator only its slice partials, summed by k_bi_v / k_bi_t
-    const bool split = S.A->split;
+    const int ns = S.A->split ? S.A->s_n : 0;
+    const bool split = ns > 0;
     auto op = [&](double* x) -> const D2* {
         if (split) return reinterpret_cast<const D2*>(zcsr_split_partials(strm, *S.A, x, gate));
         zcsr_spmv(strm, *S.A, x, S.w, gate);
@@ -333,12 +334,12 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
         const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
         for (int q = 0; q < m; ++q, ++k) {
             const D2* w = op(S.p);
-            hipLaunchKernelGGL(split ? k_bi_v<true> : k_bi_v<false>, dim3(nb), dim3(kT), 0, strm, n,
+            hipLaunchKernelGGL(ns == 4 ? k_bi_v<4> : ns == 8 ? k_bi_v<8> : k_bi_v<0>, dim3(nb), dim3(kT), 0, strm, n,
                                w, V(S.p), V(S.rh), V(S.v), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_s, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.v), V(S.s), S.st,
                                k, P0, nb);
             w = op(S.s);
-            hipLaunchKernelGGL(split ? k_bi_t<true> : k_bi_t<false>, dim3(nb), dim3(kT), 0, strm, n,
+            hipLaunchKernelGGL(ns == 4 ? k_bi_t<4> : ns == 8 ? k_bi_t<8> : k_bi_t<0>, dim3(nb), dim3(kT), 0, strm, n,
                                w, V(S.s), V(S.t), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_xr, dim3(nb), dim3(kT), 0, strm, n, y2, V(S.p), V(S.s), V(S.t),
                                V(S.r), V(S.rh), S.st, P0, P1, nb);

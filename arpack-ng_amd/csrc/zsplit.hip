@@ -1,9 +1,11 @@
 // XCD column split of the complex CSR operator (config 5: n = 5e5, ~100
 // random columns a row).  x (8 MB) does not fit one XCD's 4 MB L2, so the
 // wave-per-row kernel's random gathers miss to the Infinity Cache (0.63 ms,
-// 1.6 TB/s of algorithmic bytes).  Here the columns are cut into 8 slices of
-// x; workgroup b works on slice b % 8 -- the hardware deals workgroups
-// round-robin over the 8 XCDs, so every slice's gathers stay in ONE XCD's L2 --
+// 1.6 TB/s of algorithmic bytes).  Here the columns are cut into S slices of
+// x (S = 8, or 4 when a quarter of x fits 2 MB, see zcsr_build_split);
+// workgroup b works on slice b % S -- the hardware deals workgroups
+// round-robin over the 8 XCDs, so every slice's gathers stay in the L2 of one
+// XCD (S = 8) or of the two XCDs s and s + 4 (S = 4) --
 // with 8 lanes a row on the slice's own CSR (slice-relative 16-bit columns,
 // non-temporal matrix loads), and writes a partial y per slice; a second
 // kernel sums the 8 partials in a fixed order.  tools/zspmv_split.hip: 0.41 ms
@@ -24,30 +26,33 @@ namespace ahip::zdev {
 
 namespace {
 using namespace zc;
-constexpr int kSlices = zc::kZSlices;
+constexpr int kMaxSlices = zc::kZMaxSlices;
 constexpr int kLanes = 8;   // lanes per row (tools/zspmv_split.hip: 8 of 4/8/16)
 
+template <int S>
 __global__ void k_zsplit_count(int64_t n, int64_t sw, const int64_t* __restrict__ rp,
                                const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
-        int32_t c[kSlices] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int32_t c[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) c[s] = 0;
         for (int64_t k = rp[r]; k < rp[r + 1]; ++k) c[col[k] / sw]++;
 #pragma unroll
-        for (int s = 0; s < kSlices; ++s) cnt[(int64_t)s * (n + 1) + r] = c[s];
+        for (int s = 0; s < S; ++s) cnt[(int64_t)s * (n + 1) + r] = c[s];
     }
 }
 
-template <class CT>
+template <int S, class CT>
 __global__ void k_zsplit_fill(int64_t n, int64_t sw, const int64_t* __restrict__ rp,
                               const int32_t* __restrict__ col, const double2* __restrict__ val,
                               const int32_t* __restrict__ srp, const int64_t* __restrict__ base,
                               CT* __restrict__ scol, double2* __restrict__ sval) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
-        int64_t pos[kSlices];
+        int64_t pos[S];
 #pragma unroll
-        for (int s = 0; s < kSlices; ++s) pos[s] = base[s] + srp[(int64_t)s * (n + 1) + r];
+        for (int s = 0; s < S; ++s) pos[s] = base[s] + srp[(int64_t)s * (n + 1) + r];
         for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {  // row order kept inside each slice
             const int s = (int)(col[k] / sw);
             scol[pos[s]] = (CT)(col[k] - s * sw);
@@ -57,7 +62,7 @@ __global__ void k_zsplit_fill(int64_t n, int64_t sw, const int64_t* __restrict__
     }
 }
 
-template <class CT>
+template <int S, class CT>
 __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
                                                      const int32_t* __restrict__ srp,
                                                      const int64_t* __restrict__ base,
@@ -68,8 +73,8 @@ __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
                                                      const int* __restrict__ gate) {
     if (gate && *gate) return;  // a finished Krylov solve (zsolve.hip) skips its queued products
     typedef double dv2 __attribute__((ext_vector_type(2)));
-    const int s = (int)(blockIdx.x % kSlices);  // the XCD this workgroup runs on
-    const int64_t q = blockIdx.x / kSlices, nq = gridDim.x / kSlices;
+    const int s = (int)(blockIdx.x % S);  // the XCD (S = 4: one of two) this workgroup runs on
+    const int64_t q = blockIdx.x / S, nq = gridDim.x / S;
     const int lane = threadIdx.x & (kLanes - 1);
     constexpr int64_t kRows = 256 / kLanes;
     const int32_t* rp = srp + (int64_t)s * (n + 1);
@@ -94,11 +99,12 @@ __global__ __launch_bounds__(256) void k_zsplit_spmv(int64_t n, int64_t sw,
     }
 }
 
+template <int S>
 __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, double2* __restrict__ y,
                                  const int* __restrict__ gate) {
     if (gate && *gate) return;
     for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256)
-        y[r] = zc::slice_sum(yp, n, r);
+        y[r] = zc::slice_sum<S>(yp, n, r);
 }
 
 // ---- column-sorted tiles --------------------------------------------------
@@ -114,6 +120,7 @@ __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, doub
 constexpr int kTileRows = 4096;  // 64 KB of LDS row sums: two blocks a CU
 constexpr int kTileU = 4;        // entries a lane keeps in flight
 
+template <int S>
 __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int32_t* __restrict__ srp,
                                                const int64_t* __restrict__ base,
                                                const uint32_t* __restrict__ idx,
@@ -123,8 +130,8 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int3
     if (gate && *gate) return;
     typedef double dv2 __attribute__((ext_vector_type(2)));
     __shared__ double ylds[2 * kTileRows];
-    const int s = (int)(blockIdx.x % kSlices);  // the XCD this block runs on
-    const int64_t r0 = (int64_t)(blockIdx.x / kSlices) * kTileRows;
+    const int s = (int)(blockIdx.x % S);  // the XCD (S = 4: one of two) this block runs on
+    const int64_t r0 = (int64_t)(blockIdx.x / S) * kTileRows;
     const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
     for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
     __syncthreads();
@@ -166,12 +173,12 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int3
 // sort keys (slice column), the row of every entry, and the segment bounds of
 // the (slice, row block) segments in the slice-major entry order
 template <class CT>
-__global__ void k_ztile_keys(int64_t n, const int32_t* __restrict__ srp, const int64_t* __restrict__ base,
+__global__ void k_ztile_keys(int64_t n, int ns, const int32_t* __restrict__ srp, const int64_t* __restrict__ base,
                              const CT* __restrict__ scol, uint32_t* __restrict__ key,
                              uint32_t* __restrict__ erow, uint32_t* __restrict__ perm) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
-        for (int s = 0; s < kSlices; ++s) {
+        for (int s = 0; s < ns; ++s) {
             const int32_t* rp = srp + (int64_t)s * (n + 1);
             for (int64_t k = base[s] + rp[r]; k < base[s] + rp[r + 1]; ++k) {
                 key[k] = (uint32_t)scol[k];
@@ -181,13 +188,13 @@ __global__ void k_ztile_keys(int64_t n, const int32_t* __restrict__ srp, const i
         }
     }
 }
-__global__ void k_ztile_segs(int64_t n, int64_t nrb, const int32_t* __restrict__ srp,
+__global__ void k_ztile_segs(int64_t n, int nsl, int64_t nrb, const int32_t* __restrict__ srp,
                              const int64_t* __restrict__ base, int64_t* __restrict__ seg) {
-    const int64_t ns = kSlices * nrb;
+    const int64_t ns = nsl * nrb;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= ns;
          q += (int64_t)gridDim.x * blockDim.x) {
         if (q == ns) {
-            seg[q] = base[kSlices];
+            seg[q] = base[nsl];
             continue;
         }
         const int s = (int)(q / nrb);
@@ -244,7 +251,7 @@ static int ztile_build(ZCsr& A) {
     }();
     const int64_t n = A.n, nnz = A.nnz;
     if (off || A.s_w >= (int64_t(1) << 20) || nnz <= 0 || nnz >= (int64_t(1) << 32)) return 1;
-    const int64_t nrb = (n + kTileRows - 1) / kTileRows, nseg = kSlices * nrb;
+    const int64_t nrb = (n + kTileRows - 1) / kTileRows, nseg = A.s_n * nrb;
     uint32_t *key = nullptr, *key2 = nullptr, *erow = nullptr, *perm = nullptr, *perm2 = nullptr;
     int64_t* seg = nullptr;
     void* tmp = nullptr;
@@ -261,12 +268,12 @@ static int ztile_build(ZCsr& A) {
         rc = -2;
     } else {
         if (A.s_col16)
-            hipLaunchKernelGGL(k_ztile_keys<uint16_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_rp,
+            hipLaunchKernelGGL(k_ztile_keys<uint16_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_n, A.s_rp,
                                A.s_base, (const uint16_t*)A.s_col, key, erow, perm);
         else
-            hipLaunchKernelGGL(k_ztile_keys<int32_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_rp,
+            hipLaunchKernelGGL(k_ztile_keys<int32_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_n, A.s_rp,
                                A.s_base, (const int32_t*)A.s_col, key, erow, perm);
-        hipLaunchKernelGGL(k_ztile_segs, dim3(grid1(nseg + 1)), dim3(256), 0, nullptr, n, nrb, A.s_rp,
+        hipLaunchKernelGGL(k_ztile_segs, dim3(grid1(nseg + 1)), dim3(256), 0, nullptr, n, A.s_n, nrb, A.s_rp,
                            A.s_base, seg);
         int bits = 1;
         while ((int64_t(1) << bits) < A.s_w) ++bits;
@@ -306,7 +313,13 @@ int zcsr_build_split(ZCsr& A) {
     }();
     const int64_t n = A.n;
     if (off || n < (int64_t(1) << 18) || A.nnz < 32 * n) return 1;
-    const int64_t sw = (n + kSlices - 1) / kSlices;
+    // 4 slices while a quarter of x fits 2 MB (half an XCD's L2; slice s on XCDs
+    // s and s + 4), else 8: tools/ztile_probe.hip at config 5 (n = 5e5), 0.215 ms
+    // a product against 0.237 with 8 slices -- half the partial-sum traffic, the
+    // same column density per tile
+    const int ns = (n + 3) / 4 * 16 <= (int64_t(2) << 20) ? 4 : 8;
+    const int64_t sw = (n + ns - 1) / ns;
+    A.s_n = ns;
     A.s_w = sw;
     A.s_col16 = sw <= 65536;
     const size_t cb = A.s_col16 ? 2 : 4;
@@ -319,16 +332,19 @@ int zcsr_build_split(ZCsr& A) {
         zcsr_free_split(A);
         return rc;
     };
-    if (hipMalloc(&cnt, sizeof(int32_t) * kSlices * (n + 1)) ||
-        hipMalloc(&A.s_rp, sizeof(int32_t) * kSlices * (n + 1)) ||
-        hipMalloc(&A.s_base, sizeof(int64_t) * (kSlices + 1)))
+    if (hipMalloc(&cnt, sizeof(int32_t) * ns * (n + 1)) ||
+        hipMalloc(&A.s_rp, sizeof(int32_t) * ns * (n + 1)) ||
+        hipMalloc(&A.s_base, sizeof(int64_t) * (ns + 1)))
         return fail(-2);
-    hipLaunchKernelGGL(k_zsplit_count, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
+    if (ns == 4)
+        hipLaunchKernelGGL(k_zsplit_count<4>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
+    else
+        hipLaunchKernelGGL(k_zsplit_count<8>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, cnt, A.s_rp, (int)(n + 1));
     if (hipMalloc(&tmp, tmpb ? tmpb : 1)) return fail(-2);
-    int64_t hb[kSlices + 1];
+    int64_t hb[kMaxSlices + 1];
     hb[0] = 0;
-    for (int s = 0; s < kSlices; ++s) {
+    for (int s = 0; s < ns; ++s) {
         int32_t* c = cnt + (size_t)s * (n + 1);
         (void)hipMemsetAsync(c + n, 0, sizeof(int32_t), nullptr);
         // per-slice row offsets; int32: a slice holds < 2^31 entries (checked below)
@@ -339,51 +355,64 @@ int zcsr_build_split(ZCsr& A) {
         if (tot < 0) return fail(1);  // int32 overflow: keep the wave-per-row kernel
         hb[s + 1] = hb[s] + tot;
     }
-    if (hb[kSlices] != A.nnz) return fail(-1);
-    (void)hipMemcpy(A.s_base, hb, sizeof(hb), hipMemcpyHostToDevice);
+    if (hb[ns] != A.nnz) return fail(-1);
+    if (hipMemcpy(A.s_base, hb, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice)) return fail(-1);
     (void)hipFree(cnt);
     cnt = nullptr;
     (void)hipFree(tmp);
     tmp = nullptr;
     if (hipMalloc(&A.s_col, cb * (A.nnz ? A.nnz : 1)) || hipMalloc(&A.s_val, 16 * (A.nnz ? A.nnz : 1)) ||
-        hipMalloc(&A.s_y, 16 * (size_t)kSlices * n))
+        hipMalloc(&A.s_y, 16 * (size_t)ns * n))
         return fail(-2);
     const auto* v2 = reinterpret_cast<const double2*>(A.val);
+    auto fill = [&](auto kern, auto* sc) {
+        hipLaunchKernelGGL(kern, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, v2, A.s_rp,
+                           A.s_base, sc, (double2*)A.s_val);
+    };
     if (A.s_col16)
-        hipLaunchKernelGGL(k_zsplit_fill<uint16_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr,
-                           A.col, v2, A.s_rp, A.s_base, (uint16_t*)A.s_col, (double2*)A.s_val);
+        ns == 4 ? fill(k_zsplit_fill<4, uint16_t>, (uint16_t*)A.s_col)
+                : fill(k_zsplit_fill<8, uint16_t>, (uint16_t*)A.s_col);
     else
-        hipLaunchKernelGGL(k_zsplit_fill<int32_t>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr,
-                           A.col, v2, A.s_rp, A.s_base, (int32_t*)A.s_col, (double2*)A.s_val);
+        ns == 4 ? fill(k_zsplit_fill<4, int32_t>, (int32_t*)A.s_col)
+                : fill(k_zsplit_fill<8, int32_t>, (int32_t*)A.s_col);
     if (hipDeviceSynchronize() != hipSuccess) return fail(-1);
     A.split = true;
     (void)ztile_build(A);  // optional: the CSR split stays if the tiles cannot be built
     return 0;
 }
 
+namespace {
+template <int S>
+void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp, const int* gate) {
+    if (A.tile) {
+        hipLaunchKernelGGL(k_ztile<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
+                           A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
+        return;
+    }
+    const int g = 1024;  // 128 workgroups a slice at S = 8 (tools/zspmv_split.hip)
+    if (A.s_col16)
+        hipLaunchKernelGGL((k_zsplit_spmv<S, uint16_t>), dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
+                           A.s_base, (const uint16_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
+    else
+        hipLaunchKernelGGL((k_zsplit_spmv<S, int32_t>), dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
+                           A.s_base, (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
+}
+}  // namespace
+
 const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x, const int* gate) {
     if (!A.split) return nullptr;
     const auto* x2 = reinterpret_cast<const double2*>(x);
     auto* yp = reinterpret_cast<double2*>(A.s_y);
-    if (A.tile) {
-        hipLaunchKernelGGL(k_ztile, dim3((unsigned)(kSlices * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
-                           A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
-        return A.s_y;
-    }
-    const int g = 1024;  // 128 workgroups a slice (tools/zspmv_split.hip)
-    if (A.s_col16)
-        hipLaunchKernelGGL(k_zsplit_spmv<uint16_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
-                           (const uint16_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
-    else
-        hipLaunchKernelGGL(k_zsplit_spmv<int32_t>, dim3(g), dim3(256), 0, s, A.n, A.s_w, A.s_rp, A.s_base,
-                           (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
+    if (A.s_n == 4) split_partials<4>(s, A, x2, yp, gate);
+    else split_partials<8>(s, A, x2, yp, gate);
     return A.s_y;
 }
 
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
     const auto* yp = reinterpret_cast<const double2*>(zcsr_split_partials(s, A, x, gate));
-    hipLaunchKernelGGL(k_zsplit_combine, dim3(2048), dim3(256), 0, s, A.n, yp, reinterpret_cast<double2*>(y),
-                       gate);
+    auto* y2 = reinterpret_cast<double2*>(y);
+    if (A.s_n == 4) hipLaunchKernelGGL(k_zsplit_combine<4>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
+    else hipLaunchKernelGGL(k_zsplit_combine<8>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
 }
 
 }  // namespace ahip::zdev

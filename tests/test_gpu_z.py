@@ -122,3 +122,34 @@ def test_zcsr_spmv_xcd_split(pkg, n, per, seed):
     Z2 = pkg.ZCSR.from_arrays(rp, col, val)  # the arpack_hip_zcsr_create path
     # column-sorted tiles add into LDS row sums in schedule order: equal to rounding
     assert np.abs(Z2.matvec(x) - y).max() <= 1e-13 * np.abs(yref).max()
+
+
+_CSR_SPLIT = """
+import sys, numpy as np, scipy.sparse as sp
+sys.path.insert(0, %r)
+from bench import load_pkg
+pkg = load_pkg()
+for n, per, seed in [(300000, 64, 7), (524289, 40, 3)]:
+    Z = pkg.ZCSR.random(n, per, seed, 100.0)
+    rp, col, val = Z.download()
+    x = np.random.default_rng(seed).uniform(-1, 1, n) + 0.5j
+    y, yref = Z.matvec(x), sp.csr_matrix((val, col, rp), shape=(n, n)) @ x
+    err = np.abs(y - yref).max() / np.abs(yref).max()
+    assert err <= 1e-13, (n, err)
+print("ok")
+"""
+
+
+def test_zcsr_spmv_csr_split_form():
+    """The split's CSR form (AHIP_ZSPLIT=csr: no column-sorted tiles; the form the
+    operator keeps when the tiles cannot be built) at 4 column slices (n = 3e5,
+    32-bit slice columns) and 8 (n = 524,289, 16-bit), against SciPy's product.
+    A child process: the switch is read once per process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AHIP_ZSPLIT="csr")
+    r = subprocess.run([sys.executable, "-c", _CSR_SPLIT % root], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
