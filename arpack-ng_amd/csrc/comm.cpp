@@ -53,10 +53,10 @@ static void note(const Comm* c, bool ok) {
 
 int comm_failed(const Comm* c) {
     if (!c) return 0;
-    if (!c->failed && c->nccl) {
+    for (ncclComm_t cm : {c->nccl, c->nccl_p2p}) {  // both communicators' async errors
+        if (c->failed || !cm) continue;
         ncclResult_t a = ncclSuccess;
-        if (ncclCommGetAsyncError(c->nccl, &a) != ncclSuccess ||
-            (a != ncclSuccess && a != ncclInProgress))
+        if (ncclCommGetAsyncError(cm, &a) != ncclSuccess || (a != ncclSuccess && a != ncclInProgress))
             const_cast<Comm*>(c)->failed = 1;
     }
     return c->failed;

@@ -34,6 +34,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 
 #include "../../include/arpack_hip.h"
@@ -50,9 +51,13 @@ struct Binding {
 std::mutex g_mu;
 Binding g_bind;
 bool g_bound = false;
-// one decomposition per (communicator, local rows); they stay alive for the
-// *eupd call that follows the *aupd loop (and for later solves)
-std::map<std::pair<MPI_Fint, int64_t>, arpack_hip_dist*> g_dists;
+// one decomposition per (communicator, local rows, first row, global rows);
+// they stay alive for the *eupd call that follows the *aupd loop (and for
+// later solves).  g_cur: the decomposition of the solve in progress on a
+// (communicator, local rows) pair, fixed at its ido = 0 call.
+using DistKey = std::tuple<MPI_Fint, int64_t, long long, long long>;
+std::map<DistKey, arpack_hip_dist*> g_dists;
+std::map<std::pair<MPI_Fint, int64_t>, arpack_hip_dist*> g_cur;
 
 void host_allreduce(double* buf, int count, void* ctx) {
     MPI_Allreduce(MPI_IN_PLACE, buf, count, MPI_DOUBLE, MPI_SUM, static_cast<Binding*>(ctx)->comm);
@@ -78,6 +83,7 @@ void host_halo(const double* slo, int64_t nsl, double* rlo, int64_t nrl, const d
 void release_binding() {
     for (auto& kv : g_dists) arpack_hip_dist_destroy(kv.second);
     g_dists.clear();
+    g_cur.clear();
     if (g_bound) {
         arpack_hip_comm_destroy();
         int fin = 0;
@@ -135,21 +141,42 @@ bool bind_comm(MPI_Fint fcomm) {
 }
 
 // The decomposition of this call: nloc local rows, row0 = rows of the lower
-// ranks, n_global = all rows (collective the first time a (comm, nloc) pair is seen).
-arpack_hip_dist* dist_for(MPI_Fint fcomm, int64_t nloc) {
+// ranks, n_global = all rows.  At a solve's first call (fresh: *aupd with ido =
+// 0) it is established collectively -- MPI_Exscan / MPI_Allreduce of the local
+// sizes, then an agreement that every rank has its decomposition, so a rank
+// whose setup fails never leaves the others waiting in the solve's collectives
+// (all of them return info = -9999) -- and it serves the later calls of the
+// same solve and the *eupd call after it (no collective per RCI call).
+arpack_hip_dist* dist_for(MPI_Fint fcomm, int64_t nloc, bool fresh) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!bind_comm(fcomm)) return nullptr;
-    const auto key = std::make_pair(fcomm, nloc);
-    auto it = g_dists.find(key);
-    if (it != g_dists.end()) return it->second;
+    const auto cur = std::make_pair(fcomm, nloc);
+    if (!fresh) {
+        auto it = g_cur.find(cur);
+        if (it != g_cur.end()) return it->second;
+    }
     long long mine = nloc, row0 = 0, nglob = 0;
     MPI_Exscan(&mine, &row0, 1, MPI_LONG_LONG, MPI_SUM, g_bind.comm);
     if (g_bind.rank == 0) row0 = 0;  // MPI_Exscan leaves rank 0's result undefined
     MPI_Allreduce(&mine, &nglob, 1, MPI_LONG_LONG, MPI_SUM, g_bind.comm);
+    const DistKey key{fcomm, nloc, row0, nglob};
     arpack_hip_dist* D = nullptr;
-    if (nloc <= 0 || arpack_hip_dist_rows(&D, nloc, row0, nglob) != 0) return nullptr;
-    arpack_hip_dist_set_seed_mode(D, 1);  // PARPACK's per-rank start vector
-    g_dists[key] = D;
+    auto it = g_dists.find(key);
+    if (it != g_dists.end()) {
+        D = it->second;
+    } else if (nloc > 0 && arpack_hip_dist_rows(&D, nloc, row0, nglob) == 0) {
+        arpack_hip_dist_set_seed_mode(D, 1);  // PARPACK's per-rank start vector
+        g_dists[key] = D;
+    } else {
+        D = nullptr;
+    }
+    int ok = D ? 1 : 0, all = 0;
+    MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_bind.comm);
+    if (!all) {
+        g_cur.erase(cur);
+        return nullptr;
+    }
+    g_cur[cur] = D;
     return D;
 }
 
@@ -211,7 +238,7 @@ extern "C" {
 void pdsaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pdsaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
@@ -221,7 +248,7 @@ void pdseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int nev, double tol, double* resid, a_int ncv, double* v, a_int ldv,
                a_int* iparam, a_int* ipntr, double* workd, double* workl, a_int lworkl,
                a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_pdseupd_c(D, rvec, howmny, select, d, z, ldz, sigma, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, info);
@@ -229,7 +256,7 @@ void pdseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pssaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pssaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
@@ -238,7 +265,7 @@ void psseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                float* z, a_int ldz, float sigma, char const* bmat, a_int n, char const* which,
                a_int nev, float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_psseupd_c(D, rvec, howmny, select, d, z, ldz, sigma, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, info);
@@ -246,7 +273,7 @@ void psseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pdnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pdnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
@@ -256,7 +283,7 @@ void pdneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                char const* bmat, a_int n, char const* which, a_int nev, double tol, double* resid,
                a_int ncv, double* v, a_int ldv, a_int* iparam, a_int* ipntr, double* workd,
                double* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_pdneupd_c(D, rvec, howmny, select, dr, di, z, ldz, sigmar, sigmai, workev, bmat, n,
                          which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
@@ -265,7 +292,7 @@ void pdneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void psnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_psnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
@@ -275,7 +302,7 @@ void psneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                char const* bmat, a_int n, char const* which, a_int nev, float tol, float* resid,
                a_int ncv, float* v, a_int ldv, a_int* iparam, a_int* ipntr, float* workd,
                float* workl, a_int lworkl, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_psneupd_c(D, rvec, howmny, select, dr, di, z, ldz, sigmar, sigmai, workev, bmat, n,
                          which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
@@ -284,7 +311,7 @@ void psneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pznaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, zc* resid, a_int ncv, zc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                zc* workd, zc* workl, a_int lworkl, double* rwork, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pznaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
@@ -293,7 +320,7 @@ void pzneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int ldz, zc sigma, zc* workev, char const* bmat, a_int n, char const* which,
                a_int nev, double tol, zc* resid, a_int ncv, zc* v, a_int ldv, a_int* iparam,
                a_int* ipntr, zc* workd, zc* workl, a_int lworkl, double* rwork, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_pzneupd_c(D, rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
@@ -301,7 +328,7 @@ void pzneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pcnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, cc* resid, a_int ncv, cc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                cc* workd, cc* workl, a_int lworkl, float* rwork, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pcnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
@@ -310,7 +337,7 @@ void pcneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
                a_int ldz, cc sigma, cc* workev, char const* bmat, a_int n, char const* which,
                a_int nev, float tol, cc* resid, a_int ncv, cc* v, a_int ldv, a_int* iparam,
                a_int* ipntr, cc* workd, cc* workl, a_int lworkl, float* rwork, a_int* info) {
-    arpack_hip_dist* D = dist_for(comm, n);
+    arpack_hip_dist* D = dist_for(comm, n, false);
     if (!D) return fail(nullptr, info);
     arpack_hip_pcneupd_c(D, rvec, howmny, select, d, z, ldz, sigma, workev, bmat, n, which, nev, tol,
                          resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl, rwork, info);
