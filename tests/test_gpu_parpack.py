@@ -66,3 +66,16 @@ def test_parpack_reference_program(name, np_):
 def test_parpack_icb_program(name, np_):
     r = _mpirun(os.path.join(BIN, name + "_hip"), np_)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_parpack_resize(np_):
+    """Two solves per family (pznaupd/pzneupd, pdsaupd/pdseupd) in one process
+    with different decompositions -- rank 0 keeps its 500 rows while the global
+    size grows from 500 P to 500 + 700 (P - 1) -- against the exact top four
+    eigenvalues of a diagonal operator (tests/c/parpack_resize.c; parity
+    unpinned: no reference output, analytic answers).  libparpack_hip.so must
+    take the second decomposition at the second solve's ido = 0."""
+    r = _mpirun(os.path.join(BIN, "parpack_resize_hip"), np_)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-3000:],
+                                                                  r.stderr[-3000:])
