@@ -27,8 +27,8 @@
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
 
-template <int S, int U>
-__global__ __launch_bounds__(256) void k_tile(int64_t n, int64_t sw, int rb_rows,
+template <int S, int U, int T = 256>
+__global__ __launch_bounds__(T) void k_tile(int64_t n, int64_t sw, int rb_rows,
                                               const int64_t* __restrict__ boff,
                                               const uint32_t* __restrict__ idx,
                                               const double2* __restrict__ val,
@@ -38,18 +38,18 @@ __global__ __launch_bounds__(256) void k_tile(int64_t n, int64_t sw, int rb_rows
     const int s = (int)(blockIdx.x % S);
     const int64_t r0 = (int64_t)(blockIdx.x / S) * rb_rows;
     const int rows = (int)((n - r0) < rb_rows ? (n - r0) : rb_rows);
-    for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
+    for (int i = threadIdx.x; i < 2 * rows; i += T) ylds[i] = 0.0;
     __syncthreads();
     const double2* xs = x + (int64_t)s * sw;
     const int64_t e0 = boff[blockIdx.x], e1 = boff[blockIdx.x + 1];
     int64_t e = e0 + threadIdx.x;
-    for (; e + (U - 1) * 256 < e1; e += U * 256) {
+    for (; e + (U - 1) * T < e1; e += U * T) {
         uint32_t id[U];
         dv2 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            id[u] = __builtin_nontemporal_load(&idx[e + u * 256]);
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+            id[u] = __builtin_nontemporal_load(&idx[e + u * T]);
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * T);
         }
         double2 xv[U];
 #pragma unroll
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_tile(int64_t n, int64_t sw, int rb_rows
             atomicAdd(&ylds[2 * r + 1], v[u].x * xv[u].y + v[u].y * xv[u].x);
         }
     }
-    for (; e < e1; e += 256) {
+    for (; e < e1; e += T) {
         const uint32_t id = idx[e];
         const dv2 v = reinterpret_cast<const dv2*>(val)[e];
         const double2 xv = xs[id & 0xfffffu];
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_tile(int64_t n, int64_t sw, int rb_rows
     }
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
-    for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
+    for (int i = threadIdx.x; i < rows; i += T) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
 }
 
 template <int S>
@@ -200,6 +200,17 @@ int main() {
         one(k_tile<S, 2>);
         one(k_tile<S, 4>);
         one(k_tile<S, 8>);
+        float t512[2];
+        {
+            auto one512 = [&](auto kern, int qq) {
+                t512[qq] = timeit([&] {
+                    kern<<<grid, 512, lds>>>(n, sw, RB, d_boff, d_tidx, d_tval, d_x, d_yp);
+                    k_combine<S><<<2048, 256>>>(n, d_yp, d_y);
+                });
+            };
+            one512(k_tile<S, 2, 512>, 0);
+            one512(k_tile<S, 4, 512>, 1);
+        }
         const float tc = timeit([&] { k_combine<S><<<2048, 256>>>(n, d_yp, d_y); });
         std::vector<double2> y(n);
         CK(hipMemcpy(y.data(), d_y, 16 * n, hipMemcpyDeviceToHost));
@@ -208,14 +219,15 @@ int main() {
             err = std::max(err, std::hypot(y[i].x - yref[i].x, y[i].y - yref[i].y));
             sc = std::max(sc, std::hypot(yref[i].x, yref[i].y));
         }
-        printf("S %d RB %5d (%5u groups, LDS %2zu KB): U2 %.3f  U4 %.3f  U8 %.3f ms a product "
-               "(combine %.3f)  rel err %.1e\n", S, RB, grid, lds / 1024, t[0], t[1], t[2], tc, err / sc);
+        printf("S %d RB %5d (%5u groups, LDS %2zu KB): U2 %.3f  U4 %.3f  U8 %.3f | T512 U2 %.3f U4 %.3f ms a "
+               "product (combine %.3f)  rel err %.1e\n", S, RB, grid, lds / 1024, t[0], t[1], t[2], t512[0],
+               t512[1], tc, err / sc);
         CK(hipFree(d_boff));
         CK(hipFree(d_tidx));
         CK(hipFree(d_tval));
         return 0;
     };
-    for (int RB : {1024, 2048, 4096}) {
+    for (int RB : {2048, 4096}) {
         if (probe(std::integral_constant<int, 8>{}, RB)) return 1;
         if (probe(std::integral_constant<int, 4>{}, RB)) return 1;
     }
