@@ -269,7 +269,8 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
                                          int cstride, double* __restrict__ rec, LzState* st,
                                          double* __restrict__ hcol, int hld,
                                          const double* __restrict__ part2, int m2,
-                                         int rstart_prev, double* s_rec) {
+                                         int rstart_prev, double* s_rec,
+                                         const double* s_h = nullptr) {
     // the m + m2 (<= 2 ncv + 4) sums are staged in dynamic LDS sized by the
     // launch, so any ncv the argument checks accept fits
     extern __shared__ double s_sum[];
@@ -419,12 +420,15 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
         // Arnoldi: t = H_j s with the full upper-Hessenberg records (column q of
         // H: hcol rows 0..q, subdiagonal H(q+1,q) = rec[2q+3]); this step's
         // column is h + s, read before the daxpy below adds s to it
+        // (s_h: H(0:jm, 0:jm) staged in LDS by k_finalize<true> -- the same
+        // values in the same order, without a global-memory latency per term)
         for (int i = t; i < jm; i += nt) {
             double ti = 0.0;
             for (int q = i > 0 ? i - 1 : 0; q < jm; ++q) {
+                const double hc = s_h ? s_h[q * jm + i] : hcol[(int64_t)q * hld + i];
                 double hiq;
-                if (q == jm - 1) hiq = hcol[(int64_t)q * hld + i] + s_sum[i];
-                else if (i <= q) hiq = hcol[(int64_t)q * hld + i];
+                if (q == jm - 1) hiq = hc + s_sum[i];
+                else if (i <= q) hiq = hc;
                 else hiq = s_rec[2 * q + 3];
                 ti = fma(hiq, s_sum[q], ti);
             }
@@ -445,6 +449,8 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
 // the global copy (last written by another XCD's finalize) cost a memory
 // latency each.
 constexpr int kFoldRecMax = 2 * 66;  // T records staged for the fold's t (j <= 64)
+constexpr int kFoldHMax = 64;        // HS: H(0:j, 0:j) staged for the Arnoldi fold's t = H s
+template <bool HS>
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ part, int nblk,
                                                    int from_sums, int m, int phase, int j,
                                                    int rstart, int gate, double* __restrict__ sums,
@@ -456,13 +462,23 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    int rstart_prev) {
     __shared__ LzState s_st;
     __shared__ double s_rec[kFoldRecMax];
+    // HS (Arnoldi kFinPostCgsFold, j <= kFoldHMax): H's first j columns and rows,
+    // read once in parallel (coalesced) for the t = H s loop; the 32 KB are
+    // static, so only this variant carries them (the generic finalize keeps the
+    // whole 64 KB for its dynamic sums)
+    __shared__ double s_h[HS ? kFoldHMax * kFoldHMax : 1];
     if (threadIdx.x == 0) s_st = *st;
     if (phase == kFinPostCgsFold && 2 * (j + 1) <= kFoldRecMax)
         for (int k = threadIdx.x; k < 2 * (j + 1); k += blockDim.x) s_rec[k] = rec[k];
+    if constexpr (HS) {
+        const int jm = m - 1;
+        for (int k = threadIdx.x; k < jm * jm; k += blockDim.x)
+            s_h[k] = hcol[(int64_t)(k / jm) * hld + k % jm];
+    }
     __syncthreads();
     if (gate_closed(&s_st, gate)) return;
     fin_body(part, nblk, from_sums, m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol,
-             hld, part2, m2, rstart_prev, s_rec);
+             hld, part2, m2, rstart_prev, s_rec, HS ? s_h : nullptr);
     __syncthreads();
     if (threadIdx.x == 0) *st = s_st;
 }
@@ -921,10 +937,11 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
     }();
     const double* part2 = ws.part + (size_t)ws.nblk * ws.stride;  // region 2 (chained steps)
     const size_t lds = sizeof(double) * (size_t)(m + m2);  // s_sum (m + m2 <= 2 kMaxNcv + 4)
+    const bool hs = ph == kFinPostCgsFold && ws.hld && m - 1 <= kFoldHMax;
     auto fin = [&](int fs) {
-        AHIP_LAUNCH(k_finalize, dim3(1), dim3(1024), lds, ws.stream, ws.part, ws.nblk, fs, m,
-                           (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride, ws.rec, ws.st,
-                           ws.hcol, ws.hld, part2, m2, rstart_prev);
+        AHIP_LAUNCH(hs ? k_finalize<true> : k_finalize<false>, dim3(1), dim3(1024), lds, ws.stream,
+                    ws.part, ws.nblk, fs, m, (int)ph, j, rstart, gate, ws.sums, ws.coef, ws.stride,
+                    ws.rec, ws.st, ws.hcol, ws.hld, part2, m2, rstart_prev);
     };
     if (!from_sums && fused) {  // one launch: the finalize block sums the partials itself
         fin(0);
