@@ -132,3 +132,27 @@ def test_solve_with_symmetric_storage(pkg, golden, name):
     d, z, res = pkg.eigsh(Ad, A.shape[0], int(g["nev"]), int(g["ncv"]), str(g["which"]),
                           float(g["tol"]), v0=g["v0"], mxiter=int(g["mxiter"]), device=True)
     _check(g, d, res, z, A)
+
+
+def test_symmetric_storage_run_to_run(pkg):
+    """The symmetric SpMV's LDS adds land in schedule order, so repeated solves
+    are not bitwise equal -- but on an NS-shaped operator (band 4096, spills
+    across superblocks) three repeats of the same solve take the same restart
+    cycles and OP*x, and their Ritz values agree to 1e-13 relative with each
+    other and with the (bitwise reproducible) full-storage solve.  The full-size
+    measurement: tools/ttc_repeat.py, profiles/r03w_ttc_repeat.json."""
+    n = 400_000
+    A = pkg.CSR.banded_sym(n, 1234, 4096, 25, 0, n)
+    v0 = np.random.default_rng(3).uniform(-1, 1, n)
+    res = {}
+    for storage in ("full", "sym", "sym", "sym"):
+        A.set_symmetric(storage == "sym")
+        s = pkg.SymRci(n, 10, 30, "LA", 1e-8, mxiter=300, device=True, v0=v0)
+        assert s.aupd_cycles(A, -1) == 99 and int(s.info[0]) == 0
+        d, _, nconv = s.eupd(rvec=False)
+        assert nconv == 10
+        res.setdefault(storage, []).append((int(s.iparam[2]), int(s.iparam[8]), np.sort(d)))
+    (c0, o0, d0), = res["full"]
+    for c, o, d in res["sym"]:
+        assert (c, o) == (c0, o0)
+        assert np.max(np.abs(d - d0) / np.abs(d0)) <= 1e-13
