@@ -778,6 +778,75 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
     return d, (z if rvec else None), res
 
 
+def _ns_vectors(dr, di, z, n, nconv):
+    """dneupd's real Z (SRC/dneupd.f:81-91: a complex pair's eigenvector is
+    z(:,j) +/- i z(:,j+1), the pair stored at dr(j) +/- i di(j)) -> complex columns."""
+    Z = np.asarray(z).reshape(-1, n)[:nconv + 1].T
+    out = np.zeros((n, nconv), np.complex128)
+    j = 0
+    while j < nconv:
+        if di[j] != 0.0 and j + 1 < Z.shape[1]:
+            v = Z[:, j] + 1j * Z[:, j + 1]
+            out[:, j] = v
+            if j + 1 < nconv:
+                out[:, j + 1] = np.conj(v)
+            j += 2
+        else:
+            out[:, j] = Z[:, j]
+            j += 1
+    return out
+
+
+def eigs(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,
+         sigma=None, rtol=1e-12, maxit=200):
+    """Nonsymmetric / complex counterpart of eigsh (the calling pattern of
+    EXAMPLES/NONSYM/dndrv1.f and EXAMPLES/COMPLEX/zndrv1.f / zndrv2.f):
+
+      * op a CSR: dnaupd with OP = A on the GPU (arpack_hip_dnaupd_csr_cycles);
+      * op a ZCSR: znaupd with OP = A on the GPU, or with sigma given, shift-invert
+        mode 3 with OP = (A - sigma I)^{-1} by the device BiCGStab (ZShift, to
+        rtol within maxit iterations) -- eigenvalues of A returned (zneupd's
+        transform);
+      * op a callable y = op(x) on host vectors: the dnaupd RCI loop (real x).
+
+    Returns (d, Z, info-dict) with complex eigenvalues d (nconv of them) and,
+    if rvec, complex eigenvectors as the columns of Z."""
+    ncv = ncv or min(n, max(2 * nev + 1, 20))
+    if isinstance(op, ZCSR):
+        mode = 1 if sigma is None else 3
+        s = ZRci(n, nev, ncv, which, tol, mode=mode, mxiter=mxiter, v0=v0)
+        if sigma is None:
+            s.aupd_zcsr(op)
+        else:
+            S = ZShift(op, sigma, rtol=rtol, maxit=maxit)
+            s.aupd_zshift(S)
+        if s.info[0] < 0:
+            raise ArpackError("znaupd", int(s.info[0]))
+        res = dict(info=int(s.info[0]), iters=int(s.iparam[2]), nconv=int(s.iparam[4]),
+                   nopx=int(s.iparam[8]))
+        d, z, nconv = s.eupd(rvec=rvec, sigma=0j if sigma is None else complex(sigma))
+        return d, (z if rvec else None), res
+    s = NsRci(n, nev, ncv, which, tol, mxiter=mxiter, v0=v0)
+    if isinstance(op, CSR):
+        s.aupd_csr(op)
+    else:
+        while True:
+            ido = s.aupd()
+            if ido in (-1, 1):
+                s.slice(1)[:] = op(s.slice(0))
+            elif ido == 99:
+                break
+            else:
+                raise ArpackError("dnaupd", int(s.info[0]), {"ido": ido})
+    if s.info[0] < 0:
+        raise ArpackError("dnaupd", int(s.info[0]))
+    res = dict(info=int(s.info[0]), iters=int(s.iparam[2]), nconv=int(s.iparam[4]),
+               nopx=int(s.iparam[8]))
+    dr, di, z, nconv = s.eupd(rvec=rvec)
+    d = dr + 1j * di
+    return d, (_ns_vectors(dr, di, z, n, nconv) if rvec else None), res
+
+
 # ----------------------------------------------------------- multi-GPU (RCCL)
 def _declare_dist(L):
     L.arpack_hip_comm_unique_id.argtypes = [C.c_char_p]
