@@ -107,6 +107,9 @@ def _declare(L):
                            _PD, _PD, _I, _PI]
     L.dnaupd_.argtypes = L.dsaupd_.argtypes
     L.arpack_hip_dnaupd_csr_cycles.argtypes = L.arpack_hip_dsaupd_csr_cycles.argtypes
+    L.arpack_hip_dsaupd_shift.argtypes = [C.c_void_p, _PI, C.c_char_p, _I, C.c_char_p, _I,
+                                          C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI,
+                                          _PD, _PD, _I, _PI]
     L.arpack_hip_gen_convdiff2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
     L.znaupd_c.argtypes = [_PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I,
                            _PI, _PI, _PD, _PD, _I, _PD, _PI]
@@ -127,6 +130,11 @@ def _declare(L):
     L.arpack_hip_zshift_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, _PD]
     L.arpack_hip_zshift_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD] * 3
     L.arpack_hip_znaupd_zshift.argtypes = L.arpack_hip_znaupd_zcsr.argtypes
+    L.arpack_hip_dshift_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_double,
+                                           C.c_double, _I]
+    L.arpack_hip_dshift_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_dshift_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, _PD]
+    L.arpack_hip_dshift_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD] * 3
     L.arpack_hip_profile.argtypes = [_I]
     L.arpack_hip_profile_read.argtypes = [_PD, _PD, _PD, _I]
     L.arpack_hip_synchronize.restype = C.c_int
@@ -448,6 +456,18 @@ class SymRci:
         self.tol = tol.value
         return int(self.ido[0])
 
+    def aupd_shift(self, S: "DShift"):
+        """Whole loop on the GPU in mode 3 (construct with mode=3): OP =
+        (A - sigma I)^{-1} by the device CG S (arpack_hip_dsaupd_shift)."""
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_dsaupd_shift(S.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                      self.which.encode(), self.nev, C.byref(tol),
+                                      _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                      _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                      self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
     def slice(self, k):
         """workd slice ipntr[k] (1-based offset) of length n: a numpy view in
         host mode, the device address (int) in device mode."""
@@ -637,6 +657,48 @@ class ZShift:
                     ms=e.value, bytes_per_iter=f.value)
 
 
+class DShift:
+    """Shift-invert operator y = (A - sigma I)^{-1} x on the GPU for a symmetric CSR
+    operator (conjugate gradients; arpack_hip_dshift_*): dsaupd's mode-3 OP
+    (SRC/dsaupd.f:30-48), the caller-side solve EXAMPLES/SYM/dsdrv2.f does with
+    dgttrf/dgttrs.  A - sigma I must be positive definite."""
+
+    def __init__(self, A: "CSR", sigma=0.0, rtol=1e-12, maxit=1000):
+        self.A = A  # keeps the operator alive
+        self.sigma = float(sigma)
+        h = C.c_void_p()
+        rc = lib().arpack_hip_dshift_create(C.byref(h), A.h, self.sigma, float(rtol), int(maxit))
+        if rc != 0:
+            raise RuntimeError("arpack_hip_dshift_create failed (%d)" % rc)
+        self.h = h.value
+        self.n = A.n
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_dshift_destroy(self.h)
+        except Exception:
+            pass
+
+    def solve(self, x):
+        """y = (A - sigma I)^{-1} x for a host vector; returns (y, iters, relres)."""
+        xb, yb = DeviceBuffer(self.n), DeviceBuffer(self.n)
+        xb.write(np.ascontiguousarray(x, np.float64))
+        rr = C.c_double()
+        it = lib().arpack_hip_dshift_solve(self.h, _ptr(xb), _ptr(yb), C.byref(rr))
+        if it == -2:
+            raise RuntimeError("dshift solve: HIP error")
+        return yb.numpy().copy(), it, rr.value
+
+    def stats(self):
+        a, b, c = C.c_longlong(), C.c_longlong(), C.c_longlong()
+        d, e, f = C.c_double(), C.c_double(), C.c_double()
+        lib().arpack_hip_dshift_stats(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d),
+                                      C.byref(e), C.byref(f))
+        return dict(solves=a.value, iters=b.value, failures=c.value, max_relres=d.value,
+                    ms=e.value, bytes_per_iter=f.value)
+
+
 class ZRci:
     """znaupd/zneupd state (SRC/znaupd.f, SRC/zneupd.f): complex128 arrays,
     ipntr(14), lworkl = 3*ncv^2 + 5*ncv, rwork(ncv).  Host arrays; the caller
@@ -744,14 +806,24 @@ class _CF(C.Structure):
 
 
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,
-          device=False):
+          device=False, sigma=None, rtol=1e-12, maxit=1000):
     """Drive the RCI loop with a user OP (callable y = op(x) on workd slices), like
     TESTS/icb_arpack_c.c:60-65.  In device mode `op(x_addr, y_addr)` receives device
     addresses.  With `op` a CSR, the loop runs entirely on the GPU
-    (arpack_hip_dsaupd_csr).  Returns (d, Z, info-dict)."""
+    (arpack_hip_dsaupd_csr); with a CSR and `sigma`, in shift-invert mode 3 with
+    OP = (A - sigma I)^{-1} by the device CG (DShift; A - sigma I positive
+    definite), the eigenvalues of A nearest sigma returned (dseupd's transform).
+    Returns (d, Z, info-dict)."""
     ncv = ncv or min(n, max(2 * nev + 1, 20))
-    s = SymRci(n, nev, ncv, which, tol, mxiter=mxiter, v0=v0, device=device)
-    if isinstance(op, CSR):
+    shift = sigma is not None and isinstance(op, CSR)
+    s = SymRci(n, nev, ncv, which, tol, mode=3 if shift else 1, mxiter=mxiter, v0=v0,
+               device=device)
+    if shift:
+        S = DShift(op, sigma, rtol=rtol, maxit=maxit)
+        s.aupd_shift(S)
+        if s.tol <= 0.0:
+            s.tol = float(np.finfo(np.float64).eps / 2)
+    elif isinstance(op, CSR):
         s.aupd_csr(op)
     else:
         while True:
@@ -769,7 +841,7 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
         raise ArpackError("dsaupd", int(s.info[0]))
     res = dict(info=int(s.info[0]), iters=int(s.iparam[2]), nconv=int(s.iparam[4]),
                nopx=int(s.iparam[8]), nrorth=int(s.iparam[10]), ritz=s.ritz)
-    d, z, nconv = s.eupd(rvec=rvec)
+    d, z, nconv = s.eupd(rvec=rvec, sigma=float(sigma) if shift else 0.0)
     if rvec:
         if device:
             z = z.numpy().reshape(s.nev, n)[:nconv].T

@@ -135,9 +135,10 @@ template <class R>
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                      R* resid, int ncv, R* v, int ldv, int* iparam, int* ipntr, R* workd,
                      R* workl, int lworkl, int* info, const dev::Csr* csr, int max_cycles = -1,
-                     const DistOp* dist = nullptr, bool ns = false) {
+                     const DistOp* dist = nullptr, bool ns = false, dev::DShift* shift = nullptr) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
     if (dist) csr = dist->A;
+    if (shift) csr = shift->A;  // mode 3 free run: OP = (A - sigma I)^{-1} on the device
     if (kShadow && csr) {  // the float family: reverse communication (no device-CSR OP)
         *info = -9999;
         *ido = 99;
@@ -157,7 +158,10 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const int ishift = iparam[0], mxiter = iparam[2], mode = iparam[6];
         int ierr = ns ? ns_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter)
                       : sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
-        if (csr && (mode != 1 || bmat[0] != 'I' || csr->n != n)) ierr = (ierr ? ierr : -11);
+        // a device OP serves mode 1 (OP = A), or mode 3 through the device solve
+        // (symmetric only: CG); bmat = 'I'
+        if (csr && ((shift ? mode != 3 || ns || dist : mode != 1) || bmat[0] != 'I' || csr->n != n))
+            ierr = (ierr ? ierr : -11);
         if (dist && dist->nloc != n) ierr = (ierr ? ierr : -1);
         if (ierr != 0) {
             *info = ierr;
@@ -223,6 +227,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         if (csr) {
             S->free_run = true;
             S->csr = csr;
+            S->shift = shift;
         }
         if (dist) {
             S->dist = dist;
@@ -300,6 +305,20 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
                     (void)hipStreamSynchronize(so);
                 }
                 continue;
+            }
+            if constexpr (!kShadow) {
+                if (S->shift) {  // mode 3 (bmat = 'I': B x = x for ido = 1 too)
+                    if (dev::dshift_apply(*S->shift, S->a.stream, S->op_x, S->op_y, nullptr) < 0) {
+                        // the solve broke down or missed its tolerance: OP is not
+                        // what the caller asked for, so the Lanczos run stops
+                        S->a.sync();
+                        *info = -9999;
+                        *ido = 99;
+                        g_sym.erase(v);
+                        return;
+                    }
+                    continue;
+                }
             }
             if (S->dist) dev::prof_begin(dev::kProfSpmv, S->a.stream);
             else dev::prof_arm(dev::kProfSpmv, S->a.stream);
@@ -441,6 +460,61 @@ void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* 
                                   int* ipntr, double* workd, double* workl, int lworkl, int* info) {
     sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
              info, ahip_csr_view(A), max_cycles);
+}
+
+// ---- shift-invert on the device (dsaupd mode 3, dshift.hip) ----------------
+struct arpack_hip_dshift {
+    ahip::dev::DShift S;
+};
+
+int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, double sigma,
+                             double rtol, int maxit) {
+    if (!out || !A || !(rtol > 0.0) || maxit < 1) return -1;
+    auto* D = new arpack_hip_dshift;
+    if (ahip::dev::dshift_create(D->S, ahip_csr_view(A), sigma, rtol, maxit) != 0) {
+        delete D;
+        return -2;
+    }
+    *out = D;
+    return 0;
+}
+
+void arpack_hip_dshift_destroy(arpack_hip_dshift* D) {
+    if (!D) return;
+    ahip::dev::dshift_destroy(D->S);
+    delete D;
+}
+
+int arpack_hip_dshift_solve(arpack_hip_dshift* D, const double* x, double* y, double* relres) {
+    if (!D || !x || !y || x == y) return -2;
+    return ahip::dev::dshift_apply(D->S, nullptr, x, y, relres);
+}
+
+int arpack_hip_dshift_stats(const arpack_hip_dshift* D, long long* solves, long long* iters,
+                            long long* failures, double* max_relres, double* ms,
+                            double* bytes_per_iter) {
+    if (!D) return -1;
+    const auto& S = D->S;
+    if (solves) *solves = S.n_solves;
+    if (iters) *iters = S.n_iters;
+    if (failures) *failures = S.n_fail;
+    if (max_relres) *max_relres = S.max_relres;
+    if (ms) *ms = S.ms_total;
+    if (bytes_per_iter) *bytes_per_iter = ahip::dev::dshift_iter_bytes(S);
+    return 0;
+}
+
+void arpack_hip_dsaupd_shift(arpack_hip_dshift* D, int* ido, char const* bmat, int n,
+                             char const* which, int nev, double* tol, double* resid, int ncv,
+                             double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                             double* workl, int lworkl, int* info) {
+    if (!D) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr, -1, nullptr, false, &D->S);
 }
 
 // Row-block distributed solve (PARPACK's pdsaupd decomposition, n = LOCAL rows):

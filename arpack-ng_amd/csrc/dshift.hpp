@@ -1,0 +1,66 @@
+// Device shift-invert operator of the symmetric engine: y = (A - sigma I)^{-1} x
+// by conjugate gradients on the real CSR operator, every step on the GPU.
+//
+// The caller-side solve of dsaupd's mode 3 (SRC/dsaupd.f:30-48, OP = inv[A -
+// sigma M] M with M = I), which the reference's drivers do with a banded LU on
+// the host (EXAMPLES/SYM/dsdrv2.f: dgttrf / dgttrs).  For a symmetric operator
+// with sigma below its spectrum (the usual "smallest eigenvalues" use, e.g.
+// dsdrv2's sigma = 0 on a Laplacian) A - sigma I is positive definite and CG is
+// the Krylov solve of choice: one SpMV a step (the engine's own, full or
+// symmetric storage) and three fused vector kernels whose scalars never leave
+// the device -- each reducing kernel's blocks sum the previous kernel's
+// partials themselves in one fixed order (as the complex BiCGStab,
+// zsolve.hip).  An indefinite A - sigma I can break CG down: the solve then
+// reports failure (a non-positive curvature p'(A - sigma I)p, or no
+// convergence within maxit) and the Arnoldi run stops with info = -9999.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device.hpp"
+
+namespace ahip::dev {
+
+struct CgState {
+    int done;       // converged, broke down or hit maxit: later kernels return at once
+    int breakdown;  // p'(A - sigma I)p <= 0 (not positive definite) before convergence
+    int iters;      // iterations taken when done
+    int failed;     // done without reaching rtol
+    double rho[2];  // r'r of iteration k at [k & 1]
+    double alpha;
+    double bnorm2;  // ||b||^2
+    double rnorm2;  // ||r||^2 of the last iteration
+};
+
+struct DShift {
+    const Csr* A = nullptr;
+    double sigma = 0.0;
+    double rtol = 1e-12;
+    int maxit = 1000;
+    int64_t n = 0;
+    int nblk = 0;
+    double *r = nullptr, *p = nullptr, *w = nullptr;  // n each
+    double* part = nullptr;                           // 2 regions x 2 slots x nblk
+    CgState* st = nullptr;                            // device
+    CgState* st_host = nullptr;                       // pinned mirror
+    int chunk = 8;  // iterations enqueued before the first state read
+    long long n_solves = 0, n_iters = 0, n_fail = 0;
+    double max_relres = 0.0;
+    double ms_total = 0.0;  // device time of the solves (hipEvents)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+// 0, or a hipError_t on allocation failure (nothing leaks)
+int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit);
+void dshift_destroy(DShift& S);
+// y = (A - sigma I)^{-1} b on `stream` (device pointers; y must not alias b).
+// Returns the iterations (>= 0) and *relres = ||r|| / ||b|| of the recursively
+// updated residual; -1 if CG broke down or did not reach rtol within maxit (y
+// then holds the last iterate), -2 on a HIP error.
+int dshift_apply(DShift& S, hipStream_t stream, const double* b, double* y, double* relres);
+// algorithmic HBM bytes of one CG iteration (the CSR product in its storage and
+// the fused vector passes)
+double dshift_iter_bytes(const DShift& S);
+
+}  // namespace ahip::dev

@@ -12,6 +12,7 @@
 #include "dense.hpp"
 #include "device.hpp"
 #include "dist.hpp"
+#include "dshift.hpp"
 #include "rci.hpp"
 
 namespace ahip {
@@ -123,6 +124,9 @@ public:
     const DistOp* dist = nullptr;
     int64_t row0 = 0;
     const dev::Csr* csr = nullptr;
+    // mode 3 free run (arpack_hip_dsaupd_shift): OP = (A - sigma I)^{-1} by the
+    // device CG of dshift.hip on csr = shift->A
+    dev::DShift* shift = nullptr;
 
     // nonsymmetric Arnoldi (dnaupd): full upper-Hessenberg H (ld ncv)
     bool arnoldi = false;

@@ -316,6 +316,36 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, 
                               a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
                               a_dcomplex* workl, int lworkl, double* rwork, int* info);
 
+/* ---- shift-invert on the device, symmetric (dsaupd mode 3) ------------------
+ * y = (A - sigma I)^{-1} x by conjugate gradients on the device CSR operator A
+ * (full or symmetric storage), to ||r|| <= rtol ||x|| within maxit iterations:
+ * the caller-side solve of dsaupd's mode 3 (SRC/dsaupd.f:30-48), which the
+ * reference's EXAMPLES/SYM/dsdrv2.f does with dgttrf/dgttrs.  A - sigma I must be
+ * positive definite (sigma below the spectrum of A, the usual smallest-
+ * eigenvalue use); an indefinite shift makes CG break down, which is reported
+ * as a failed solve.  Returns as arpack_hip_zshift_*. */
+typedef struct arpack_hip_dshift arpack_hip_dshift;
+int arpack_hip_dshift_create(arpack_hip_dshift** S, const arpack_hip_csr* A, double sigma,
+                             double rtol, int maxit);
+void arpack_hip_dshift_destroy(arpack_hip_dshift* S);
+/* x, y device pointers (y != x); synchronous.  The iterations (>= 0; *relres =
+ * ||r||/||x||), -1 on breakdown / missed rtol, -2 on a HIP error. */
+int arpack_hip_dshift_solve(arpack_hip_dshift* S, const double* x, double* y, double* relres);
+/* Totals: solves, iterations, failures, worst final relative residual, device
+ * time (ms) and the algorithmic HBM bytes of one CG iteration (the CSR product
+ * in its storage + 11 n-vector passes). */
+int arpack_hip_dshift_stats(const arpack_hip_dshift* S, long long* solves, long long* iters,
+                            long long* failures, double* max_relres, double* ms,
+                            double* bytes_per_iter);
+/* dsaupd in mode 3 (iparam[6] = 3, bmat = 'I') with OP = (A - sigma I)^{-1}
+ * served on the GPU by S; returns with ido = 99 (dseupd_c with the same sigma
+ * then gives the eigenvalues of A).  A failed solve ends the run with
+ * info = -9999. */
+void arpack_hip_dsaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, int n,
+                             char const* which, int nev, double* tol, double* resid, int ncv,
+                             double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                             double* workl, int lworkl, int* info);
+
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
  * rows) and PARPACK/SRC/MPI/pdsaitr.f.  One process per GPU; the communicator

@@ -1,0 +1,110 @@
+"""GPU: the device shift-invert operator of the symmetric engine (csrc/dshift.hip:
+conjugate gradients on the real CSR operator) and dsaupd in mode 3 with it as OP
+(arpack_hip_dsaupd_shift).
+
+  * the solve against SciPy's direct solve (true residual ||(A - sigma I) y - x||
+    <= 1e-11 ||x||), full and symmetric storage; b = 0 gives y = 0;
+  * a negative-definite shift (sigma above the spectrum) breaks CG down: the
+    solve reports -1 and a mode-3 run served by it ends with info = -9999;
+  * mode 3 on the reference's m2 fixture (tests/golden/m2_sym_std_si: the
+    reference's dsaupd_ in mode 3 with a sparse-LU OP, EXAMPLES/SYM/dsdrv2.f's
+    setting: 1-D FEM stiffness n = 400, sigma = 0, nev 4, ncv 20, tol 1e-10):
+    the same restart cycles, OP*x count and converged set, eigenvalues within
+    1e-9 relative;
+  * eigsh(CSR, sigma=...) on a 2-D Laplacian against SciPy's eigsh(sigma=...).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spl
+
+from oracle import matrices as M
+
+sys.path.insert(0, os.path.dirname(__file__))
+import modes  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("storage", ["full", "sym"])
+@pytest.mark.parametrize("sigma", [0.0, -0.5])
+def test_dshift_solve(pkg, storage, sigma):
+    m = 120
+    A = pkg.CSR.laplace2d(m)
+    As = M.to_scipy(*M.laplace2d(m))
+    if storage == "sym":
+        A.set_symmetric(True)
+    n = m * m
+    S = pkg.DShift(A, sigma, rtol=1e-12, maxit=2000)
+    x = np.random.default_rng(3).uniform(-1, 1, n)
+    y, it, rr = S.solve(x)
+    assert it > 0 and rr <= 1e-12, (it, rr)
+    true = np.linalg.norm(As @ y - sigma * y - x) / np.linalg.norm(x)
+    assert true <= 1e-11, true
+    yref = spl.spsolve((As - sigma * sp.identity(n)).tocsc(), x)
+    assert np.linalg.norm(y - yref) <= 1e-9 * np.linalg.norm(yref)
+    y0, it0, _ = S.solve(np.zeros(n))
+    assert it0 == 0 and not y0.any()
+    st = S.stats()
+    assert st["solves"] == 2 and st["failures"] == 0 and st["iters"] == it
+
+
+def test_dshift_negative_definite_fails_loudly(pkg):
+    m = 40
+    A = pkg.CSR.laplace2d(m)  # spectrum in (0, 8)
+    S = pkg.DShift(A, 10.0, rtol=1e-12, maxit=500)
+    y, it, rr = S.solve(np.ones(m * m))
+    assert it == -1 and S.stats()["failures"] == 1
+    s = pkg.SymRci(m * m, 4, 20, "LM", 1e-10, mode=3, mxiter=50)
+    assert s.aupd_shift(S) == 99 and int(s.info[0]) == -9999
+
+
+def test_dsaupd_mode3_device_solve_m2(pkg, golden):
+    g = golden("m2_sym_std_si")
+    n, sigma = int(g["n"]), float(g["sigma"])
+    c = modes.StdShiftInvert(str(g["kind"]), n, sigma)
+    Acsr = c.A.tocsr()
+    A = pkg.CSR.from_arrays(Acsr.indptr, Acsr.indices, Acsr.data)
+    S = pkg.DShift(A, sigma, rtol=1e-13, maxit=4000)
+    s = pkg.SymRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
+                   mxiter=300, v0=g["v0"])
+    assert s.aupd_shift(S) == 99
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[2]) == int(g["iparam"][2])
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    assert int(s.iparam[8]) == int(g["nopx"])
+    st = S.stats()
+    assert st["solves"] == int(s.iparam[8]) and st["failures"] == 0
+    d, z, nconv = s.eupd(sigma=sigma)
+    dref = np.sort(g["d"])
+    np.testing.assert_allclose(np.sort(d), dref, rtol=1e-9, atol=0)
+
+
+def test_eigsh_shift_invert_laplace2d(pkg):
+    m = 60
+    A = pkg.CSR.laplace2d(m)
+    As = M.to_scipy(*M.laplace2d(m))
+    n = m * m
+    v0 = np.random.default_rng(5).uniform(-1, 1, n)
+    d, z, res = pkg.eigsh(A, n, nev=6, ncv=20, which="LM", tol=1e-12, v0=v0, sigma=0.0)
+    assert res["info"] == 0 and res["nconv"] == 6
+    # the square grid's spectrum is degenerate (lambda_ij = lambda_ji), where
+    # ARPACK may return one copy of a double eigenvalue and the next one (SciPy
+    # does here) or both copies: every Ritz value must be an exact eigenvalue
+    # among the smallest, and agree with SciPy's eigsh(sigma=0) where both have it
+    c = 2.0 * np.cos(np.arange(1, m + 1) * np.pi / (m + 1))
+    exact = np.sort((4.0 - c[:, None] - c[None, :]).ravel())
+    for x in d:
+        assert np.abs(exact - x).min() <= 1e-9 * x
+        assert x <= exact[7] * (1 + 1e-9)
+    dref = spl.eigsh(As.tocsc(), k=6, ncv=20, sigma=0.0, which="LM", tol=1e-12, v0=v0,
+                     return_eigenvectors=False)
+    for x in dref:
+        if x <= np.max(d):
+            assert np.abs(d - x).min() <= 1e-9 * x, (x, d)
+    for k in range(6):
+        r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
+        assert r <= 1e-9 * 8.0 * np.linalg.norm(z[:, k])
