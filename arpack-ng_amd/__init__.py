@@ -133,6 +133,7 @@ def _declare(L):
     L.arpack_hip_dshift_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_double,
                                            C.c_double, _I]
     L.arpack_hip_dshift_destroy.argtypes = [C.c_void_p]
+    L.arpack_hip_dshift_set_method.argtypes = [C.c_void_p, _I]
     L.arpack_hip_dshift_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, _PD]
     L.arpack_hip_dshift_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD] * 3
     L.arpack_hip_profile.argtypes = [_I]
@@ -659,11 +660,13 @@ class ZShift:
 
 class DShift:
     """Shift-invert operator y = (A - sigma I)^{-1} x on the GPU for a symmetric CSR
-    operator (conjugate gradients; arpack_hip_dshift_*): dsaupd's mode-3 OP
-    (SRC/dsaupd.f:30-48), the caller-side solve EXAMPLES/SYM/dsdrv2.f does with
-    dgttrf/dgttrs.  A - sigma I must be positive definite."""
+    operator (conjugate gradients or MINRES; arpack_hip_dshift_*): dsaupd's mode-3
+    OP (SRC/dsaupd.f:30-48), the caller-side solve EXAMPLES/SYM/dsdrv2.f does with
+    dgttrf/dgttrs."""
 
-    def __init__(self, A: "CSR", sigma=0.0, rtol=1e-12, maxit=1000):
+    def __init__(self, A: "CSR", sigma=0.0, rtol=1e-12, maxit=1000, method="cg"):
+        """method: "cg" (A - sigma I positive definite) or "minres" (any symmetric
+        A - sigma I, e.g. sigma inside the spectrum)."""
         self.A = A  # keeps the operator alive
         self.sigma = float(sigma)
         h = C.c_void_p()
@@ -672,6 +675,8 @@ class DShift:
             raise RuntimeError("arpack_hip_dshift_create failed (%d)" % rc)
         self.h = h.value
         self.n = A.n
+        if lib().arpack_hip_dshift_set_method(self.h, {"cg": 0, "minres": 1}[method]) != 0:
+            raise ValueError(method)
 
     def __del__(self):
         try:
@@ -806,20 +811,21 @@ class _CF(C.Structure):
 
 
 def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=True,
-          device=False, sigma=None, rtol=1e-12, maxit=1000):
+          device=False, sigma=None, rtol=1e-12, maxit=1000, solver="minres"):
     """Drive the RCI loop with a user OP (callable y = op(x) on workd slices), like
     TESTS/icb_arpack_c.c:60-65.  In device mode `op(x_addr, y_addr)` receives device
     addresses.  With `op` a CSR, the loop runs entirely on the GPU
     (arpack_hip_dsaupd_csr); with a CSR and `sigma`, in shift-invert mode 3 with
-    OP = (A - sigma I)^{-1} by the device CG (DShift; A - sigma I positive
-    definite), the eigenvalues of A nearest sigma returned (dseupd's transform).
+    OP = (A - sigma I)^{-1} by the device solve (DShift: `solver` "minres", any
+    sigma, or "cg", cheaper, A - sigma I positive definite), the eigenvalues of A
+    nearest sigma returned (dseupd's transform).
     Returns (d, Z, info-dict)."""
     ncv = ncv or min(n, max(2 * nev + 1, 20))
     shift = sigma is not None and isinstance(op, CSR)
     s = SymRci(n, nev, ncv, which, tol, mode=3 if shift else 1, mxiter=mxiter, v0=v0,
                device=device)
     if shift:
-        S = DShift(op, sigma, rtol=rtol, maxit=maxit)
+        S = DShift(op, sigma, rtol=rtol, maxit=maxit, method=solver)
         s.aupd_shift(S)
         if s.tol <= 0.0:
             s.tol = float(np.finfo(np.float64).eps / 2)

@@ -479,6 +479,13 @@ int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, d
     return 0;
 }
 
+int arpack_hip_dshift_set_method(arpack_hip_dshift* D, int method) {
+    if (!D || (method != ahip::dev::kDShiftCg && method != ahip::dev::kDShiftMinres)) return -1;
+    D->S.method = method;
+    D->S.chunk = 8;  // the previous method's iteration count says nothing here
+    return 0;
+}
+
 void arpack_hip_dshift_destroy(arpack_hip_dshift* D) {
     if (!D) return;
     ahip::dev::dshift_destroy(D->S);

@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <utility>
 
 #include "dshift.hpp"
 #include "passes.hpp"
@@ -156,6 +157,140 @@ __global__ __launch_bounds__(kT) void k_cg_p(int64_t n, const double* __restrict
         p[i] = r[i] + beta * p[i];
 }
 
+// ---- MINRES (Paige & Saunders; x0 = 0, no preconditioner) ------------------
+// Iteration k with Lanczos vector v (= r2 / beta), previous r1, r2:
+//   y = A v - sigma v - (beta/oldb) r1;  P0 <- partials of v'y     k_mr_a
+//   alfa = v'y;  y -= (alfa/beta) r2;    P1 <- partials of y'y     k_mr_b
+//   (host: r1 <- r2, r2 <- y)
+//   beta' = ||y||; the Givens recurrence (delta, gbar, epsln, dbar, gamma, cs,
+//   sn, phi, phibar); w' = (v - oldeps w1 - delta w2)/gamma; x += phi w';
+//   v' = r2 / beta'; stop when phibar <= rtol ||b||                 k_mr_c
+__global__ __launch_bounds__(kT) void k_mr_init_fin(const double* __restrict__ part, int nblk,
+                                                    CgState* __restrict__ st) {
+    const double t = cg_total(part, nblk);
+    if (threadIdx.x == 0) {
+        const double b1 = std::sqrt(t);
+        st->done = t == 0.0 ? 1 : 0;
+        st->breakdown = 0;
+        st->iters = 0;
+        st->failed = 0;
+        st->bnorm2 = t;
+        st->rnorm2 = t;
+        st->beta1 = b1;
+        MrRec& r = st->rec[0];
+        r.beta = b1;
+        r.oldb = 0.0;
+        r.cs = -1.0;
+        r.sn = 0.0;
+        r.dbar = 0.0;
+        r.epsln = 0.0;
+        r.phibar = b1;
+    }
+}
+
+// v = b / beta1 (the first Lanczos vector), w = w2 = 0, x = 0
+__global__ __launch_bounds__(kT) void k_mr_start(int64_t n, const double* __restrict__ b,
+                                                 double* __restrict__ v, double* __restrict__ w,
+                                                 double* __restrict__ w2, double* __restrict__ x,
+                                                 const CgState* __restrict__ st) {
+    if (st->done) return;
+    const double s = 1.0 / st->beta1;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        v[i] = b[i] * s;
+        w[i] = 0.0;
+        w2[i] = 0.0;
+        x[i] = 0.0;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_mr_a(int64_t n, double* __restrict__ y,
+                                             const double* __restrict__ v,
+                                             const double* __restrict__ r1, double sigma,
+                                             const CgState* __restrict__ st, int k,
+                                             double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    const MrRec& rc = st->rec[k & 1];
+    const double c1 = rc.oldb != 0.0 ? rc.beta / rc.oldb : 0.0;
+    double acc[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double vi = v[i];
+        double yi = y[i] - sigma * vi;
+        if (c1 != 0.0) yi -= c1 * r1[i];
+        y[i] = yi;
+        acc[0] += vi * yi;
+    }
+    cg_put<1>(acc, part, nblk);
+}
+
+__global__ __launch_bounds__(kT) void k_mr_b(int64_t n, double* __restrict__ y,
+                                             const double* __restrict__ r2,
+                                             CgState* __restrict__ st, int k,
+                                             const double* __restrict__ part_in,
+                                             double* __restrict__ part_out, int nblk) {
+    if (st->done) return;
+    const double alfa = cg_total(part_in, nblk);
+    const double c2 = alfa / st->rec[k & 1].beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->alpha = alfa;
+    double acc[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double yi = y[i] - c2 * r2[i];
+        y[i] = yi;
+        acc[0] += yi * yi;
+    }
+    cg_put<1>(acc, part_out, nblk);
+}
+
+// r2 = the y of k_mr_b (rotated by the host); w1 = the older w, w2 = the newer;
+// the new w overwrites w1
+__global__ __launch_bounds__(kT) void k_mr_c(int64_t n, double* __restrict__ v,
+                                             const double* __restrict__ r2,
+                                             double* __restrict__ w1, const double* __restrict__ w2,
+                                             double* __restrict__ x, CgState* __restrict__ st, int k,
+                                             double rtol, const double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    const double yy = cg_total(part, nblk);
+    const MrRec& o = st->rec[k & 1];
+    const double alfa = st->alpha;
+    const double beta = std::sqrt(yy);
+    const double oldeps = o.epsln;
+    const double delta = o.cs * o.dbar + o.sn * alfa;
+    const double gbar = o.sn * o.dbar - o.cs * alfa;
+    const double epsln = o.sn * beta;
+    const double dbar = -o.cs * beta;
+    const double gamma = std::sqrt(gbar * gbar + beta * beta);
+    const bool bd = !(gamma > 0.0);
+    const double cs = bd ? 0.0 : gbar / gamma, sn = bd ? 0.0 : beta / gamma;
+    const double phi = cs * o.phibar, phibar = sn * o.phibar;
+    const bool conv = phibar <= rtol * st->beta1;
+    // beta = 0: the Krylov space is invariant, x is exact (phibar = 0 then)
+    const bool stop = bd || conv || !(beta > 0.0) || !(phibar == phibar);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        MrRec& r = st->rec[(k + 1) & 1];
+        r.beta = beta;
+        r.oldb = o.beta;
+        r.cs = cs;
+        r.sn = sn;
+        r.dbar = dbar;
+        r.epsln = epsln;
+        r.phibar = phibar;
+        st->rnorm2 = phibar * phibar;
+        if (stop) {
+            st->iters = k + 1;
+            st->breakdown = bd ? 1 : 0;
+            st->failed = conv ? 0 : 1;  // (beta = 0 gives sn = 0, phibar = 0: converged)
+            st->done = 1;
+        }
+    }
+    if (bd) return;
+    const double dinv = 1.0 / gamma, vs = beta > 0.0 ? 1.0 / beta : 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double wn = (v[i] - oldeps * w1[i] - delta * w2[i]) * dinv;
+        w1[i] = wn;
+        x[i] += phi * wn;
+        v[i] = r2[i] * vs;
+    }
+}
+
 }  // namespace
 
 int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit) {
@@ -169,9 +304,8 @@ int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit)
     S.nblk = (int)(g < 1 ? 1 : (g > kMaxBlk ? kMaxBlk : g));
     const size_t vb = sizeof(double) * (size_t)(S.n > 0 ? S.n : 1);
     hipError_t e = hipSuccess;
-    double** vecs[] = {&S.r, &S.p, &S.w};
-    for (double** q : vecs)
-        if (e == hipSuccess) e = hipMalloc(q, vb);
+    for (double*& q : S.vec)
+        if (e == hipSuccess) e = hipMalloc(&q, vb);
     if (e == hipSuccess) e = hipMalloc(&S.part, sizeof(double) * 2 * (size_t)S.nblk);
     if (e == hipSuccess) e = hipMalloc(&S.st, sizeof(CgState));
     if (e == hipSuccess) e = hipHostMalloc(&S.st_host, sizeof(CgState));
@@ -186,9 +320,9 @@ int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit)
 }
 
 void dshift_destroy(DShift& S) {
-    double* vecs[] = {S.r, S.p, S.w, S.part};
-    for (double* q : vecs)
+    for (double* q : S.vec)
         if (q) (void)hipFree(q);
+    if (S.part) (void)hipFree(S.part);
     if (S.st) (void)hipFree(S.st);
     if (S.st_host) (void)hipHostFree(S.st_host);
     if (S.ev0) (void)hipEventDestroy(S.ev0);
@@ -198,8 +332,10 @@ void dshift_destroy(DShift& S) {
 
 double dshift_iter_bytes(const DShift& S) {
     // the product as its storage streams it (csr_bytes: matrix + x/y), and the
-    // 11 n-vector passes of k_cg_pq (w, p), k_cg_xr (w, p, y, r; y, r) and k_cg_p (r, p; p)
-    return csr_bytes(*S.A) + 88.0 * (double)S.n;
+    // n-vector passes -- CG 11: k_cg_pq (w, p), k_cg_xr (w, p, y, r; y, r),
+    // k_cg_p (r, p; p); MINRES 16: k_mr_a (y, v, r1; y), k_mr_b (y, r2; y),
+    // k_mr_c (v, r2, w1, w2, x; w1, x, v)
+    return csr_bytes(*S.A) + (S.method == kDShiftMinres ? 128.0 : 88.0) * (double)S.n;
 }
 
 int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double* relres) {
@@ -208,19 +344,45 @@ int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double
     double* P0 = S.part;
     double* P1 = S.part + nb;
     if (hipEventRecord(S.ev0, strm) != hipSuccess) return -2;
-    hipLaunchKernelGGL(k_cg_init, dim3(nb), dim3(kT), 0, strm, n, b, S.r, S.p, y, P0, nb);
-    hipLaunchKernelGGL(k_cg_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
+    const bool mr = S.method == kDShiftMinres;
+    // CG: r, p, w; MINRES: v, r1, r2, y (rotated r1 <- r2 <- y <- r1 each
+    // iteration) and w1, w2 (swapped each iteration)
+    double *r = S.vec[0], *p = S.vec[1], *w = S.vec[2];
+    double *mv = S.vec[0], *r1 = S.vec[1], *r2 = S.vec[2], *my = S.vec[3], *w1 = S.vec[4],
+           *w2 = S.vec[5];
+    if (mr) {
+        hipLaunchKernelGGL(k_cg_init, dim3(nb), dim3(kT), 0, strm, n, b, r1, r2, my, P0, nb);
+        hipLaunchKernelGGL(k_mr_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
+        hipLaunchKernelGGL(k_mr_start, dim3(nb), dim3(kT), 0, strm, n, b, mv, w1, w2, y, S.st);
+    } else {
+        hipLaunchKernelGGL(k_cg_init, dim3(nb), dim3(kT), 0, strm, n, b, r, p, y, P0, nb);
+        hipLaunchKernelGGL(k_cg_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
+    }
     const double rtol2 = S.rtol * S.rtol;
     int k = 0, chunk = S.chunk > 0 ? S.chunk : 8;
     bool done = false;
     while (k < S.maxit) {
         const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
         for (int q = 0; q < m; ++q, ++k) {
-            csr_spmv(strm, *S.A, S.p, S.w);
-            hipLaunchKernelGGL(k_cg_pq, dim3(nb), dim3(kT), 0, strm, n, S.w, S.p, S.sigma, S.st, P0, nb);
-            hipLaunchKernelGGL(k_cg_xr, dim3(nb), dim3(kT), 0, strm, n, S.w, S.p, S.sigma, y, S.r, S.st,
-                               k, P0, P1, nb);
-            hipLaunchKernelGGL(k_cg_p, dim3(nb), dim3(kT), 0, strm, n, S.r, S.p, S.st, k, rtol2, P1, nb);
+            if (mr) {
+                csr_spmv(strm, *S.A, mv, my);
+                hipLaunchKernelGGL(k_mr_a, dim3(nb), dim3(kT), 0, strm, n, my, mv, r1, S.sigma, S.st, k,
+                                   P0, nb);
+                hipLaunchKernelGGL(k_mr_b, dim3(nb), dim3(kT), 0, strm, n, my, r2, S.st, k, P0, P1, nb);
+                double* t = r1;  // r1 <- r2, r2 <- y, y <- the old r1 (free)
+                r1 = r2;
+                r2 = my;
+                my = t;
+                hipLaunchKernelGGL(k_mr_c, dim3(nb), dim3(kT), 0, strm, n, mv, r2, w1, w2, y, S.st, k,
+                                   S.rtol, P1, nb);
+                std::swap(w1, w2);  // the new w (written over w1) is the newer one now
+                continue;
+            }
+            csr_spmv(strm, *S.A, p, w);
+            hipLaunchKernelGGL(k_cg_pq, dim3(nb), dim3(kT), 0, strm, n, w, p, S.sigma, S.st, P0, nb);
+            hipLaunchKernelGGL(k_cg_xr, dim3(nb), dim3(kT), 0, strm, n, w, p, S.sigma, y, r, S.st, k,
+                               P0, P1, nb);
+            hipLaunchKernelGGL(k_cg_p, dim3(nb), dim3(kT), 0, strm, n, r, p, S.st, k, rtol2, P1, nb);
         }
         if (hipGetLastError() != hipSuccess ||
             hipMemcpyAsync(S.st_host, S.st, sizeof(CgState), hipMemcpyDeviceToHost, strm) !=

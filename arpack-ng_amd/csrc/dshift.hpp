@@ -1,5 +1,7 @@
 // Device shift-invert operator of the symmetric engine: y = (A - sigma I)^{-1} x
-// by conjugate gradients on the real CSR operator, every step on the GPU.
+// by conjugate gradients (positive-definite A - sigma I) or MINRES (any
+// symmetric A - sigma I: sigma inside the spectrum, interior eigenvalues) on the
+// real CSR operator, every step on the GPU.
 //
 // The caller-side solve of dsaupd's mode 3 (SRC/dsaupd.f:30-48, OP = inv[A -
 // sigma M] M with M = I), which the reference's drivers do with a banded LU on
@@ -12,7 +14,9 @@
 // partials themselves in one fixed order (as the complex BiCGStab,
 // zsolve.hip).  An indefinite A - sigma I can break CG down: the solve then
 // reports failure (a non-positive curvature p'(A - sigma I)p, or no
-// convergence within maxit) and the Arnoldi run stops with info = -9999.
+// convergence within maxit) and the Lanczos run stops with info = -9999;
+// MINRES (method kDShiftMinres) serves indefinite shifts, one more vector pass
+// an iteration.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -22,25 +26,37 @@
 
 namespace ahip::dev {
 
+// MINRES recurrence scalars at the start of an iteration (Paige & Saunders)
+struct MrRec {
+    double beta, oldb, cs, sn, dbar, epsln, phibar;
+};
+
+// device-resident solver state (CG, or MINRES: rec double-buffered by
+// iteration parity, so a kernel's blocks read one copy while block 0 writes the other)
 struct CgState {
     int done;       // converged, broke down or hit maxit: later kernels return at once
-    int breakdown;  // p'(A - sigma I)p <= 0 (not positive definite) before convergence
+    int breakdown;  // CG: p'(A - sigma I)p <= 0 (not positive definite); MINRES: gamma = 0
     int iters;      // iterations taken when done
     int failed;     // done without reaching rtol
-    double rho[2];  // r'r of iteration k at [k & 1]
-    double alpha;
+    double rho[2];  // CG: r'r of iteration k at [k & 1]
+    double alpha;   // CG: alpha; MINRES: alfa = v'(A - sigma I)v of the iteration
     double bnorm2;  // ||b||^2
-    double rnorm2;  // ||r||^2 of the last iteration
+    double rnorm2;  // ||r||^2 of the last iteration (MINRES: phibar^2, its estimate)
+    double beta1;   // MINRES: ||b||
+    MrRec rec[2];
 };
+
+enum DShiftMethod { kDShiftCg = 0, kDShiftMinres = 1 };
 
 struct DShift {
     const Csr* A = nullptr;
     double sigma = 0.0;
     double rtol = 1e-12;
     int maxit = 1000;
+    int method = kDShiftCg;
     int64_t n = 0;
     int nblk = 0;
-    double *r = nullptr, *p = nullptr, *w = nullptr;  // n each
+    double* vec[6] = {};  // n each -- CG: r, p, w; MINRES: v, r1, r2, y, w, w2
     double* part = nullptr;                           // 2 regions x 2 slots x nblk
     CgState* st = nullptr;                            // device
     CgState* st_host = nullptr;                       // pinned mirror
@@ -59,8 +75,8 @@ void dshift_destroy(DShift& S);
 // updated residual; -1 if CG broke down or did not reach rtol within maxit (y
 // then holds the last iterate), -2 on a HIP error.
 int dshift_apply(DShift& S, hipStream_t stream, const double* b, double* y, double* relres);
-// algorithmic HBM bytes of one CG iteration (the CSR product in its storage and
-// the fused vector passes)
+// algorithmic HBM bytes of one iteration (the CSR product in its storage and
+// the fused vector passes of the method)
 double dshift_iter_bytes(const DShift& S);
 
 }  // namespace ahip::dev

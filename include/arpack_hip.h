@@ -317,7 +317,7 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, 
                               a_dcomplex* workl, int lworkl, double* rwork, int* info);
 
 /* ---- shift-invert on the device, symmetric (dsaupd mode 3) ------------------
- * y = (A - sigma I)^{-1} x by conjugate gradients on the device CSR operator A
+ * y = (A - sigma I)^{-1} x by conjugate gradients (or MINRES, below) on the device CSR operator A
  * (full or symmetric storage), to ||r|| <= rtol ||x|| within maxit iterations:
  * the caller-side solve of dsaupd's mode 3 (SRC/dsaupd.f:30-48), which the
  * reference's EXAMPLES/SYM/dsdrv2.f does with dgttrf/dgttrs.  A - sigma I must be
@@ -328,6 +328,10 @@ typedef struct arpack_hip_dshift arpack_hip_dshift;
 int arpack_hip_dshift_create(arpack_hip_dshift** S, const arpack_hip_csr* A, double sigma,
                              double rtol, int maxit);
 void arpack_hip_dshift_destroy(arpack_hip_dshift* S);
+/* 0: conjugate gradients (the default; A - sigma I positive definite), 1: MINRES
+ * (any symmetric A - sigma I, e.g. sigma inside the spectrum for interior
+ * eigenvalues; 16 instead of 11 vector passes an iteration).  0 or -1. */
+int arpack_hip_dshift_set_method(arpack_hip_dshift* S, int method);
 /* x, y device pointers (y != x); synchronous.  The iterations (>= 0; *relres =
  * ||r||/||x||), -1 on breakdown / missed rtol, -2 on a HIP error. */
 int arpack_hip_dshift_solve(arpack_hip_dshift* S, const double* x, double* y, double* relres);

@@ -1,6 +1,6 @@
 """GPU: the device shift-invert operator of the symmetric engine (csrc/dshift.hip:
-conjugate gradients on the real CSR operator) and dsaupd in mode 3 with it as OP
-(arpack_hip_dsaupd_shift).
+conjugate gradients or MINRES on the real CSR operator) and dsaupd in mode 3
+with it as OP (arpack_hip_dsaupd_shift).
 
   * the solve against SciPy's direct solve (true residual ||(A - sigma I) y - x||
     <= 1e-11 ||x||), full and symmetric storage; b = 0 gives y = 0;
@@ -11,7 +11,10 @@ conjugate gradients on the real CSR operator) and dsaupd in mode 3 with it as OP
     setting: 1-D FEM stiffness n = 400, sigma = 0, nev 4, ncv 20, tol 1e-10):
     the same restart cycles, OP*x count and converged set, eigenvalues within
     1e-9 relative;
-  * eigsh(CSR, sigma=...) on a 2-D Laplacian against SciPy's eigsh(sigma=...).
+  * eigsh(CSR, sigma=...) on a 2-D Laplacian against SciPy's eigsh(sigma=...);
+  * MINRES with sigma inside the spectrum (indefinite A - sigma I): the solve
+    against SciPy's direct solve, and interior eigenvalues against the exact
+    spectrum (parity unpinned by a reference fixture: analytic answers).
 """
 import os
 import sys
@@ -29,16 +32,17 @@ import modes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("method", ["cg", "minres"])
 @pytest.mark.parametrize("storage", ["full", "sym"])
 @pytest.mark.parametrize("sigma", [0.0, -0.5])
-def test_dshift_solve(pkg, storage, sigma):
+def test_dshift_solve(pkg, storage, sigma, method):
     m = 120
     A = pkg.CSR.laplace2d(m)
     As = M.to_scipy(*M.laplace2d(m))
     if storage == "sym":
         A.set_symmetric(True)
     n = m * m
-    S = pkg.DShift(A, sigma, rtol=1e-12, maxit=2000)
+    S = pkg.DShift(A, sigma, rtol=1e-12, maxit=2000, method=method)
     x = np.random.default_rng(3).uniform(-1, 1, n)
     y, it, rr = S.solve(x)
     assert it > 0 and rr <= 1e-12, (it, rr)
@@ -62,13 +66,14 @@ def test_dshift_negative_definite_fails_loudly(pkg):
     assert s.aupd_shift(S) == 99 and int(s.info[0]) == -9999
 
 
-def test_dsaupd_mode3_device_solve_m2(pkg, golden):
+@pytest.mark.parametrize("method", ["cg", "minres"])
+def test_dsaupd_mode3_device_solve_m2(pkg, golden, method):
     g = golden("m2_sym_std_si")
     n, sigma = int(g["n"]), float(g["sigma"])
     c = modes.StdShiftInvert(str(g["kind"]), n, sigma)
     Acsr = c.A.tocsr()
     A = pkg.CSR.from_arrays(Acsr.indptr, Acsr.indices, Acsr.data)
-    S = pkg.DShift(A, sigma, rtol=1e-13, maxit=4000)
+    S = pkg.DShift(A, sigma, rtol=1e-13, maxit=4000, method=method)
     s = pkg.SymRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
                    mxiter=300, v0=g["v0"])
     assert s.aupd_shift(S) == 99
@@ -106,5 +111,47 @@ def test_eigsh_shift_invert_laplace2d(pkg):
         if x <= np.max(d):
             assert np.abs(d - x).min() <= 1e-9 * x, (x, d)
     for k in range(6):
+        r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
+        assert r <= 1e-9 * 8.0 * np.linalg.norm(z[:, k])
+
+
+def test_minres_indefinite_solve(pkg):
+    """sigma inside the spectrum: A - sigma I indefinite, where CG breaks down and
+    MINRES converges (true residual <= 1e-10 ||x||, against SciPy's direct solve)."""
+    m = 40
+    A = pkg.CSR.laplace2d(m)
+    As = M.to_scipy(*M.laplace2d(m))
+    n = m * m
+    sigma = 3.93
+    x = np.random.default_rng(9).uniform(-1, 1, n)
+    S = pkg.DShift(A, sigma, rtol=1e-12, maxit=20000, method="minres")
+    y, it, rr = S.solve(x)
+    assert it > 0 and rr <= 1e-12, (it, rr)
+    Bs = (As - sigma * sp.identity(n)).tocsc()
+    assert np.linalg.norm(Bs @ y - x) <= 1e-10 * np.linalg.norm(x)
+    yref = spl.spsolve(Bs, x)
+    assert np.linalg.norm(y - yref) <= 1e-8 * np.linalg.norm(yref)
+
+
+def test_eigsh_interior_eigenvalues_minres(pkg):
+    """Interior eigenvalues (nearest sigma = 3.93 of a 2-D Laplacian spectrum in
+    (0, 8)) by shift-invert mode 3 with the device MINRES: every Ritz value an
+    exact eigenvalue among the nearest to sigma, residuals <= 1e-9 ||A||."""
+    m = 40
+    A = pkg.CSR.laplace2d(m)
+    As = M.to_scipy(*M.laplace2d(m))
+    n = m * m
+    sigma = 3.93
+    v0 = np.random.default_rng(2).uniform(-1, 1, n)
+    d, z, res = pkg.eigsh(A, n, nev=4, ncv=20, which="LM", tol=1e-10, v0=v0, sigma=sigma,
+                          maxit=20000, solver="minres")
+    assert res["info"] == 0 and res["nconv"] == 4
+    c = 2.0 * np.cos(np.arange(1, m + 1) * np.pi / (m + 1))
+    exact = (4.0 - c[:, None] - c[None, :]).ravel()
+    near = exact[np.argsort(np.abs(exact - sigma))]
+    for x in d:
+        assert np.abs(exact - x).min() <= 1e-9 * abs(x)
+        assert abs(x - sigma) <= abs(near[7] - sigma) * (1 + 1e-9)
+    for k in range(4):
         r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
         assert r <= 1e-9 * 8.0 * np.linalg.norm(z[:, k])
