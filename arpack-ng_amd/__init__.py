@@ -110,6 +110,7 @@ def _declare(L):
     L.arpack_hip_dsaupd_shift.argtypes = [C.c_void_p, _PI, C.c_char_p, _I, C.c_char_p, _I,
                                           C.POINTER(C.c_double), _PD, _I, _PD, _I, _PI, _PI,
                                           _PD, _PD, _I, _PI]
+    L.arpack_hip_dnaupd_shift.argtypes = L.arpack_hip_dsaupd_shift.argtypes
     L.arpack_hip_gen_convdiff2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
     L.znaupd_c.argtypes = [_PI, C.c_char_p, _I, C.c_char_p, _I, C.c_double, _PD, _I, _PD, _I,
                            _PI, _PI, _PD, _PD, _I, _PD, _PI]
@@ -527,6 +528,18 @@ class NsRci(SymRci):
         self.tol = tol.value
         return int(self.ido[0])
 
+    def aupd_shift(self, S: "DShift"):
+        """dnaupd in mode 3 (real shift) with OP = (A - sigma I)^{-1} by the
+        device BiCGStab S (arpack_hip_dnaupd_shift)."""
+        tol = C.c_double(self.tol)
+        lib().arpack_hip_dnaupd_shift(S.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                      self.which.encode(), self.nev, C.byref(tol),
+                                      _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                      _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                      self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
     def aupd_csr(self, A: CSR):
         r = self.aupd_cycles(A, -1)
         if self.tol <= 0.0:
@@ -665,8 +678,9 @@ class DShift:
     dgttrf/dgttrs."""
 
     def __init__(self, A: "CSR", sigma=0.0, rtol=1e-12, maxit=1000, method="cg"):
-        """method: "cg" (A - sigma I positive definite) or "minres" (any symmetric
-        A - sigma I, e.g. sigma inside the spectrum)."""
+        """method: "cg" (A - sigma I positive definite), "minres" (any symmetric
+        A - sigma I, e.g. sigma inside the spectrum) or "bicgstab" (a nonsymmetric
+        A: dnaupd's real shift-invert)."""
         self.A = A  # keeps the operator alive
         self.sigma = float(sigma)
         h = C.c_void_p()
@@ -675,7 +689,8 @@ class DShift:
             raise RuntimeError("arpack_hip_dshift_create failed (%d)" % rc)
         self.h = h.value
         self.n = A.n
-        if lib().arpack_hip_dshift_set_method(self.h, {"cg": 0, "minres": 1}[method]) != 0:
+        if lib().arpack_hip_dshift_set_method(self.h, {"cg": 0, "minres": 1,
+                                                       "bicgstab": 2}[method]) != 0:
             raise ValueError(method)
 
     def __del__(self):
@@ -885,6 +900,8 @@ def eigs(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=
         mode 3 with OP = (A - sigma I)^{-1} by the device BiCGStab (ZShift, to
         rtol within maxit iterations) -- eigenvalues of A returned (zneupd's
         transform);
+      * op a CSR and a real sigma: dnaupd in shift-invert mode 3 with OP =
+        (A - sigma I)^{-1} by the device BiCGStab (DShift);
       * op a callable y = op(x) on host vectors: the dnaupd RCI loop (real x).
 
     Returns (d, Z, info-dict) with complex eigenvalues d (nconv of them) and,
@@ -904,8 +921,14 @@ def eigs(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=
                    nopx=int(s.iparam[8]))
         d, z, nconv = s.eupd(rvec=rvec, sigma=0j if sigma is None else complex(sigma))
         return d, (z if rvec else None), res
-    s = NsRci(n, nev, ncv, which, tol, mxiter=mxiter, v0=v0)
-    if isinstance(op, CSR):
+    shift = sigma is not None and isinstance(op, CSR)
+    s = NsRci(n, nev, ncv, which, tol, mode=3 if shift else 1, mxiter=mxiter, v0=v0)
+    if shift:  # real shift-invert: OP = (A - sigma I)^{-1} by the device BiCGStab
+        S = DShift(op, float(sigma), rtol=rtol, maxit=maxit, method="bicgstab")
+        s.aupd_shift(S)
+        if s.tol <= 0.0:
+            s.tol = float(np.finfo(np.float64).eps / 2)
+    elif isinstance(op, CSR):
         s.aupd_csr(op)
     else:
         while True:
@@ -920,7 +943,7 @@ def eigs(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=
         raise ArpackError("dnaupd", int(s.info[0]))
     res = dict(info=int(s.info[0]), iters=int(s.iparam[2]), nconv=int(s.iparam[4]),
                nopx=int(s.iparam[8]))
-    dr, di, z, nconv = s.eupd(rvec=rvec)
+    dr, di, z, nconv = s.eupd(rvec=rvec, sigmar=float(sigma) if shift else 0.0)
     d = dr + 1j * di
     return d, (_ns_vectors(dr, di, z, n, nconv) if rvec else None), res
 

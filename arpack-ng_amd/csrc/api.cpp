@@ -160,7 +160,10 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
                       : sym_check(bmat[0], n, w, nev, ncv, lworkl, mode, ishift, mxiter);
         // a device OP serves mode 1 (OP = A), or mode 3 through the device solve
         // (symmetric only: CG); bmat = 'I'
-        if (csr && ((shift ? mode != 3 || ns || dist : mode != 1) || bmat[0] != 'I' || csr->n != n))
+        // (dnaupd: a nonsymmetric A needs the general solve, BiCGStab)
+        if (csr && ((shift ? mode != 3 || dist || (ns && shift->method != dev::kDShiftBicgstab)
+                           : mode != 1) ||
+                    bmat[0] != 'I' || csr->n != n))
             ierr = (ierr ? ierr : -11);
         if (dist && dist->nloc != n) ierr = (ierr ? ierr : -1);
         if (ierr != 0) {
@@ -480,7 +483,7 @@ int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, d
 }
 
 int arpack_hip_dshift_set_method(arpack_hip_dshift* D, int method) {
-    if (!D || (method != ahip::dev::kDShiftCg && method != ahip::dev::kDShiftMinres)) return -1;
+    if (!D || method < ahip::dev::kDShiftCg || method > ahip::dev::kDShiftBicgstab) return -1;
     D->S.method = method;
     D->S.chunk = 8;  // the previous method's iteration count says nothing here
     return 0;
@@ -522,6 +525,22 @@ void arpack_hip_dsaupd_shift(arpack_hip_dshift* D, int* ido, char const* bmat, i
     }
     sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
              info, nullptr, -1, nullptr, false, &D->S);
+}
+
+// dnaupd in mode 3 with a real shift, OP = (A - sigma I)^{-1} by the device
+// BiCGStab (arpack_hip_dshift_set_method(S, 2)); dneupd_c with sigmar = sigma,
+// sigmai = 0 then gives the eigenvalues of A
+void arpack_hip_dnaupd_shift(arpack_hip_dshift* D, int* ido, char const* bmat, int n,
+                             char const* which, int nev, double* tol, double* resid, int ncv,
+                             double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                             double* workl, int lworkl, int* info) {
+    if (!D) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr, -1, nullptr, true, &D->S);
 }
 
 // Row-block distributed solve (PARPACK's pdsaupd decomposition, n = LOCAL rows):

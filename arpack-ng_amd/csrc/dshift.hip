@@ -291,6 +291,145 @@ __global__ __launch_bounds__(kT) void k_mr_c(int64_t n, double* __restrict__ v,
     }
 }
 
+// ---- BiCGStab (van der Vorst; x0 = 0, rh = b), the real twin of zsolve.hip --
+//   w = A p;  v = w - sigma p;  P0 <- partials of rh'v              k_bs_v
+//   alpha = rho / rh'v;  s = r - alpha v                           k_bs_s (reduces P0)
+//   w = A s;  t = w - sigma s;  P0 <- partials of t's, t't         k_bs_t
+//   omega = t's / t't;  x += alpha p + omega s;  r = s - omega t;  k_bs_xr (reduces P0)
+//   P1 <- partials of rh'r, r'r
+//   rho' = rh'r; stop if ||r|| <= rtol ||b||, else
+//   p = r + (rho'/rho)(alpha/omega)(p - omega v)                  k_bs_p (reduces P1)
+__global__ __launch_bounds__(kT) void k_bs_init(int64_t n, const double* __restrict__ b,
+                                                double* __restrict__ r, double* __restrict__ rh,
+                                                double* __restrict__ p, double* __restrict__ x,
+                                                double* __restrict__ part, int nblk) {
+    double acc[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double bi = b[i];
+        r[i] = bi;
+        rh[i] = bi;
+        p[i] = bi;
+        x[i] = 0.0;
+        acc[0] += bi * bi;
+    }
+    cg_put<1>(acc, part, nblk);
+}
+
+template <int NS>
+__device__ __forceinline__ void cg_totals(const double* __restrict__ part, int nblk, double (&out)[NS]) {
+    __shared__ double red[kT / 64][NS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        double a = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kT) a += part[(int64_t)q * nblk + b];
+        a = wave_sum(a);
+        if (lane == 0) red[wave][q] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NS; ++q) out[q] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+}
+
+__global__ __launch_bounds__(kT) void k_bs_v(int64_t n, const double* __restrict__ w,
+                                             const double* __restrict__ p,
+                                             const double* __restrict__ rh, double* __restrict__ v,
+                                             double sigma, const CgState* __restrict__ st,
+                                             double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double acc[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double vi = w[i] - sigma * p[i];
+        v[i] = vi;
+        acc[0] += rh[i] * vi;
+    }
+    cg_put<1>(acc, part, nblk);
+}
+
+__global__ __launch_bounds__(kT) void k_bs_s(int64_t n, const double* __restrict__ r,
+                                             const double* __restrict__ v, double* __restrict__ s,
+                                             CgState* __restrict__ st, int k,
+                                             const double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    const double d = cg_total(part, nblk);
+    const bool bd = d == 0.0;
+    const double alpha = bd ? 0.0 : st->rho[k & 1] / d;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->alpha = alpha;
+        if (bd) st->breakdown = 1;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT)
+        s[i] = r[i] - alpha * v[i];
+}
+
+__global__ __launch_bounds__(kT) void k_bs_t(int64_t n, const double* __restrict__ w,
+                                             const double* __restrict__ s, double* __restrict__ t,
+                                             double sigma, const CgState* __restrict__ st,
+                                             double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double si = s[i];
+        const double ti = w[i] - sigma * si;
+        t[i] = ti;
+        acc[0] += ti * si;
+        acc[1] += ti * ti;
+    }
+    cg_put<2>(acc, part, nblk);
+}
+
+__global__ __launch_bounds__(kT) void k_bs_xr(int64_t n, double* __restrict__ x,
+                                              const double* __restrict__ p,
+                                              const double* __restrict__ s,
+                                              const double* __restrict__ t, double* __restrict__ r,
+                                              const double* __restrict__ rh,
+                                              CgState* __restrict__ st,
+                                              const double* __restrict__ part_in,
+                                              double* __restrict__ part_out, int nblk) {
+    if (st->done) return;
+    double tt[2];
+    cg_totals<2>(part_in, nblk, tt);
+    const double omega = tt[1] > 0.0 ? tt[0] / tt[1] : 0.0;  // t = 0 (s = 0): r = s, stop next
+    const double alpha = st->alpha;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->omega = omega;
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double si = s[i];
+        x[i] += alpha * p[i] + omega * si;
+        const double ri = si - omega * t[i];
+        r[i] = ri;
+        acc[0] += rh[i] * ri;
+        acc[1] += ri * ri;
+    }
+    cg_put<2>(acc, part_out, nblk);
+}
+
+__global__ __launch_bounds__(kT) void k_bs_p(int64_t n, const double* __restrict__ r,
+                                             double* __restrict__ p, const double* __restrict__ v,
+                                             CgState* __restrict__ st, int k, double rtol2,
+                                             const double* __restrict__ part, int nblk) {
+    if (st->done) return;
+    double tt[2];
+    cg_totals<2>(part, nblk, tt);
+    const double rho1 = tt[0], rho0 = st->rho[k & 1];
+    const double alpha = st->alpha, omega = st->omega;
+    const bool conv = tt[1] <= rtol2 * st->bnorm2;
+    const bool stop = conv || st->breakdown || omega == 0.0 || rho1 == 0.0 || !(tt[1] == tt[1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rho[(k + 1) & 1] = rho1;
+        st->rnorm2 = tt[1];
+        if (stop) {
+            st->iters = k + 1;
+            st->failed = conv ? 0 : 1;
+            st->done = 1;
+        }
+    }
+    if (stop) return;
+    const double beta = (rho1 / rho0) * (alpha / omega);
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT)
+        p[i] = r[i] + beta * (p[i] - omega * v[i]);
+}
+
 }  // namespace
 
 int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit) {
@@ -306,7 +445,7 @@ int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit)
     hipError_t e = hipSuccess;
     for (double*& q : S.vec)
         if (e == hipSuccess) e = hipMalloc(&q, vb);
-    if (e == hipSuccess) e = hipMalloc(&S.part, sizeof(double) * 2 * (size_t)S.nblk);
+    if (e == hipSuccess) e = hipMalloc(&S.part, sizeof(double) * 4 * (size_t)S.nblk);
     if (e == hipSuccess) e = hipMalloc(&S.st, sizeof(CgState));
     if (e == hipSuccess) e = hipHostMalloc(&S.st_host, sizeof(CgState));
     if (e == hipSuccess) e = hipEventCreate(&S.ev0);
@@ -335,6 +474,9 @@ double dshift_iter_bytes(const DShift& S) {
     // n-vector passes -- CG 11: k_cg_pq (w, p), k_cg_xr (w, p, y, r; y, r),
     // k_cg_p (r, p; p); MINRES 16: k_mr_a (y, v, r1; y), k_mr_b (y, r2; y),
     // k_mr_c (v, r2, w1, w2, x; w1, x, v)
+    // BiCGStab: two products and 18 passes -- k_bs_v (w, p, rh; v), k_bs_s (r, v; s),
+    // k_bs_t (w, s; t), k_bs_xr (x, p, s, t, rh; x, r), k_bs_p (r, p, v; p)
+    if (S.method == kDShiftBicgstab) return 2.0 * csr_bytes(*S.A) + 144.0 * (double)S.n;
     return csr_bytes(*S.A) + (S.method == kDShiftMinres ? 128.0 : 88.0) * (double)S.n;
 }
 
@@ -342,7 +484,7 @@ int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double
     const int64_t n = S.n;
     const int nb = S.nblk;
     double* P0 = S.part;
-    double* P1 = S.part + nb;
+    double* P1 = S.part + 2 * (size_t)nb;  // 2 slots a region (BiCGStab)
     if (hipEventRecord(S.ev0, strm) != hipSuccess) return -2;
     const bool mr = S.method == kDShiftMinres;
     // CG: r, p, w; MINRES: v, r1, r2, y (rotated r1 <- r2 <- y <- r1 each
@@ -350,7 +492,13 @@ int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double
     double *r = S.vec[0], *p = S.vec[1], *w = S.vec[2];
     double *mv = S.vec[0], *r1 = S.vec[1], *r2 = S.vec[2], *my = S.vec[3], *w1 = S.vec[4],
            *w2 = S.vec[5];
-    if (mr) {
+    const bool bs = S.method == kDShiftBicgstab;
+    double *br = S.vec[0], *brh = S.vec[1], *bp = S.vec[2], *bv = S.vec[3], *bsv = S.vec[4],
+           *bt = S.vec[5], *bw = S.vec[6];
+    if (bs) {
+        hipLaunchKernelGGL(k_bs_init, dim3(nb), dim3(kT), 0, strm, n, b, br, brh, bp, y, P0, nb);
+        hipLaunchKernelGGL(k_cg_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
+    } else if (mr) {
         hipLaunchKernelGGL(k_cg_init, dim3(nb), dim3(kT), 0, strm, n, b, r1, r2, my, P0, nb);
         hipLaunchKernelGGL(k_mr_init_fin, dim3(1), dim3(kT), 0, strm, P0, nb, S.st);
         hipLaunchKernelGGL(k_mr_start, dim3(nb), dim3(kT), 0, strm, n, b, mv, w1, w2, y, S.st);
@@ -364,6 +512,20 @@ int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double
     while (k < S.maxit) {
         const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
         for (int q = 0; q < m; ++q, ++k) {
+            if (bs) {
+                csr_spmv(strm, *S.A, bp, bw);
+                hipLaunchKernelGGL(k_bs_v, dim3(nb), dim3(kT), 0, strm, n, bw, bp, brh, bv, S.sigma, S.st,
+                                   P0, nb);
+                hipLaunchKernelGGL(k_bs_s, dim3(nb), dim3(kT), 0, strm, n, br, bv, bsv, S.st, k, P0, nb);
+                csr_spmv(strm, *S.A, bsv, bw);
+                hipLaunchKernelGGL(k_bs_t, dim3(nb), dim3(kT), 0, strm, n, bw, bsv, bt, S.sigma, S.st,
+                                   P0, nb);
+                hipLaunchKernelGGL(k_bs_xr, dim3(nb), dim3(kT), 0, strm, n, y, bp, bsv, bt, br, brh,
+                                   S.st, P0, P1, nb);
+                hipLaunchKernelGGL(k_bs_p, dim3(nb), dim3(kT), 0, strm, n, br, bp, bv, S.st, k, rtol2,
+                                   P1, nb);
+                continue;
+            }
             if (mr) {
                 csr_spmv(strm, *S.A, mv, my);
                 hipLaunchKernelGGL(k_mr_a, dim3(nb), dim3(kT), 0, strm, n, my, mv, r1, S.sigma, S.st, k,

@@ -44,9 +44,12 @@ struct CgState {
     double rnorm2;  // ||r||^2 of the last iteration (MINRES: phibar^2, its estimate)
     double beta1;   // MINRES: ||b||
     MrRec rec[2];
+    double omega;   // BiCGStab
 };
 
-enum DShiftMethod { kDShiftCg = 0, kDShiftMinres = 1 };
+// CG: A - sigma I symmetric positive definite; MINRES: symmetric; BiCGStab:
+// general (dnaupd's real shift-invert)
+enum DShiftMethod { kDShiftCg = 0, kDShiftMinres = 1, kDShiftBicgstab = 2 };
 
 struct DShift {
     const Csr* A = nullptr;
@@ -56,7 +59,8 @@ struct DShift {
     int method = kDShiftCg;
     int64_t n = 0;
     int nblk = 0;
-    double* vec[6] = {};  // n each -- CG: r, p, w; MINRES: v, r1, r2, y, w, w2
+    double* vec[7] = {};  // n each -- CG: r, p, w; MINRES: v, r1, r2, y, w, w2;
+                          // BiCGStab: r, rh, p, v, s, t, w
     double* part = nullptr;                           // 2 regions x 2 slots x nblk
     CgState* st = nullptr;                            // device
     CgState* st_host = nullptr;                       // pinned mirror

@@ -330,7 +330,9 @@ int arpack_hip_dshift_create(arpack_hip_dshift** S, const arpack_hip_csr* A, dou
 void arpack_hip_dshift_destroy(arpack_hip_dshift* S);
 /* 0: conjugate gradients (the default; A - sigma I positive definite), 1: MINRES
  * (any symmetric A - sigma I, e.g. sigma inside the spectrum for interior
- * eigenvalues; 16 instead of 11 vector passes an iteration).  0 or -1. */
+ * eigenvalues; 16 instead of 11 vector passes an iteration), 2: BiCGStab (a
+ * nonsymmetric A: dnaupd's real shift-invert; two products an iteration).
+ * 0 or -1. */
 int arpack_hip_dshift_set_method(arpack_hip_dshift* S, int method);
 /* x, y device pointers (y != x); synchronous.  The iterations (>= 0; *relres =
  * ||r||/||x||), -1 on breakdown / missed rtol, -2 on a HIP error. */
@@ -346,6 +348,12 @@ int arpack_hip_dshift_stats(const arpack_hip_dshift* S, long long* solves, long 
  * then gives the eigenvalues of A).  A failed solve ends the run with
  * info = -9999. */
 void arpack_hip_dsaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, int n,
+                             char const* which, int nev, double* tol, double* resid, int ncv,
+                             double* v, int ldv, int* iparam, int* ipntr, double* workd,
+                             double* workl, int lworkl, int* info);
+/* dnaupd in mode 3 with a real shift (iparam[6] = 3, bmat = 'I'; S set to
+ * BiCGStab, method 2); dneupd_c with sigmar = sigma, sigmai = 0 afterwards. */
+void arpack_hip_dnaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, int n,
                              char const* which, int nev, double* tol, double* resid, int ncv,
                              double* v, int ldv, int* iparam, int* ipntr, double* workd,
                              double* workl, int lworkl, int* info);

@@ -155,3 +155,47 @@ def test_eigsh_interior_eigenvalues_minres(pkg):
     for k in range(4):
         r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
         assert r <= 1e-9 * 8.0 * np.linalg.norm(z[:, k])
+
+
+def test_dnaupd_mode3_bicgstab_unreachable_fails_loudly(pkg, golden):
+    """dndrv2's operator (the m7 fixture: 1-D convection-diffusion n = 400,
+    sigma = 1) is strongly non-normal: BiCGStab takes ~3,500 iterations to
+    1e-10 and stagnates near 2e-11 (measured), where the reference factors the
+    tridiagonal A - sigma I directly (dgttrf/dgttrs).  A device solve that
+    cannot reach its rtol is never passed on as OP: the mode-3 run ends with
+    info = -9999 instead of returning eigenvalues of a perturbed operator."""
+    g = golden("m7_ns_std_si")
+    n, sigma = int(g["n"]), float(g["sigma"])
+    c = modes.StdShiftInvert(str(g["kind"]), n, sigma)
+    Acsr = c.A.tocsr()
+    A = pkg.CSR.from_arrays(Acsr.indptr, Acsr.indices, Acsr.data)
+    S = pkg.DShift(A, sigma, rtol=1e-12, maxit=500, method="bicgstab")
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
+                  mxiter=300, v0=g["v0"])
+    assert s.aupd_shift(S) == 99
+    assert int(s.info[0]) == -9999
+    assert S.stats()["failures"] == 1
+
+
+def test_eigs_real_shift_invert(pkg):
+    """eigs(CSR, sigma=...) -- dnaupd mode 3, device BiCGStab -- on dndrv1's 2-D
+    convection-diffusion operator against SciPy's eigs(sigma=...): the
+    eigenvalues nearest a shift where A - sigma I is well conditioned (the
+    Krylov solve's domain; see the m7 test above for one where it is not)."""
+    m, rho = 30, 10.0
+    A = pkg.CSR.convdiff2d(m, rho)
+    As = M.to_scipy(*M.convdiff2d(m, rho))
+    n = m * m
+    sigma = -100.0  # left of the spectrum (real parts ~20..3,800): A - sigma I well conditioned
+    v0 = np.random.default_rng(12).uniform(-1, 1, n)
+    d, z, res = pkg.eigs(A, n, nev=6, ncv=20, which="LM", tol=1e-12, v0=v0, sigma=sigma,
+                         maxit=5000)
+    assert res["info"] == 0 and res["nconv"] >= 6
+    dref = spl.eigs(As.tocsc(), k=6, ncv=20, sigma=sigma, which="LM", tol=1e-12, v0=v0,
+                    return_eigenvectors=False)
+    for x in dref:
+        assert np.abs(d - x).min() <= 1e-9 * np.abs(dref).max(), (x, d)
+    an = abs(As).sum(axis=0).max()
+    for k in range(len(d)):
+        r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
+        assert r <= 1e-9 * an * np.linalg.norm(z[:, k])
