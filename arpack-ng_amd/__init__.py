@@ -836,7 +836,10 @@ def eigsh(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec
     nearest sigma returned (dseupd's transform).
     Returns (d, Z, info-dict)."""
     ncv = ncv or min(n, max(2 * nev + 1, 20))
-    shift = sigma is not None and isinstance(op, CSR)
+    if sigma is not None and not isinstance(op, CSR):
+        raise ValueError("sigma needs a CSR operator (the device solve); with a callable, "
+                         "drive SymRci(mode=3) and apply (A - sigma I)^{-1} yourself")
+    shift = sigma is not None
     s = SymRci(n, nev, ncv, which, tol, mode=3 if shift else 1, mxiter=mxiter, v0=v0,
                device=device)
     if shift:
@@ -921,7 +924,10 @@ def eigs(op, n, nev=6, ncv=None, which="LM", tol=0.0, v0=None, mxiter=300, rvec=
                    nopx=int(s.iparam[8]))
         d, z, nconv = s.eupd(rvec=rvec, sigma=0j if sigma is None else complex(sigma))
         return d, (z if rvec else None), res
-    shift = sigma is not None and isinstance(op, CSR)
+    if sigma is not None and not isinstance(op, CSR):
+        raise ValueError("sigma needs a CSR or ZCSR operator (the device solve); with a "
+                         "callable, drive NsRci(mode=3) and apply (A - sigma I)^{-1} yourself")
+    shift = sigma is not None
     s = NsRci(n, nev, ncv, which, tol, mode=3 if shift else 1, mxiter=mxiter, v0=v0)
     if shift:  # real shift-invert: OP = (A - sigma I)^{-1} by the device BiCGStab
         S = DShift(op, float(sigma), rtol=rtol, maxit=maxit, method="bicgstab")
