@@ -293,6 +293,7 @@ void arpack_hip_znaupd_zcsr(const arpack_hip_zcsr* A, int* ido, char const* bmat
  * drivers do with a banded LU (EXAMPLES/COMPLEX/zndrv2.f:179,250 zgttrf/zgttrs).
  * Stops when ||r|| <= rtol ||x|| (r the recursively updated residual) or after
  * maxit iterations.  A solve object serves one stream at a time. */
+/* S keeps a reference to A: A must outlive S. */
 typedef struct arpack_hip_zshift arpack_hip_zshift;
 int arpack_hip_zshift_create(arpack_hip_zshift** S, const arpack_hip_zcsr* A, double sigma_re,
                              double sigma_im, double rtol, int maxit);
@@ -324,6 +325,8 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, 
  * positive definite (sigma below the spectrum of A, the usual smallest-
  * eigenvalue use); an indefinite shift makes CG break down, which is reported
  * as a failed solve.  Returns as arpack_hip_zshift_*. */
+/* S keeps a reference to A: A must outlive S (and must not be changed --
+ * e.g. arpack_hip_csr_set_symmetric -- while S serves a solve). */
 typedef struct arpack_hip_dshift arpack_hip_dshift;
 int arpack_hip_dshift_create(arpack_hip_dshift** S, const arpack_hip_csr* A, double sigma,
                              double rtol, int maxit);
