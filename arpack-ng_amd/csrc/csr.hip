@@ -239,7 +239,16 @@ int build_generated(int64_t rows, Count count, Fill fill, int64_t** rp_out, int3
 // LDS x-window tables, then the SELL-64 layout over them (default kernel);
 // matrices whose rows span more than a window keep the CSR-stream kernel.
 void analyse_window_sell(arpack_hip_csr* A, int64_t ncols) {
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) != 0) return;
+    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) != 0) {
+        // rows spanning several distant column bands (a 3-D stencil in natural
+        // order): multi-range windows, read by the SELL kernel only
+        if (ahip::dev::csr_analyse_ranges(A->A, ncols, &A->win) != 0) return;
+        if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
+            A->A.kernel = ahip::dev::kCsrSell;
+            A->A.s_unroll = 10;
+        }
+        return;
+    }
     A->A.kernel = ahip::dev::kCsrWVecX;
     if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
         A->A.kernel = ahip::dev::kCsrSell;
@@ -382,7 +391,7 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
         return 0;
     }
     if (kernel >= ahip::dev::kCsrWindow && kernel <= ahip::dev::kCsrWVecP4) {
-        if (!A->win) return -1;
+        if (!A->win || A->A.w_rng) return -1;  // multi-range windows: SELL only
         A->A.kernel = kernel;
         return 0;
     }
@@ -548,6 +557,7 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     A->sell = nullptr;
     A->A.s_val = nullptr;
     A->A.w_nsb = 0;
+    A->A.w_rng = nullptr;  // (inside the freed window allocation)
     A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;
     analyse_window_sell(A, ncols);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -212,6 +212,12 @@ struct Csr {
     const int32_t* w_sb_span = nullptr;   // window length
     int64_t w_nsb = 0;
     const uint16_t* w_colw = nullptr;     // col - c0(superblock), 16 bit (owned separately)
+    // multi-range windows (csr_analyse_ranges, operators whose rows span several
+    // distant column bands, e.g. a 3-D stencil in natural order): per superblock
+    // kMaxRanges x ranges staged back to back in LDS -- rng[8 sb + r] = first
+    // column of range r, rng[8 sb + 4 + r] = LDS offset << 32 | length (0: unused);
+    // w_colw is then the LDS slot.  nullptr: one range [c0, c0 + span).
+    const int64_t* w_rng = nullptr;
     // SELL-64 slices inside each window superblock (kCsrSell, csr_build_sell):
     // the superblock's rows sorted by length, 64 per slice (one per lane),
     // entries stored column-step-major so a wave reads 64 consecutive values
@@ -283,6 +289,11 @@ int csr_build_sell(Csr& A, void** owned);
 // span exceeds the window (then the stream kernel is used).  *owned receives
 // the single device allocation holding the tables.
 int csr_analyse_window(Csr& A, int64_t ncols, void** owned);
+// The same tables for rows that span more than one window but whose columns fall
+// in at most kMaxRanges bands (w_rng); -1 if the operator does not fit, -2 on a
+// HIP error.  Only the SELL kernel (kCsrSell) reads such windows.
+constexpr int kMaxRanges = 4;
+int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned);
 // Build the CSR-stream row blocks (host-side greedy pass over rowptr, once per
 // matrix, like a sparse-library "analysis" step).  Returns 0, or -1 if a row
 // is longer than the tile (the matrix then keeps the vector kernel).

@@ -368,12 +368,13 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvecp(
 // whole slices (lane = row); a column step is one coalesced 512-B val load and
 // one 128-B colw load per wave.  Each row is summed sequentially in its CSR
 // (column) order.
-template <int U, bool XCD, bool NTL = false>
+template <int U, bool XCD, bool NTL = false, bool MR = false>
 __global__ __launch_bounds__(kWinThreads) void k_csr_sell(
     const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
     const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
     const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
-    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y) {
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
+    const int64_t* __restrict__ rng) {
     // unfused multiply-add: each row is summed exactly as a sequential CSR loop
     // (y_i = ((0 + a_i1 x_1) + a_i2 x_2) + ...) -- SciPy's csr_matvec, the OP
     // the reference's RCI callers use -- so y is bitwise the CPU result
@@ -410,7 +411,16 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_sell(
         w = (int)((sptr[s + 1] - base) >> 6);
         load(cur, base, w, 0);
     }
-    for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    if constexpr (MR) {  // the superblock's column bands, back to back in LDS
+#pragma unroll
+        for (int r = 0; r < kMaxRanges; ++r) {
+            const int64_t a = rng[8 * sb + r], ol = rng[8 * sb + 4 + r];
+            const int off = (int)(ol >> 32), len = (int)(ol & 0xffffffff);
+            for (int i = t; i < len; i += kWinThreads) xw[off + i] = x[a + i];
+        }
+    } else {
+        for (int i = t; i < span; i += kWinThreads) xw[i] = x[c0 + i];
+    }
     __syncthreads();
     for (; s < s1; s += NW) {
         const int row = srow[s * 64 + lane];
@@ -564,7 +574,189 @@ __global__ void k_row_span(int64_t n, const int64_t* __restrict__ rp, const int3
     }
 }
 
+// per row up to kMaxRanges column bands: sorted columns split where two
+// consecutive ones are more than kBandGap apart; cnt = -1 if the row's columns
+// are unsorted or form more bands
+constexpr int kBandGap = 1024;
+__global__ void k_row_bands(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                            int32_t* __restrict__ lo, int32_t* __restrict__ hi, int8_t* __restrict__ cnt) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int c = 0;
+        int32_t prev = 0;
+        bool ok = true;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            const int32_t j = col[k];
+            if (c == 0 || j > prev + kBandGap) {
+                if (c == kMaxRanges || (c > 0 && j < prev)) {
+                    ok = false;
+                    break;
+                }
+                lo[i * kMaxRanges + c] = j;
+                ++c;
+            } else if (j < prev) {
+                ok = false;
+                break;
+            }
+            hi[i * kMaxRanges + c - 1] = j;
+            prev = j;
+        }
+        cnt[i] = ok ? (int8_t)c : (int8_t)-1;
+    }
+}
+
+// 16-bit LDS slot of every nonzero of superblock blockIdx.x (range lookup)
+__global__ void k_colw_ranges(const int64_t* __restrict__ sb_tile0, const int64_t* __restrict__ tiles,
+                              const int64_t* __restrict__ rng, const int64_t* __restrict__ rp,
+                              const int32_t* __restrict__ col, uint16_t* __restrict__ colw) {
+    const int64_t sb = blockIdx.x;
+    const int64_t k0 = rp[tiles[sb_tile0[sb]]], k1 = rp[tiles[sb_tile0[sb + 1]]];
+    int64_t a[kMaxRanges];
+    int off[kMaxRanges], len[kMaxRanges];
+#pragma unroll
+    for (int r = 0; r < kMaxRanges; ++r) {
+        a[r] = rng[8 * sb + r];
+        off[r] = (int)(rng[8 * sb + 4 + r] >> 32);
+        len[r] = (int)(rng[8 * sb + 4 + r] & 0xffffffff);
+    }
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
+        const int64_t c = col[k];
+        int slot = 0;
+#pragma unroll
+        for (int r = 0; r < kMaxRanges; ++r)
+            if (c >= a[r] && c < a[r] + len[r]) slot = off[r] + (int)(c - a[r]);
+        colw[k] = (uint16_t)slot;
+    }
+}
+
 }  // namespace
+
+int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
+    const int64_t n = A.n;
+    if (n <= 0 || A.nnz <= 0) return -1;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> lo((size_t)n * kMaxRanges), hi((size_t)n * kMaxRanges);
+    std::vector<int8_t> cnt(n);
+    int32_t *dlo = nullptr, *dhi = nullptr;
+    int8_t* dcnt = nullptr;
+    auto cleanup = [&]() {
+        for (void* q : {(void*)dlo, (void*)dhi, (void*)dcnt})
+            if (q) (void)hipFree(q);
+    };
+    const size_t bb = sizeof(int32_t) * (size_t)n * kMaxRanges;
+    if (hipMalloc(&dlo, bb) || hipMalloc(&dhi, bb) || hipMalloc(&dcnt, (size_t)n)) {
+        cleanup();
+        return -2;
+    }
+    int64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    AHIP_LAUNCH(k_row_bands, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dlo, dhi, dcnt);
+    const bool ok = hipMemcpy(lo.data(), dlo, bb, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(hi.data(), dhi, bb, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(cnt.data(), dcnt, (size_t)n, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost) ==
+                        hipSuccess;
+    cleanup();
+    if (!ok) return -2;
+    // greedy superblocks: the union of their rows' bands, merged when they
+    // overlap or touch (gap <= kBandGap), must stay within kMaxRanges bands of
+    // kWinX columns in total; tiles (<= kWinTile nonzeros) as in csr_analyse_window
+    struct Band {
+        int64_t a, b;  // [a, b]
+    };
+    std::vector<Band> cur, nxt;
+    auto merge_into = [](std::vector<Band>& S, const Band& x) {
+        S.push_back(x);
+        std::sort(S.begin(), S.end(), [](const Band& p, const Band& q) { return p.a < q.a; });
+        std::vector<Band> m;
+        for (const Band& q : S) {
+            if (!m.empty() && q.a <= m.back().b + kBandGap) m.back().b = std::max(m.back().b, q.b);
+            else m.push_back(q);
+        }
+        S.swap(m);
+    };
+    auto fits = [](const std::vector<Band>& S) {
+        int64_t len = 0;
+        for (const Band& q : S) len += q.b - q.a + 1;
+        return (int)S.size() <= kMaxRanges && len <= kWinX;
+    };
+    std::vector<int64_t> tiles{0}, sb_tile0{0}, sb_c0, rng;
+    std::vector<int32_t> sb_span;
+    auto close_sb = [&]() {
+        int64_t off = 0, a0 = cur.empty() ? 0 : cur[0].a;
+        for (int r = 0; r < kMaxRanges; ++r) rng.push_back(r < (int)cur.size() ? cur[r].a : 0);
+        for (int r = 0; r < kMaxRanges; ++r) {
+            const int64_t len = r < (int)cur.size() ? cur[r].b - cur[r].a + 1 : 0;
+            rng.push_back((off << 32) | len);
+            off += len;
+        }
+        sb_c0.push_back(a0);
+        sb_span.push_back((int32_t)off);
+        sb_tile0.push_back((int64_t)tiles.size() - 1);
+    };
+    int64_t sb_start = 0, tile_start = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (cnt[i] < 0 || rp[i + 1] - rp[i] > kWinTile) return -1;
+        nxt = cur;
+        for (int c = 0; c < cnt[i]; ++c)
+            merge_into(nxt, Band{lo[(size_t)i * kMaxRanges + c], hi[(size_t)i * kMaxRanges + c]});
+        if (!fits(nxt)) {
+            if (i == sb_start) return -1;  // the row alone does not fit
+            tiles.push_back(i);
+            close_sb();
+            sb_start = tile_start = i;
+            cur.clear();
+            for (int c = 0; c < cnt[i]; ++c)
+                merge_into(cur, Band{lo[(size_t)i * kMaxRanges + c], hi[(size_t)i * kMaxRanges + c]});
+            if (!fits(cur)) return -1;
+            continue;
+        }
+        cur.swap(nxt);
+        if (i > tile_start && rp[i + 1] - rp[tile_start] > kWinTile) {
+            tiles.push_back(i);
+            tile_start = i;
+        }
+    }
+    tiles.push_back(n);
+    close_sb();
+    const int64_t nsb = (int64_t)sb_c0.size();
+    const size_t b_tiles = sizeof(int64_t) * tiles.size(), b_t0 = sizeof(int64_t) * sb_tile0.size(),
+                 b_c0 = sizeof(int64_t) * nsb, b_sp = sizeof(int32_t) * nsb,
+                 b_rng = sizeof(int64_t) * rng.size();
+    char* d = nullptr;
+    if (hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_rng + b_sp)) return -2;
+    bool cp = hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d + b_tiles + b_t0 + b_c0, rng.data(), b_rng, hipMemcpyHostToDevice) ==
+                  hipSuccess &&
+              hipMemcpy(d + b_tiles + b_t0 + b_c0 + b_rng, sb_span.data(), b_sp, hipMemcpyHostToDevice) ==
+                  hipSuccess;
+    uint16_t* cw = nullptr;
+    if (cp && hipMalloc(&cw, sizeof(uint16_t) * A.nnz) == hipSuccess) {
+        AHIP_LAUNCH(k_colw_ranges, dim3((unsigned)nsb), dim3(256), 0, nullptr,
+                    (const int64_t*)(d + b_tiles), (const int64_t*)d,
+                    (const int64_t*)(d + b_tiles + b_t0 + b_c0), A.rowptr, A.col, cw);
+        cp = hipDeviceSynchronize() == hipSuccess;
+    } else {
+        cp = false;
+    }
+    if (!cp) {
+        if (cw) (void)hipFree(cw);
+        (void)hipFree(d);
+        return -2;
+    }
+    A.w_tiles = (const int64_t*)d;
+    A.w_sb_tile0 = (const int64_t*)(d + b_tiles);
+    A.w_sb_c0 = (const int64_t*)(d + b_tiles + b_t0);
+    A.w_rng = (const int64_t*)(d + b_tiles + b_t0 + b_c0);
+    A.w_sb_span = (const int32_t*)(d + b_tiles + b_t0 + b_c0 + b_rng);
+    A.w_nsb = nsb;
+    A.w_colw = cw;
+    *owned = d;
+    (void)ncols;
+    return 0;
+}
 
 int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     const int64_t n = A.n;
@@ -786,12 +978,27 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
     }
     if (A.kernel == kCsrSell && A.s_val) {
         const size_t lds = sizeof(double) * kWinX;
-        auto go = [&](auto kern) {
+        auto go = [&](auto kern) {  // k_csr_sell (one window range: no range table)
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            AHIP_LAUNCH(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
+                               A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y,
+                               (const int64_t*)nullptr);
+        };
+        auto go2 = [&](auto kern) {  // k_csr_sell2
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             AHIP_LAUNCH(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
                                A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y);
         };
+        if (A.w_rng) {  // multi-range windows: only this form stages them
+            (void)hipFuncSetAttribute((const void*)k_csr_sell<4, true, true, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            AHIP_LAUNCH((k_csr_sell<4, true, true, true>), dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s,
+                        A.s_sb_slice0, A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y,
+                        A.w_rng);
+            return;
+        }
         if (A.s_unroll == 4) go(k_csr_sell<4, true>);
         else if (A.s_unroll == 9) go(k_csr_sell<8, true, true>);   // non-temporal val/col
         else if (A.s_unroll == 10) go(k_csr_sell<4, true, true>);
@@ -799,8 +1006,8 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
         else if (A.s_unroll == 2) go(k_csr_sell<2, true>);
         else if (A.s_unroll == 3) go(k_csr_sell<3, true>);
         else if (A.s_unroll == 6) go(k_csr_sell<6, true>);
-        else if (A.s_unroll == 5) go(k_csr_sell2<4, true>);  // two slices per wave
-        else if (A.s_unroll == 7) go(k_csr_sell2<2, true>);
+        else if (A.s_unroll == 5) go2(k_csr_sell2<4, true>);  // two slices per wave
+        else if (A.s_unroll == 7) go2(k_csr_sell2<2, true>);
         else go(k_csr_sell<8, true>);
         return;
     }

@@ -32,6 +32,25 @@ from bench import load_pkg  # noqa: E402
 W, K = 2, 10
 
 
+PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md), as bench.py
+
+
+def roofline(prof):
+    """Per-kernel-class GB/s of algorithmic bytes (kernel-mode hipEvents, as
+    bench.py's roofline) and the SpMV's and SpMV + Gram-Schmidt's fraction of peak."""
+    out = {k: dict(ms=v[0], launches=v[2], gbs=(v[1] / (v[0] * 1e-3) / 1e9) if v[0] > 0 else None)
+           for k, v in prof.items() if v[2]}
+    sp = prof.get("spmv", (0.0, 0.0, 0))
+    # as bench.py: the finalize launches' time counts, their partial-sum bytes do not
+    ms = sp[0] + sum(prof[k][0] for k in ("cgs_dots", "update", "place", "finalize"))
+    by = sp[1] + sum(prof[k][1] for k in ("cgs_dots", "update", "place"))
+    spmv_gbs = sp[1] / (sp[0] * 1e-3) / 1e9 if sp[0] > 0 else None
+    step_gbs = by / (ms * 1e-3) / 1e9 if ms > 0 else None
+    return dict(kernels=out, spmv_gbs=spmv_gbs, spmv_frac=spmv_gbs / PEAK_GBS if spmv_gbs else None,
+                spmv_plus_orth_gbs=step_gbs,
+                spmv_plus_orth_frac=step_gbs / PEAK_GBS if step_gbs else None, peak_gbs=PEAK_GBS)
+
+
 def timed(pkg, s, A, ns=False):
     for k in (0, W):
         ido = s.aupd_cycles(A, k)
@@ -44,8 +63,15 @@ def timed(pkg, s, A, ns=False):
     pkg.synchronize()
     el = time.perf_counter() - t
     nc = K if ido == 98 else int(s.iparam[2]) - W
-    return dict(iters_per_s=nc / el, ms_per_cycle=1e3 * el / nc, cycles=nc,
-                lanczos_steps_per_s=(pkg.stats()["nopx"] - it0) / el)
+    rec = dict(iters_per_s=nc / el, ms_per_cycle=1e3 * el / nc, cycles=nc,
+               lanczos_steps_per_s=(pkg.stats()["nopx"] - it0) / el)
+    if ido == 98:  # the next cycles with per-kernel events (out of the timed region)
+        pkg.profile(True)
+        pkg.profile_read()
+        if s.aupd_cycles(A, min(K, 5)) in (98, 99):
+            rec["roofline"] = roofline(pkg.profile_read())
+        pkg.profile(False)
+    return rec
 
 
 def main():
