@@ -574,6 +574,22 @@ __global__ void k_row_span(int64_t n, const int64_t* __restrict__ rp, const int3
     }
 }
 
+// Superblock height cap: at least two workgroups per CU (the SELL kernel's
+// 80 KB x window lets two share a CU's LDS).  Without it a wide-band operator
+// of ~10^6 rows (a 2-D stencil with m = 1000: 8,240 rows per 10,240-column
+// window) gives ~120 superblocks -- half the CUs idle.  Capped superblocks
+// stage more x (R + band per R rows) but fill the chip.
+int64_t sb_row_cap(int64_t n) {
+    static const int ncu = [] {
+        int v = 0;
+        return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && v > 0
+                   ? v
+                   : 256;
+    }();
+    const int64_t cap = (n + 2 * (int64_t)ncu - 1) / (2 * (int64_t)ncu);
+    return cap < 1024 ? 1024 : cap;
+}
+
 // per row up to kMaxRanges column bands: sorted columns split where two
 // consecutive ones are more than kBandGap apart; cnt = -1 if the row's columns
 // are unsorted or form more bands
@@ -695,12 +711,13 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
         sb_tile0.push_back((int64_t)tiles.size() - 1);
     };
     int64_t sb_start = 0, tile_start = 0;
+    const int64_t rcap = sb_row_cap(n);
     for (int64_t i = 0; i < n; ++i) {
         if (cnt[i] < 0 || rp[i + 1] - rp[i] > kWinTile) return -1;
         nxt = cur;
         for (int c = 0; c < cnt[i]; ++c)
             merge_into(nxt, Band{lo[(size_t)i * kMaxRanges + c], hi[(size_t)i * kMaxRanges + c]});
-        if (!fits(nxt)) {
+        if (!fits(nxt) || i - sb_start >= rcap) {
             if (i == sb_start) return -1;  // the row alone does not fit
             tiles.push_back(i);
             close_sb();
@@ -777,6 +794,7 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     std::vector<int32_t> sb_span;
     int64_t sb_start = 0, tile_start = 0;
     int64_t lo = INT64_MAX, hi = -1;
+    const int64_t rcap = sb_row_cap(n);
     auto close_sb = [&](int64_t end_row) {
         if (lo > hi) { lo = 0; hi = 0; }
         sb_c0.push_back(lo);
@@ -793,7 +811,7 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
             nhi = std::max<int64_t>(hi, mx[i]);
             if (mx[i] - mn[i] + 1 > kWinX) return -1;
         }
-        if (i > sb_start && nhi >= nlo && nhi - nlo + 1 > kWinX) {
+        if (i > sb_start && ((nhi >= nlo && nhi - nlo + 1 > kWinX) || i - sb_start >= rcap)) {
             // close tile and superblock before row i
             tiles.push_back(i);
             close_sb(i);
