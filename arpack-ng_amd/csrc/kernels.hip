@@ -987,6 +987,12 @@ void vq_update(const Workspace& ws, int64_t n, R* V, int64_t ld, int kplusp, int
                       : nts ? go(k_vq_update<R, 16, kPolNt, true>) : go(k_vq_update<R, 16>);
     else if (kplusp <= 32) ws.v_plain ? go(k_vq_update<R, 32, kPolPlain>)
                            : nts ? go(k_vq_update<R, 32, kPolNt, true>) : go(k_vq_update<R, 32>);
+    // 40 / 48: the ncv = 40 of configs 3 and 5 in 127 VGPRs (four waves a
+    // SIMD) where MAXK = 64 takes 211 (two)
+    else if (kplusp <= 40) ws.v_plain ? go(k_vq_update<R, 40, kPolPlain>)
+                           : nts ? go(k_vq_update<R, 40, kPolNt, true>) : go(k_vq_update<R, 40>);
+    else if (kplusp <= 48) ws.v_plain ? go(k_vq_update<R, 48, kPolPlain>)
+                           : nts ? go(k_vq_update<R, 48, kPolNt, true>) : go(k_vq_update<R, 48>);
     else if (kplusp <= 64) ws.v_plain ? go(k_vq_update<R, 64, kPolPlain>)
                            : nts ? go(k_vq_update<R, 64, kPolNt, true>) : go(k_vq_update<R, 64>);
     else  // ws.scratch: nblk * kBlock * (ncv + 1) doubles, allocated by ws_create for ncv > 64

@@ -347,6 +347,9 @@ void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
     else if (k <= 32)
         hipLaunchKernelGGL((k_zgemm<R, 32>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
                            Z2, ldz);
+    else if (k <= 40)  // ncv = 40 (config 5): 40 row values in registers, not 64
+        hipLaunchKernelGGL((k_zgemm<R, 40>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
+                           Z2, ldz);
     else if (k <= 64)
         hipLaunchKernelGGL((k_zgemm<R, 64>), dim3(grid(n)), dim3(kB), 0, ws.stream, n, V2, ld, k, nz, M2,
                            Z2, ldz);
