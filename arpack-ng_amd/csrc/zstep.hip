@@ -21,6 +21,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdint>
+#include <cstdlib>
 
 #include "zcommon.hpp"
 #include "zengine.hpp"
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(kB) void k_zs_update(int64_t n, const typename C2<R
     }
 }
 
-// generic width (j > 32): rout = rin - V c, no fused partials
+// generic width (j > 40): rout = rin - V c, no fused partials
 template <class R>
 __global__ __launch_bounds__(kB) void k_zs_update_generic(int64_t n, int j,
                                                           const typename C2<R>::T* __restrict__ V,
@@ -353,6 +354,7 @@ void step_place(const Ws& ws, int64_t n, const R* r, R* vcol, R* copy1, R* copy2
     M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
 #define AHIP_ZS_C32(M) \
     M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
+#define AHIP_ZS_C40(M) M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40)
 
 template <class R>
 void step_dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, int gate) {
@@ -385,6 +387,14 @@ void step_dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* 
     }
 }
 
+// widest fused update; AHIP_ZFUSE_MAX=32 restores the round-2 split above 32
+// columns (read per call: a test compares both forms in one process)
+static int fused_max() {
+    const char* e = getenv("AHIP_ZFUSE_MAX");
+    const int v = e ? atoi(e) : 40;
+    return v >= 1 && v <= 40 ? v : 40;
+}
+
 template <class R>
 void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
                  R* rout, bool spec, int gate) {
@@ -394,7 +404,11 @@ void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int whi
     const T* ri = reinterpret_cast<const T*>(rin);
     T* ro = reinterpret_cast<T*>(rout);
     const dim3 g(sgrid(ws)), b(kB);
-    if (j >= 1 && j <= 32) {
+    // up to 40 columns (config 5's ncv) the update and the next sweep's partials
+    // share one pass: the row's V entries stay in registers (J = 40: 256 VGPRs +
+    // 82 AGPRs, no scratch); the sums are those of step_dots over rout, term for
+    // term, so the partials are the same either way
+    if (j >= 1 && j <= fused_max()) {
         switch (j) {
 #define AHIP_ZS_UPD(J)                                                                             \
     case J:                                                                                        \
@@ -407,6 +421,7 @@ void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int whi
         break;
             AHIP_ZS_C16(AHIP_ZS_UPD)
             AHIP_ZS_C32(AHIP_ZS_UPD)
+            AHIP_ZS_C40(AHIP_ZS_UPD)
 #undef AHIP_ZS_UPD
             default: break;
         }
