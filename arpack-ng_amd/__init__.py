@@ -399,10 +399,16 @@ class SymRci:
         self.iparam[6] = mode
         self.lworkl = ncv * ncv + 8 * ncv
         self.workl = np.zeros(self.lworkl, self.dt)
-        self.ldv = n
+        # device V: columns padded to 128-B lines (ldv >= n, as ARPACK allows);
+        # a column start off a line costs the Gram-Schmidt and V*Q passes 8-12%
+        # (profiles/r03am_summary.txt: n = 10^7 - 1 against 10^7)
+        # (ARPACK_HIP_LDV_PAD=0: ldv = n, for a same-box A/B)
+        al = 128 // np.dtype(self.dt).itemsize
+        pad = device and os.environ.get("ARPACK_HIP_LDV_PAD", "1") != "0"
+        self.ldv = -(-n // al) * al if pad else n
         if device:
             self.resid = DeviceBuffer(n, self.dt)
-            self.v = DeviceBuffer(ncv * n, self.dt)
+            self.v = DeviceBuffer(ncv * self.ldv, self.dt)
             self.workd = DeviceBuffer(3 * n, self.dt)
             if v0 is not None:
                 self.resid.write(np.asarray(v0, self.dt))
@@ -490,7 +496,8 @@ class SymRci:
         info = np.zeros(1, np.int32)
         f = (getattr(lib(), self.prec + "seupd_c") if dist is None
              else partial(lib().arpack_hip_pdseupd_c, dist.h))
-        f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z), self.n, sigma,
+        ldz = self.ldv if z is self.v else self.n  # Z = V (the reference's drivers)
+        f(1 if rvec else 0, howmny.encode(), _ip(select), d.ctypes.data, _ptr(z), ldz, sigma,
           self.bmat.encode(), self.n, self.which.encode(), self.nev, self.tol, _ptr(self.resid),
           self.ncv, _ptr(self.v), self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
           self.workl.ctypes.data, self.lworkl, _ip(info))
@@ -558,8 +565,9 @@ class NsRci(SymRci):
         info = np.zeros(1, np.int32)
         f = (getattr(lib(), self.prec + "neupd_c") if dist is None
              else partial(lib().arpack_hip_pdneupd_c, dist.h))
+        ldz = self.ldv if z is self.v else self.n  # Z = V (the reference's drivers)
         f(1 if rvec else 0, howmny.encode(), _ip(select), dr.ctypes.data, di.ctypes.data, _ptr(z),
-          self.n, sigmar, sigmai, workev.ctypes.data, self.bmat.encode(), self.n,
+          ldz, sigmar, sigmai, workev.ctypes.data, self.bmat.encode(), self.n,
           self.which.encode(), self.nev, self.tol, _ptr(self.resid), self.ncv, _ptr(self.v),
           self.ldv, _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd), self.workl.ctypes.data,
           self.lworkl, _ip(info))

@@ -52,7 +52,10 @@ int ArraysT<R>::attach(int64_t nn, int nc, R* resid, R* v, int ldv, R* workd) {
         own_stream = true;
     }
     if (host_mode) {
-        d_ld = (n + 1) & ~int64_t(1);
+        // columns start on 128-B lines: an odd n (config 4's 215^3) put every
+        // other column off a line and cost the V passes 8-12% (profiles/r03am)
+        constexpr int64_t al = 128 / (int64_t)sizeof(R);
+        d_ld = (n + al - 1) / al * al;
         if (hipMalloc(&d_v, sizeof(R) * (size_t)d_ld * ncv) != hipSuccess) return -2;
         if (hipMalloc(&d_resid, sizeof(R) * (size_t)n) != hipSuccess) return -2;
         if (hipMalloc(&d_workd, sizeof(R) * 3 * (size_t)n) != hipSuccess) return -2;
