@@ -90,6 +90,7 @@ def _declare(L):
     L.arpack_hip_gen_banded_sym.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64,
                                             C.c_int64, C.c_uint32, C.c_int, C.c_int]
     L.arpack_hip_set_stream.argtypes = [C.c_void_p]
+    L.arpack_hip_fault_inject.argtypes = [C.c_long]
     L.arpack_hip_malloc.argtypes = [C.c_size_t]
     L.arpack_hip_malloc.restype = C.c_void_p
     L.arpack_hip_free.argtypes = [C.c_void_p]
@@ -248,6 +249,12 @@ def profile_read():
     cnt = np.zeros(k, np.int64)
     lib().arpack_hip_profile_read(ms.ctypes.data, by.ctypes.data, cnt.ctypes.data, k)
     return {c: (float(ms[i]), float(by[i]), int(cnt[i])) for i, c in enumerate(PROF_CLASSES)}
+
+
+def fault_inject(k: int):
+    """Test hook: the k-th checked HIP call of the engine from now on reports
+    hipErrorInvalidValue (arpack_hip_fault_inject); 0 disarms."""
+    lib().arpack_hip_fault_inject(int(k))
 
 
 def synchronize():

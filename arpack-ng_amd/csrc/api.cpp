@@ -274,10 +274,12 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
     // a failed collective (RCCL / transport error) ends the solve with
     // info = -9999 at the next return to the caller: the ranks' sums no longer
     // agree.  Every rank's communicator reports the failure of a collective it
-    // took part in, so the ranks stop at the same return.
-    auto comm_broken = [&]() {
-        if (!S->dist || !comm_failed(S->dist->comm)) return false;
-        S->a.sync();
+    // took part in, so the ranks stop at the same return.  So does a failed HIP
+    // call of this solve (the sticky S->a.err: a copy, an enqueue, or a kernel
+    // fault surfacing at a sync).
+    auto broken = [&]() {
+        if (!S->a.err.bad() && (!S->dist || !comm_failed(S->dist->comm))) return false;
+        (void)hipStreamSynchronize(S->a.stream);
         *info = -9999;
         *ido = 99;
         g_sym.erase(v);
@@ -287,7 +289,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
-        if (r.ido != -1 && r.ido != 1 && comm_broken()) return;
+        if (r.ido != -1 && r.ido != 1 && broken()) return;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
             // it); a row-distributed SpMV also holds its halo exchange: marker mode
@@ -336,12 +338,12 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park
             // the caller may free or reuse its arrays before resuming: drain
             S->a.sync();
-            if (comm_broken()) return;
+            if (broken()) return;
             *ido = r.ido;
             return;
         }
         // hand the request to the caller
-        if ((r.ido == -1 || r.ido == 1) && comm_broken()) return;
+        if ((r.ido == -1 || r.ido == 1) && broken()) return;
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) {
             S->a.d2h_workd(r.x, n);
             if (r.ido == 1 && r.bx >= 0 && S->mode >= 3) S->a.d2h_workd(r.bx, n);
@@ -355,7 +357,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         return;
     }
     // ido = 99: dsaupd post-processing (SRC/dsaupd.f:613-627)
-    if (comm_broken()) return;
+    if (broken()) return;
     *ido = 99;
     iparam[2] = S->mxiter;
     iparam[4] = S->np;
@@ -367,6 +369,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
     *info = inf;
     S->a.download_all();
     S->a.sync();
+    if (S->a.err.bad()) *info = -9999;
     wl_out();
     g_sym.erase(v);
 }
@@ -610,6 +613,8 @@ int arpack_hip_dist_set_seed_mode(arpack_hip_dist* D, int mode) {
     const_cast<DistOp*>(ahip_dist_view(D))->seed_mode = mode;
     return 0;
 }
+
+void arpack_hip_fault_inject(long k) { fault_inject(k); }
 
 void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }
 

@@ -238,25 +238,33 @@ int build_generated(int64_t rows, Count count, Fill fill, int64_t** rp_out, int3
 
 // LDS x-window tables, then the SELL-64 layout over them (default kernel);
 // matrices whose rows span more than a window keep the CSR-stream kernel.
-void analyse_window_sell(arpack_hip_csr* A, int64_t ncols) {
-    if (ahip::dev::csr_analyse_window(A->A, ncols, &A->win) != 0) {
+// -2 if a HIP call of the analysis failed (-1 from a builder: the layout does
+// not fit this matrix, and the next form is tried).
+int analyse_window_sell(arpack_hip_csr* A, int64_t ncols) {
+    int rc = ahip::dev::csr_analyse_window(A->A, ncols, &A->win);
+    if (rc == -2) return -2;
+    if (rc != 0) {
         // rows spanning several distant column bands (a 3-D stencil in natural
         // order): multi-range windows, read by the SELL kernel only
-        if (ahip::dev::csr_analyse_ranges(A->A, ncols, &A->win) != 0) return;
-        if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
-            A->A.kernel = ahip::dev::kCsrSell;
-            A->A.s_unroll = 10;
-        }
-        return;
+        rc = ahip::dev::csr_analyse_ranges(A->A, ncols, &A->win);
+        if (rc != 0) return rc == -2 ? -2 : 0;
+    } else {
+        A->A.kernel = ahip::dev::kCsrWVecX;
     }
-    A->A.kernel = ahip::dev::kCsrWVecX;
-    if (ahip::dev::csr_build_sell(A->A, &A->sell) == 0) {
+    rc = ahip::dev::csr_build_sell(A->A, &A->sell);
+    if (rc == -2) return -2;
+    if (rc == 0) {
         A->A.kernel = ahip::dev::kCsrSell;
         A->A.s_unroll = 10;  // U = 4 with non-temporal val/col loads (tools/spmv_full_time.py)
     }
+    return 0;
 }
 
-arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, int32_t* col, double* val) {
+// The operator object over device arrays rp/col/val (ownership taken) and its
+// SpMV plans.  0, or -2 if a HIP call of the plan builders failed: then
+// everything, rp/col/val included, is released and *out is untouched.
+int finish(arpack_hip_csr** out, int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, int32_t* col,
+           double* val) {
     auto* A = new arpack_hip_csr;
     A->rowptr = rp;
     A->col = col;
@@ -268,9 +276,15 @@ arpack_hip_csr* finish(int64_t rows, int64_t ncols, int64_t nnz, int64_t* rp, in
     A->A.col = col;
     A->A.val = val;
     A->A.group = pick_group(rows, nnz);
-    if (ahip::dev::csr_analyse(A->A, 4096, &A->rblk) == 0) A->A.kernel = ahip::dev::kCsrStream;
-    analyse_window_sell(A, ncols);
-    return A;
+    int rc = ahip::dev::csr_analyse(A->A, 4096, &A->rblk);
+    if (rc == 0) A->A.kernel = ahip::dev::kCsrStream;
+    if (rc != -2) rc = analyse_window_sell(A, ncols);
+    if (rc == -2) {
+        arpack_hip_csr_destroy(A);
+        return -2;
+    }
+    *out = A;
+    return 0;
 }
 
 }  // namespace
@@ -295,8 +309,7 @@ int arpack_hip_csr_create(arpack_hip_csr** out, int64_t n, int64_t nnz, const in
         (void)hipFree(v);
         return -1;
     }
-    *out = finish(n, n, nnz, rp, c, v);
-    return 0;
+    return finish(out, n, n, nnz, rp, c, v);
 }
 
 void arpack_hip_csr_destroy(arpack_hip_csr* A) {
@@ -440,8 +453,7 @@ static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, doubl
         },
         &rp, &col, &val, &nnz);
     if (rc != 0) return rc;
-    *out = finish(n, n, nnz, rp, col, val);
-    return 0;
+    return finish(out, n, n, nnz, rp, col, val);
 }
 
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 2, scale); }
@@ -467,8 +479,7 @@ int arpack_hip_gen_convdiff2d(arpack_hip_csr** out, int64_t m, double rho) {
         },
         &rp, &col, &val, &nnz);
     if (rc != 0) return rc;
-    *out = finish(n, n, nnz, rp, col, val);
-    return 0;
+    return finish(out, n, n, nnz, rp, col, val);
 }
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 3, scale); }
 int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed) {
@@ -494,7 +505,7 @@ int arpack_hip_gen_banded_sym(arpack_hip_csr** out, int64_t n, int64_t r0, int64
         },
         &rp, &col, &val, &nnz);
     if (rc != 0) return rc;
-    *out = finish(rows, n, nnz, rp, col, val);
+    if (finish(out, rows, n, nnz, rp, col, val) != 0) return -2;
     (*out)->row_begin = r0;
     return 0;
 }

@@ -15,6 +15,28 @@
 
 #include <cstdint>
 
+namespace ahip {
+
+// Test hook (arpack_hip_fault_inject): the k-th checked HIP call from now on
+// reports hipErrorInvalidValue (the call itself was issued); 0 disarms.
+hipError_t fault_filter(hipError_t e);
+void fault_inject(long k);
+
+// Sticky device-error record of one solve: the first failed HIP call (an
+// enqueue, a copy, or a kernel fault surfacing at a stream sync) is kept, and
+// the driver turns it into info = -9999 at its next return to the caller
+// instead of running the restart loop on stale state.
+struct DevErr {
+    hipError_t e = hipSuccess;
+    void ck(hipError_t r) {
+        r = fault_filter(r);
+        if (r != hipSuccess && e == hipSuccess) e = r;
+    }
+    bool bad() const { return e != hipSuccess; }
+};
+
+}  // namespace ahip
+
 namespace ahip::dev {
 
 constexpr int kBlock = 256;

@@ -55,6 +55,8 @@ struct ArraysT {
     R* d_workd = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    DevErr err;  // first failed HIP call of this solve (sticky)
+    void ck(hipError_t e) { err.ck(e); }
 
     // fails with a negative code if pointer kinds are mixed
     int attach(int64_t n, int ncv, R* resid, R* v, int ldv, R* workd);

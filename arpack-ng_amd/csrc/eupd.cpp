@@ -101,10 +101,10 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
         }
     } guard{a, ws};
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
-                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream);
+        a.ck(hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
+                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream));
         a.upload_resid();
-        (void)hipMemcpyAsync(a.d_workd, workd, sizeof(R) * n, hipMemcpyHostToDevice, a.stream);
+        a.ck(hipMemcpyAsync(a.d_workd, workd, sizeof(R) * n, hipMemcpyHostToDevice, a.stream));
     }
     double bnorm2 = rnorm;
     if (bmat == 'G') {  // dnrm2(n, workd, 1); pdnorm2 over the ranks (pdseupd.f:456)
@@ -116,8 +116,9 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
         } else {
             dev::finalize(ws, 1, dev::kFinNorm, 0, 0, -1);
         }
-        (void)hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream);
+        a.ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
         a.sync();
+        if (a.err.bad()) return -9999;
         bnorm2 = ws.st_host->rnorm;
     }
 
@@ -198,7 +199,7 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
         for (int j = 0; j < nconv; ++j) M[(size_t)j * ncv + j] = 1.0;
         la::orm2r('L', 'N', ncv, nconv, nconv, workl + iq, ldq, workl + iw + ncv, M.data(), ncv,
                   work.data());
-        (void)hipMemcpyAsync(ws.q, M.data(), sizeof(double) * M.size(), hipMemcpyHostToDevice, a.stream);
+        a.ck(hipMemcpyAsync(ws.q, M.data(), sizeof(double) * M.size(), hipMemcpyHostToDevice, a.stream));
         dev::vq_gemm(ws, n, a.d_v, a.d_ld, ncv, nconv, a.d_v, a.d_ld);
         // last row of Q for the Ritz estimates (SRC/dseupd.f:752-765)
         for (int j = 0; j < ncv - 1; ++j) workl[ihb + j] = 0.0;
@@ -231,32 +232,32 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
         if (zdev) {
             zd = z;
             ldzd = ldz;
-            (void)hipMemcpy2DAsync(zd, sizeof(R) * ldz, a.d_v, sizeof(R) * a.d_ld,
-                                   sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
+            a.ck(hipMemcpy2DAsync(zd, sizeof(R) * ldz, a.d_v, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream));
         } else {
             if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess)
                 return -9999;
-            (void)hipMemcpyAsync(zd, a.d_v, sizeof(R) * (size_t)a.d_ld * nconv,
-                                 hipMemcpyDeviceToDevice, a.stream);
+            a.ck(hipMemcpyAsync(zd, a.d_v, sizeof(R) * (size_t)a.d_ld * nconv,
+                                 hipMemcpyDeviceToDevice, a.stream));
         }
         if (type != REGULR) {
-            (void)hipMemcpyAsync(ws.coef, workl + iw, sizeof(double) * nconv, hipMemcpyHostToDevice,
-                                 a.stream);
+            a.ck(hipMemcpyAsync(ws.coef, workl + iw, sizeof(double) * nconv, hipMemcpyHostToDevice,
+                                 a.stream));
             dev::ger_cols(a.stream, n, nconv, a.d_resid, ws.coef, zd, ldzd);
         }
         // V first, then Z: with Z = V (the reference's drivers pass v for z) the
         // purified Ritz vectors must be what V(:,1:nconv) holds on return
         if (a.host_mode)  // the reference leaves V * Q in V (dorm2r in place)
-            (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
-                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+            a.ck(hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream));
         if (!zdev) {
-            (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
-                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+            a.ck(hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
+                                   sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream));
             (void)hipFreeAsync(zd, a.stream);
         }
-        a.sync();
     }
-    return 0;
+    a.sync();  // a failed copy or a kernel fault of this call: -9999
+    return a.err.bad() ? -9999 : 0;
 }
 
 }  // namespace ahip

@@ -270,11 +270,11 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out
         }
     } guard{a, ws};
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
-                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream);
+        a.ck(hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(R) * ldv,
+                               sizeof(R) * n, ncv, hipMemcpyHostToDevice, a.stream));
         a.upload_resid();
     }
-    (void)hipMemcpyAsync(ws.q, Qh.data(), sizeof(double) * Qh.size(), hipMemcpyHostToDevice, a.stream);
+    a.ck(hipMemcpyAsync(ws.q, Qh.data(), sizeof(double) * Qh.size(), hipMemcpyHostToDevice, a.stream));
     dev::vq_gemm(ws, n, a.d_v, a.d_ld, ncv, ncv, a.d_v, a.d_ld);
     const bool zdev = is_device_pointer(z);
     R* zd = nullptr;
@@ -288,30 +288,30 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out
     }
     if (howmny == 'A') {
         a.sync();  // ws.q (Qh) consumed before it is overwritten
-        (void)hipMemcpyAsync(ws.q, M2.data(), sizeof(double) * M2.size(), hipMemcpyHostToDevice,
-                             a.stream);
+        a.ck(hipMemcpyAsync(ws.q, M2.data(), sizeof(double) * M2.size(), hipMemcpyHostToDevice,
+                             a.stream));
         dev::vq_gemm(ws, n, a.d_v, a.d_ld, nconv, nconv, zd, ldzd);
         if (type == SHIFTI) {
-            (void)hipMemcpyAsync(ws.coef, wpur.data(), sizeof(double) * nconv, hipMemcpyHostToDevice,
-                                 a.stream);
+            a.ck(hipMemcpyAsync(ws.coef, wpur.data(), sizeof(double) * nconv, hipMemcpyHostToDevice,
+                                 a.stream));
             dev::ger_cols(a.stream, n, nconv, a.d_resid, ws.coef, zd, ldzd);
         }
     } else if (zd != a.d_v) {  // 'P': Z = the Schur vectors
-        (void)hipMemcpy2DAsync(zd, sizeof(R) * ldzd, a.d_v, sizeof(R) * a.d_ld,
-                               sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream);
+        a.ck(hipMemcpy2DAsync(zd, sizeof(R) * ldzd, a.d_v, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream));
     }
     // V first, then Z: a caller may pass Z = V (the reference's drivers do),
     // and the reference then leaves the Ritz vectors in V(:,1:nconv)
     if (a.host_mode)  // the reference leaves V*Qh (the Schur basis) in V
-        (void)hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
-                               sizeof(R) * n, ncv, hipMemcpyDeviceToHost, a.stream);
+        a.ck(hipMemcpy2DAsync(v, sizeof(R) * ldv, a.d_v, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, ncv, hipMemcpyDeviceToHost, a.stream));
     if (!zdev) {
-        (void)hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
-                               sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream);
+        a.ck(hipMemcpy2DAsync(z, sizeof(R) * ldz, zd, sizeof(R) * a.d_ld,
+                               sizeof(R) * n, nconv, hipMemcpyDeviceToHost, a.stream));
         (void)hipFreeAsync(zd, a.stream);
     }
-    a.sync();
-    return 0;
+    a.sync();  // a failed copy or a kernel fault of this call: -9999
+    return a.err.bad() ? -9999 : 0;
 }
 
 }  // namespace ahip

@@ -36,6 +36,7 @@ Task SolverT<R>::run_ns() {
 
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
+    if (a.err.bad()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
@@ -45,6 +46,7 @@ Task SolverT<R>::run_ns() {
     write_state();
 
     co_await saitr(0, nev, sinfo);
+    if (a.err.bad()) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -58,6 +60,7 @@ Task SolverT<R>::run_ns() {
         ++iter;
         np = kplusp - nev;
         co_await saitr(nev, np, sinfo);
+        if (a.err.bad()) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -162,11 +165,16 @@ Task SolverT<R>::run_ns() {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
         read_state();
+        if (a.err.bad()) goto fault;
         rnorm = ws.st_host->rnorm;
     }
 done:
     mxiter = iter;
     nev0 = numcnv;
+    goto fail;
+fault:  // a failed HIP call: the device state is not trustworthy (see sym.cpp)
+    mxiter = iter;
+    info = -9999;
 fail:
     iparam[2] = mxiter;
     co_return;

@@ -5,7 +5,29 @@
 #include <thread>
 #include <vector>
 
+#include <atomic>
+#include <cstdlib>
+
 #include "device.hpp"
+
+namespace ahip {
+
+namespace {
+// countdown of the fault-injection hook; AHIP_FAULT_AT=k arms it at load
+std::atomic<long> g_fault_at{[] {
+    const char* e = getenv("AHIP_FAULT_AT");
+    return e ? atol(e) : 0L;
+}()};
+}  // namespace
+
+hipError_t fault_filter(hipError_t e) {
+    if (g_fault_at.load(std::memory_order_relaxed) <= 0) return e;
+    return g_fault_at.fetch_sub(1) == 1 ? hipErrorInvalidValue : e;
+}
+
+void fault_inject(long k) { g_fault_at.store(k > 0 ? k : 0); }
+
+}  // namespace ahip
 
 namespace ahip::dev {
 

@@ -25,6 +25,9 @@ namespace ahip::dev {
 
 namespace {
 
+// a plan-table HIP call succeeded (the fault-injection hook sees every one)
+inline bool hok(hipError_t e) { return fault_filter(e) == hipSuccess; }
+
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_csr_vector(int64_t n, const int64_t* __restrict__ rp,
                                                        const int32_t* __restrict__ col,
@@ -660,18 +663,17 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
             if (q) (void)hipFree(q);
     };
     const size_t bb = sizeof(int32_t) * (size_t)n * kMaxRanges;
-    if (hipMalloc(&dlo, bb) || hipMalloc(&dhi, bb) || hipMalloc(&dcnt, (size_t)n)) {
+    if (!hok(hipMalloc(&dlo, bb)) || !hok(hipMalloc(&dhi, bb)) || !hok(hipMalloc(&dcnt, (size_t)n))) {
         cleanup();
         return -2;
     }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     AHIP_LAUNCH(k_row_bands, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dlo, dhi, dcnt);
-    const bool ok = hipMemcpy(lo.data(), dlo, bb, hipMemcpyDeviceToHost) == hipSuccess &&
-                    hipMemcpy(hi.data(), dhi, bb, hipMemcpyDeviceToHost) == hipSuccess &&
-                    hipMemcpy(cnt.data(), dcnt, (size_t)n, hipMemcpyDeviceToHost) == hipSuccess &&
-                    hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost) ==
-                        hipSuccess;
+    const bool ok = hok(hipMemcpy(lo.data(), dlo, bb, hipMemcpyDeviceToHost)) &&
+                    hok(hipMemcpy(hi.data(), dhi, bb, hipMemcpyDeviceToHost)) &&
+                    hok(hipMemcpy(cnt.data(), dcnt, (size_t)n, hipMemcpyDeviceToHost)) &&
+                    hok(hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
     cleanup();
     if (!ok) return -2;
     // greedy superblocks: the union of their rows' bands, merged when they
@@ -741,20 +743,18 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
                  b_c0 = sizeof(int64_t) * nsb, b_sp = sizeof(int32_t) * nsb,
                  b_rng = sizeof(int64_t) * rng.size();
     char* d = nullptr;
-    if (hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_rng + b_sp)) return -2;
-    bool cp = hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d + b_tiles + b_t0 + b_c0, rng.data(), b_rng, hipMemcpyHostToDevice) ==
-                  hipSuccess &&
-              hipMemcpy(d + b_tiles + b_t0 + b_c0 + b_rng, sb_span.data(), b_sp, hipMemcpyHostToDevice) ==
-                  hipSuccess;
+    if (!hok(hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_rng + b_sp))) return -2;
+    bool cp = hok(hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles + b_t0 + b_c0, rng.data(), b_rng, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles + b_t0 + b_c0 + b_rng, sb_span.data(), b_sp, hipMemcpyHostToDevice));
     uint16_t* cw = nullptr;
-    if (cp && hipMalloc(&cw, sizeof(uint16_t) * A.nnz) == hipSuccess) {
+    if (cp && hok(hipMalloc(&cw, sizeof(uint16_t) * A.nnz))) {
         AHIP_LAUNCH(k_colw_ranges, dim3((unsigned)nsb), dim3(256), 0, nullptr,
                     (const int64_t*)(d + b_tiles), (const int64_t*)d,
                     (const int64_t*)(d + b_tiles + b_t0 + b_c0), A.rowptr, A.col, cw);
-        cp = hipDeviceSynchronize() == hipSuccess;
+        cp = hok(hipDeviceSynchronize());
     } else {
         cp = false;
     }
@@ -780,15 +780,19 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     std::vector<int64_t> rp(n + 1);
     std::vector<int32_t> mn(n), mx(n);
     int32_t *dmn = nullptr, *dmx = nullptr;
-    if (hipMalloc(&dmn, sizeof(int32_t) * n) || hipMalloc(&dmx, sizeof(int32_t) * n)) return -2;
+    if (!hok(hipMalloc(&dmn, sizeof(int32_t) * n)) || !hok(hipMalloc(&dmx, sizeof(int32_t) * n))) {
+        (void)hipFree(dmn);
+        return -2;
+    }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     AHIP_LAUNCH(k_row_span, dim3((unsigned)g), dim3(256), 0, nullptr, n, A.rowptr, A.col, dmn, dmx);
-    (void)hipMemcpy(mn.data(), dmn, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(mx.data(), dmx, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
+    const bool got = hok(hipMemcpy(mn.data(), dmn, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) &&
+                     hok(hipMemcpy(mx.data(), dmx, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) &&
+                     hok(hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
     (void)hipFree(dmn);
     (void)hipFree(dmx);
+    if (!got) return -2;
     // greedy superblocks (column span <= kWinX) split into tiles (<= kWinTile nnz)
     std::vector<int64_t> tiles{0}, sb_tile0{0}, sb_c0;
     std::vector<int32_t> sb_span;
@@ -835,24 +839,33 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     const size_t b_tiles = sizeof(int64_t) * tiles.size(), b_t0 = sizeof(int64_t) * sb_tile0.size(),
                  b_c0 = sizeof(int64_t) * nsb, b_sp = sizeof(int32_t) * nsb;
     char* d = nullptr;
-    if (hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_sp)) return -2;
-    (void)hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d + b_tiles + b_t0 + b_c0, sb_span.data(), b_sp, hipMemcpyHostToDevice);
+    if (!hok(hipMalloc(&d, b_tiles + b_t0 + b_c0 + b_sp))) return -2;
+    bool cp = hok(hipMemcpy(d, tiles.data(), b_tiles, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles, sb_tile0.data(), b_t0, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles + b_t0, sb_c0.data(), b_c0, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d + b_tiles + b_t0 + b_c0, sb_span.data(), b_sp, hipMemcpyHostToDevice));
+    // 16-bit window-relative column indices (one per nonzero)
+    uint16_t* cw = nullptr;
+    if (cp && A.nnz > 0) {
+        cp = hok(hipMalloc(&cw, sizeof(uint16_t) * A.nnz));
+        if (cp) {
+            AHIP_LAUNCH(k_colw, dim3((unsigned)nsb), dim3(256), 0, nullptr,
+                        (const int64_t*)(d + b_tiles), (const int64_t*)d,
+                        (const int64_t*)(d + b_tiles + b_t0), A.rowptr, A.col, cw);
+            cp = hok(hipDeviceSynchronize());
+        }
+    }
+    if (!cp) {
+        if (cw) (void)hipFree(cw);
+        (void)hipFree(d);
+        return -2;
+    }
     A.w_tiles = (const int64_t*)d;
     A.w_sb_tile0 = (const int64_t*)(d + b_tiles);
     A.w_sb_c0 = (const int64_t*)(d + b_tiles + b_t0);
     A.w_sb_span = (const int32_t*)(d + b_tiles + b_t0 + b_c0);
     A.w_nsb = nsb;
-    // 16-bit window-relative column indices (one per nonzero)
-    uint16_t* cw = nullptr;
-    if (A.nnz > 0 && hipMalloc(&cw, sizeof(uint16_t) * A.nnz) == hipSuccess) {
-        AHIP_LAUNCH(k_colw, dim3((unsigned)nsb), dim3(256), 0, nullptr, A.w_sb_tile0, A.w_tiles,
-                           A.w_sb_c0, A.rowptr, A.col, cw);
-        (void)hipDeviceSynchronize();
-        A.w_colw = cw;
-    }
+    A.w_colw = cw;
     *owned = d;
     (void)ncols;
     return 0;
@@ -862,10 +875,12 @@ int csr_build_sell(Csr& A, void** owned) {
     if (!A.w_colw || A.w_nsb <= 0 || A.n >= (int64_t)INT32_MAX) return -1;
     const int64_t n = A.n, nsb = A.w_nsb;
     std::vector<int64_t> rp(n + 1), sb_tile0(nsb + 1);
-    (void)hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(sb_tile0.data(), A.w_sb_tile0, sizeof(int64_t) * (nsb + 1), hipMemcpyDeviceToHost);
+    if (!hok(hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost)) ||
+        !hok(hipMemcpy(sb_tile0.data(), A.w_sb_tile0, sizeof(int64_t) * (nsb + 1), hipMemcpyDeviceToHost)))
+        return -2;
     std::vector<int64_t> tiles((size_t)sb_tile0[nsb] + 1);
-    (void)hipMemcpy(tiles.data(), A.w_tiles, sizeof(int64_t) * tiles.size(), hipMemcpyDeviceToHost);
+    if (!hok(hipMemcpy(tiles.data(), A.w_tiles, sizeof(int64_t) * tiles.size(), hipMemcpyDeviceToHost)))
+        return -2;
     std::vector<int64_t> sb_slice0{0}, sptr{0};
     std::vector<int32_t> srow;
     std::vector<int32_t> order;
@@ -890,7 +905,7 @@ int csr_build_sell(Csr& A, void** owned) {
                  bc = sizeof(uint16_t) * (size_t)(padded ? padded : 1);
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     char* d = nullptr;
-    if (hipMalloc(&d, up(b0) + up(b1) + up(b2) + up(bv) + up(bc))) return -2;
+    if (!hok(hipMalloc(&d, up(b0) + up(b1) + up(b2) + up(bv) + up(bc)))) return -2;
     char* p = d;
     auto take = [&](size_t bytes) {
         char* r = p;
@@ -902,13 +917,13 @@ int csr_build_sell(Csr& A, void** owned) {
     auto* d2 = (int32_t*)take(b2);
     auto* dv = (double*)take(bv);
     auto* dc = (uint16_t*)take(bc);
-    (void)hipMemcpy(d0, sb_slice0.data(), b0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d1, sptr.data(), b1, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d2, srow.data(), b2, hipMemcpyHostToDevice);
-    if (ns > 0)
+    bool cp = hok(hipMemcpy(d0, sb_slice0.data(), b0, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d1, sptr.data(), b1, hipMemcpyHostToDevice)) &&
+              hok(hipMemcpy(d2, srow.data(), b2, hipMemcpyHostToDevice));
+    if (cp && ns > 0)
         AHIP_LAUNCH(k_sell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, d1, d2, A.rowptr,
                            A.w_colw, A.val, dc, dv);
-    if (hipDeviceSynchronize() != hipSuccess) {
+    if (!cp || !hok(hipDeviceSynchronize())) {
         (void)hipFree(d);
         return -2;
     }
@@ -925,8 +940,7 @@ int csr_build_sell(Csr& A, void** owned) {
 
 int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
     std::vector<int64_t> rp(A.n + 1);
-    if (hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost) !=
-        hipSuccess)
+    if (!hok(hipMemcpy(rp.data(), A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost)))
         return -2;
     std::vector<int64_t> blk;
     blk.reserve(A.nnz / (tile / 2) + 16);
@@ -943,8 +957,11 @@ int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
     }
     blk.push_back(A.n);
     int64_t* d = nullptr;
-    if (hipMalloc(&d, sizeof(int64_t) * blk.size()) != hipSuccess) return -2;
-    (void)hipMemcpy(d, blk.data(), sizeof(int64_t) * blk.size(), hipMemcpyHostToDevice);
+    if (!hok(hipMalloc(&d, sizeof(int64_t) * blk.size()))) return -2;
+    if (!hok(hipMemcpy(d, blk.data(), sizeof(int64_t) * blk.size(), hipMemcpyHostToDevice))) {
+        (void)hipFree(d);
+        return -2;
+    }
     *rblk_dev = d;
     A.rblk = d;
     A.nrblk = (int64_t)blk.size() - 1;

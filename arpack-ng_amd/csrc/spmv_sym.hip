@@ -473,8 +473,8 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     const int64_t n = A.n;
     if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
     int32_t *dcnt = nullptr, *dcm = nullptr;
-    if (hipMalloc(&dcnt, sizeof(int32_t) * n) != hipSuccess) return -2;
-    if (hipMalloc(&dcm, sizeof(int32_t) * n) != hipSuccess) {
+    if (fault_filter(hipMalloc(&dcnt, sizeof(int32_t) * n)) != hipSuccess) return -2;
+    if (fault_filter(hipMalloc(&dcm, sizeof(int32_t) * n)) != hipSuccess) {
         (void)hipFree(dcnt);
         return -2;
     }
@@ -483,10 +483,12 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
                        dcnt, dcm);
     std::vector<int32_t> cnt(n), cm(n);
-    (void)hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    const bool got =
+        fault_filter(hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
+        fault_filter(hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess;
     (void)hipFree(dcnt);
     (void)hipFree(dcm);
+    if (!got) return -2;
     std::vector<int64_t> r0s, off;
     std::vector<int32_t> spans, pre;
     int ncu = 0;
@@ -546,8 +548,9 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
                  b_slot = sizeof(double) * (size_t)std::max<int64_t>(nslot, 1),
                  b_wg0 = sizeof(int64_t) * wg0.size(), b_wsl = sizeof(int32_t) * wsl.size();
     char* d = nullptr;
-    if (hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) + up(b_row) +
-                          up(b_val) + up(b_cw) + 2 * up(b_slot) + up(b_wg0) + up(b_wsl)))
+    if (fault_filter(hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) +
+                                       up(b_row) + up(b_val) + up(b_cw) + 2 * up(b_slot) + up(b_wg0) +
+                                       up(b_wsl))) != hipSuccess)
         return -2;
     char* p = d;
     auto take = [&](size_t bytes) {
@@ -568,28 +571,25 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     auto* d_hi = (double*)take(b_slot);
     auto* d_wg0 = (int64_t*)take(b_wg0);
     auto* d_wsl = (int32_t*)take(b_wsl);
-    (void)hipMemcpy(d_wg0, wg0.data(), b_wg0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_wsl, wsl.data(), b_wsl, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_r0, r0s.data(), b_r0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_sp, spans.data(), b_sp, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_pre, pre.data(), b_pre, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_off, off.data(), b_off, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_s0, slice0.data(), b_s0, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_ptr, sptr.data(), b_ptr, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_row, srow.data(), b_row, hipMemcpyHostToDevice);
+    auto h2d = [](void* dst, const void* src, size_t bytes) {
+        return fault_filter(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)) == hipSuccess;
+    };
+    bool ok = h2d(d_wg0, wg0.data(), b_wg0) && h2d(d_wsl, wsl.data(), b_wsl) &&
+              h2d(d_r0, r0s.data(), b_r0) && h2d(d_sp, spans.data(), b_sp) &&
+              h2d(d_pre, pre.data(), b_pre) && h2d(d_off, off.data(), b_off) &&
+              h2d(d_s0, slice0.data(), b_s0) && h2d(d_ptr, sptr.data(), b_ptr) &&
+              h2d(d_row, srow.data(), b_row);
     int64_t* d_sr0 = nullptr;
-    if (ns > 0) {
-        if (hipMalloc(&d_sr0, sizeof(int64_t) * ns)) {
-            (void)hipFree(d);
-            return -2;
-        }
-        (void)hipMemcpy(d_sr0, slice_r0.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice);
-        AHIP_LAUNCH(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, coff, d_ptr, d_row,
-                           d_sr0, A.rowptr, A.col, A.val, d_cw, d_val);
+    if (ok && ns > 0) {
+        ok = fault_filter(hipMalloc(&d_sr0, sizeof(int64_t) * ns)) == hipSuccess &&
+             h2d(d_sr0, slice_r0.data(), sizeof(int64_t) * ns);
+        if (ok)
+            AHIP_LAUNCH(k_symsell_fill, dim3((unsigned)ns), dim3(64), 0, nullptr, coff, d_ptr, d_row,
+                        d_sr0, A.rowptr, A.col, A.val, d_cw, d_val);
     }
     // the outgoing spill's tail past the last window is never written: zero it once
-    (void)hipMemset(d_lo, 0, b_slot);
-    const bool ok = hipDeviceSynchronize() == hipSuccess;
+    ok = ok && fault_filter(hipMemset(d_lo, 0, b_slot)) == hipSuccess;
+    ok = ok && fault_filter(hipDeviceSynchronize()) == hipSuccess;
     if (d_sr0) (void)hipFree(d_sr0);
     if (!ok) {
         (void)hipFree(d);

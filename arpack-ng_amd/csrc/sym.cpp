@@ -19,10 +19,6 @@
 
 namespace ahip {
 
-namespace {
-inline void ck(hipError_t e) { (void)e; }
-}  // namespace
-
 // ------------------------------------------------------------------ Arrays ---
 
 bool is_device_pointer(const void* p) {
@@ -48,7 +44,7 @@ int ArraysT<R>::attach(int64_t nn, int nc, R* resid, R* v, int ldv, R* workd) {
     h_workd = workd;
     stream = default_stream();
     if (!stream) {
-        ck(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -2;
         own_stream = true;
     }
     if (host_mode) {
@@ -74,11 +70,11 @@ int ArraysT<R>::attach(int64_t nn, int nc, R* resid, R* v, int ldv, R* workd) {
 template <class R>
 void ArraysT<R>::release() {
     if (host_mode) {
-        if (d_v) ck(hipFree(d_v));
-        if (d_resid) ck(hipFree(d_resid));
-        if (d_workd) ck(hipFree(d_workd));
+        if (d_v) (void)hipFree(d_v);
+        if (d_resid) (void)hipFree(d_resid);
+        if (d_workd) (void)hipFree(d_workd);
     }
-    if (own_stream && stream) ck(hipStreamDestroy(stream));
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
     d_v = d_resid = d_workd = nullptr;
     stream = nullptr;
     own_stream = false;
@@ -204,13 +200,13 @@ void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m
 
 template <class R>
 void SolverT<R>::read_state() {
-    ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
+    a.ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
 
 template <class R>
 void SolverT<R>::write_state() {
-    ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
+    a.ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
 }
 
 // dgetv0: generate (or take) a start vector, force it into range(OP), and for
@@ -366,10 +362,10 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             double* hc = ws.host_hcol;
             for (int c = 0; c < k; ++c)
                 for (int i = 0; i < ncv; ++i) hc[(size_t)c * ncv + i] = i <= c ? h[i + (size_t)c * ncv] : 0.0;
-            ck(hipMemcpyAsync(ws.hcol, hc, sizeof(double) * (size_t)k * ncv, hipMemcpyHostToDevice,
+            a.ck(hipMemcpyAsync(ws.hcol, hc, sizeof(double) * (size_t)k * ncv, hipMemcpyHostToDevice,
                               a.stream));
         }
-        ck(hipMemcpyAsync(ws.rec, hs, sizeof(double) * 2 * k, hipMemcpyHostToDevice, a.stream));
+        a.ck(hipMemcpyAsync(ws.rec, hs, sizeof(double) * 2 * k, hipMemcpyHostToDevice, a.stream));
     }
 
     for (;;) {
@@ -501,6 +497,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
+        if (a.err.bad()) co_return;  // run() ends the solve with info = -9999
         // a park inside a folded cycle leaves resid = r of the step before the
         // parked one, BEFORE its DGKS sweep (st.fold: the sweep was taken)
         const bool was_folded = fold_ok;
@@ -551,7 +548,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     write_state();
     // assemble the new columns of H from the per-step device records
     double* rec = ws.host_scratch;
-    ck(hipMemcpyAsync(rec, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost, a.stream));
+    a.ck(hipMemcpyAsync(rec, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost, a.stream));
     double* h = workl + ih;
     if (!arnoldi) {  // T(ncv,2): h(:,1) subdiagonal, h(:,2) diagonal
         a.sync();
@@ -561,7 +558,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
         }
     } else {  // H(ncv,ncv): h(1:j,j) from the device, h(j,j-1) = beta_j (SRC/dnaitr.f:566-590)
         std::vector<double> hc((size_t)ncv * npk);
-        ck(hipMemcpyAsync(hc.data(), ws.hcol + (size_t)k * ncv, sizeof(double) * hc.size(),
+        a.ck(hipMemcpyAsync(hc.data(), ws.hcol + (size_t)k * ncv, sizeof(double) * hc.size(),
                           hipMemcpyDeviceToHost, a.stream));
         a.sync();
         for (int jj = k + 1; jj <= k + npk; ++jj) {
@@ -617,7 +614,7 @@ void SolverT<R>::vq_device(int kev, int kplusp, double sigmak, double betak) {
     }
     for (int c = 0; c <= kev && c < kplusp; ++c)
         for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
-    ck(hipMemcpyAsync(ws.q, qbuf, sizeof(double) * m, hipMemcpyHostToDevice, a.stream));
+    a.ck(hipMemcpyAsync(ws.q, qbuf, sizeof(double) * m, hipMemcpyHostToDevice, a.stream));
     dev::vq_update(ws, n, a.d_v, a.d_ld, kplusp, kev, sigmak, betak, a.d_resid);
     if (!ws.host_hcol) a.sync();  // pageable qvec: its lifetime
 }
@@ -641,6 +638,7 @@ Task SolverT<R>::run() {
 
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
+    if (a.err.bad()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
@@ -650,6 +648,7 @@ Task SolverT<R>::run() {
     write_state();
 
     co_await saitr(0, nev0, sinfo);
+    if (a.err.bad()) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -662,6 +661,7 @@ Task SolverT<R>::run() {
         if (pause_budget > 0) --pause_budget;
         ++iter;
         co_await saitr(nev, np, sinfo);
+        if (a.err.bad()) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -747,7 +747,13 @@ Task SolverT<R>::run() {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
         read_state();
+        if (a.err.bad()) goto fault;
         rnorm = ws.st_host->rnorm;
+    }
+fault:  // a failed HIP call: the device state is not trustworthy
+    if (a.err.bad()) {
+        mxiter = iter;
+        info = -9999;
     }
 done:
     nev0 = nev;

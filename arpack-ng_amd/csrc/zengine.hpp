@@ -22,6 +22,11 @@ struct Ws {
     // row-distributed solve: every reduction of `dots` is allreduced over the
     // ranks before it reaches the host (PARPACK/SRC/MPI/pznaitr.f's MPI_ALLREDUCEs)
     const Comm* comm = nullptr;
+    // the owning solve's sticky error record (nullptr: unchecked)
+    DevErr* err = nullptr;
+    void ck(hipError_t e) const {
+        if (err) err->ck(e);
+    }
     int nblk = 0;
     double* part = nullptr;  // 2*(ncv+2) slots x nblk
     double* sums = nullptr;

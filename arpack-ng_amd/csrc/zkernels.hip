@@ -317,8 +317,8 @@ void dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, co
     const int m = 2 * (j + (w ? 1 : 0));
     hipLaunchKernelGGL(k_sum_slots, dim3(m), dim3(kB), 0, ws.stream, ws.part, ws.nblk, ws.sums);
     if (ws.comm) comm_allreduce_sum(ws.comm, ws.sums, m, ws.stream);  // the ranks' local sums
-    (void)hipMemcpyAsync(ws.host, ws.sums, sizeof(double) * m, hipMemcpyDeviceToHost, ws.stream);
-    (void)hipStreamSynchronize(ws.stream);
+    ws.ck(hipMemcpyAsync(ws.host, ws.sums, sizeof(double) * m, hipMemcpyDeviceToHost, ws.stream));
+    ws.ck(hipStreamSynchronize(ws.stream));
     for (int c = 0; c < m / 2; ++c) out[c] = std::complex<double>(ws.host[2 * c], ws.host[2 * c + 1]);
 }
 
@@ -326,18 +326,18 @@ template <class R>
 void update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const std::complex<double>* h,
             const R* rin, R* rout) {
     using T = typename C2<R>::T;
-    if (j > 0) (void)hipMemcpyAsync(ws.coef, h, sizeof(double) * 2 * j, hipMemcpyHostToDevice, ws.stream);
+    if (j > 0) ws.ck(hipMemcpyAsync(ws.coef, h, sizeof(double) * 2 * j, hipMemcpyHostToDevice, ws.stream));
     hipLaunchKernelGGL(k_zupdate<R>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, j,
                        reinterpret_cast<const T*>(V), ld, reinterpret_cast<const double2*>(ws.coef),
                        reinterpret_cast<const T*>(rin), reinterpret_cast<T*>(rout));
-    (void)hipStreamSynchronize(ws.stream);  // h is host memory
+    ws.ck(hipStreamSynchronize(ws.stream));  // h is host memory
 }
 
 template <class R>
 void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
           const std::complex<double>* M, R* Z, int64_t ldz) {
     using T = typename C2<R>::T;
-    (void)hipMemcpyAsync(ws.q, M, sizeof(double) * 2 * (size_t)k * nz, hipMemcpyHostToDevice, ws.stream);
+    ws.ck(hipMemcpyAsync(ws.q, M, sizeof(double) * 2 * (size_t)k * nz, hipMemcpyHostToDevice, ws.stream));
     auto V2 = reinterpret_cast<const T*>(V);
     auto M2 = reinterpret_cast<const double2*>(ws.q);
     auto Z2 = reinterpret_cast<T*>(Z);
@@ -356,7 +356,7 @@ void gemm(const Ws& ws, int64_t n, const R* V, int64_t ld, int k, int nz,
     else  // grid = nblk: ws.scratch holds nblk * kB rows of ncv outputs
         hipLaunchKernelGGL((k_zgemm_generic<R>), dim3(ws.nblk), dim3(kB), 0, ws.stream, n, V2, ld, k,
                            nz, M2, Z2, ldz, reinterpret_cast<double2*>(ws.scratch));
-    (void)hipStreamSynchronize(ws.stream);
+    ws.ck(hipStreamSynchronize(ws.stream));
 }
 
 template <class R>
@@ -372,11 +372,11 @@ template <class R>
 void ger(const Ws& ws, int64_t n, int k, const R* x, const std::complex<double>* w, R* Z,
          int64_t ldz) {
     using T = typename C2<R>::T;
-    (void)hipMemcpyAsync(ws.coef, w, sizeof(double) * 2 * k, hipMemcpyHostToDevice, ws.stream);
+    ws.ck(hipMemcpyAsync(ws.coef, w, sizeof(double) * 2 * k, hipMemcpyHostToDevice, ws.stream));
     hipLaunchKernelGGL(k_zger<R>, dim3(grid(n)), dim3(kB), 0, ws.stream, n, k,
                        reinterpret_cast<const T*>(x), reinterpret_cast<const double2*>(ws.coef),
                        reinterpret_cast<T*>(Z), ldz);
-    (void)hipStreamSynchronize(ws.stream);
+    ws.ck(hipStreamSynchronize(ws.stream));
 }
 
 #define AHIP_ZINST(R)                                                                              \
@@ -423,7 +423,7 @@ static hipError_t ws_alloc(Ws& ws, int64_t n, int ncv, hipStream_t s) {
         const char* f = getenv("AHIP_FORCE_DGKS2");
         ws.st_host->force_dgks2 = (f && f[0] == '1') ? 1 : 0;
     }
-    (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, s);
+    if ((e = hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, s))) return e;
     if ((e = hipMalloc(&ws.q, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
     if ((e = hipHostMalloc(&ws.host, sizeof(double) * slots))) return e;
     if (ncv > 64 &&  // per-thread output columns of k_zgemm_generic

@@ -127,13 +127,13 @@ Task ZSolverT<R>::getv0(bool initv, int j, int itry, int& ierr) {
 
 template <class R>
 void ZSolverT<R>::read_state() {
-    (void)hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream);
+    a.ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
 
 template <class R>
 void ZSolverT<R>::write_state() {
-    (void)hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream);
+    a.ck(hipMemcpyAsync(ws.st, ws.st_host, sizeof(dev::LzState), hipMemcpyHostToDevice, a.stream));
 }
 
 // The second DGKS sweep of step j (SRC/znaitr.f:730-780, gated on the device
@@ -241,10 +241,10 @@ Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
     {
         std::vector<cd> hc((size_t)ncv * npk);
         std::vector<double> beta((size_t)(k + npk));
-        (void)hipMemcpyAsync(hc.data(), ws.hcol + 2 * (size_t)k * ncv, sizeof(cd) * hc.size(),
-                             hipMemcpyDeviceToHost, a.stream);
-        (void)hipMemcpyAsync(beta.data(), ws.rec, sizeof(double) * beta.size(), hipMemcpyDeviceToHost,
-                             a.stream);
+        a.ck(hipMemcpyAsync(hc.data(), ws.hcol + 2 * (size_t)k * ncv, sizeof(cd) * hc.size(),
+                             hipMemcpyDeviceToHost, a.stream));
+        a.ck(hipMemcpyAsync(beta.data(), ws.rec, sizeof(double) * beta.size(), hipMemcpyDeviceToHost,
+                             a.stream));
         a.sync();
         for (int jj = k + 1; jj <= k + npk; ++jj) {
             cd* colh = h + (size_t)(jj - 1) * ldh;
@@ -393,11 +393,13 @@ Task ZSolverT<R>::run() {
     int ierr = 0, sinfo = 0;
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
+    if (a.err.bad()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
     }
     co_await naitr(0, nev, sinfo);
+    if (a.err.bad()) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -408,6 +410,7 @@ Task ZSolverT<R>::run() {
         ++iter;
         np = kplusp - nev;
         co_await naitr(nev, np, sinfo);
+        if (a.err.bad()) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -496,9 +499,14 @@ Task ZSolverT<R>::run() {
             dev::copy(a.stream, 2 * (int64_t)n, a.d_resid, wd(0));
             rnorm = cnorm(a.d_resid);
         }
+        if (a.err.bad()) goto fault;
     }
 done:
     mxiter = iter;
+    goto fail;
+fault:  // a failed HIP call: the device state is not trustworthy (see sym.cpp)
+    mxiter = iter;
+    info = -9999;
 fail:
     iparam[2] = mxiter;
     co_return;
@@ -602,6 +610,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             *ido = 99;
             return;
         }
+        S->ws.err = &S->a.err;
         S->csr = csr;
         S->n_global = dist ? dist->n_global : n;
         if (dist) {  // row block of a distributed solve (PARPACK's pznaupd)
@@ -638,9 +647,10 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         }
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) S->a.h2d_workd(2 * r.y, 2 * (int64_t)n);
     }
-    auto comm_broken = [&]() {  // a failed collective: info = -9999 (see sym_aupd)
-        if (!S->dist || !comm_failed(S->dist->comm)) return false;
-        S->a.sync();
+    // a failed collective or HIP call: info = -9999 (see sym_aupd)
+    auto comm_broken = [&]() {
+        if (!S->a.err.bad() && (!S->dist || !comm_failed(S->dist->comm))) return false;
+        (void)hipStreamSynchronize(S->a.stream);
         *info = -9999;
         *ido = 99;
         g_z.erase(v);
@@ -692,6 +702,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
     *info = inf;
     S->a.download_all();
     S->a.sync();
+    if (S->a.err.bad()) *info = -9999;
     wl_out();
     g_z.erase(v);
 }
@@ -854,9 +865,10 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
         a.release();
         return -9999;
     }
+    ws.err = &a.err;
     if (a.host_mode) {
-        (void)hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(CT) * ldv, sizeof(CT) * n, ncv,
-                               hipMemcpyHostToDevice, a.stream);
+        a.ck(hipMemcpy2DAsync(a.d_v, sizeof(R) * a.d_ld, v, sizeof(CT) * ldv, sizeof(CT) * n, ncv,
+                               hipMemcpyHostToDevice, a.stream));
         a.upload_resid();
     }
     const int64_t ldc = a.d_ld / 2;
@@ -878,22 +890,23 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
         zdev::gemm(ws, n, a.d_v, ldc, nconv, nconv, X.data(), zd, ldzd);
         if (type == SHIFTI) zdev::ger(ws, n, nconv, a.d_resid, wpur.data(), zd, ldzd);
     } else if (zd != a.d_v) {
-        (void)hipMemcpy2DAsync(zd, sizeof(CT) * ldzd, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, nconv,
-                               hipMemcpyDeviceToDevice, a.stream);
+        a.ck(hipMemcpy2DAsync(zd, sizeof(CT) * ldzd, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, nconv,
+                               hipMemcpyDeviceToDevice, a.stream));
     }
     // V first, then Z: a caller may pass Z = V (the reference's drivers do)
     if (a.host_mode)
-        (void)hipMemcpy2DAsync(v, sizeof(CT) * ldv, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, ncv,
-                               hipMemcpyDeviceToHost, a.stream);
+        a.ck(hipMemcpy2DAsync(v, sizeof(CT) * ldv, a.d_v, sizeof(R) * a.d_ld, sizeof(CT) * n, ncv,
+                               hipMemcpyDeviceToHost, a.stream));
     if (!zdevp) {
-        (void)hipMemcpy2DAsync(z, sizeof(CT) * ldz, zd, sizeof(CT) * ldc, sizeof(CT) * n, nconv,
-                               hipMemcpyDeviceToHost, a.stream);
+        a.ck(hipMemcpy2DAsync(z, sizeof(CT) * ldz, zd, sizeof(CT) * ldc, sizeof(CT) * n, nconv,
+                               hipMemcpyDeviceToHost, a.stream));
     }
     a.sync();
     if (!zdevp) (void)hipFree(zd);
     zdev::ws_destroy(ws);
+    const bool bad = a.err.bad();  // a failed copy or a kernel fault of this call
     a.release();
-    return 0;
+    return bad ? -9999 : 0;
 }
 
 }  // namespace ahip

@@ -211,7 +211,9 @@ int arpack_hip_memset(void* dst, int value, size_t bytes);
 int arpack_hip_synchronize(void);
 
 /* Register a CSR matrix (rowptr int64[n+1], col int32[nnz], val f64[nnz]).
- * Pointers may be host or device; host data is copied to HBM. */
+ * Pointers may be host or device; host data is copied to HBM.  0; -1 if the
+ * arrays could not be placed in HBM; -2 if a HIP call of the SpMV plan
+ * analysis failed (nothing is kept). */
 int arpack_hip_csr_create(arpack_hip_csr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
                           const int32_t* col, const double* val);
 void arpack_hip_csr_destroy(arpack_hip_csr* A);
@@ -516,6 +518,11 @@ void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
 /* Per-kernel-class device timing with hipEvents on the launch stream.
  * Classes: 0 SpMV, 1 CGS dots, 2 update(+fused DGKS dots), 3 V*Q, 4 place,
  * 5 finalize, 6 other.  read() synchronises and resets; returns #classes. */
+/* Test hook: the k-th checked HIP call of the engine from now on (copies,
+ * syncs and plan-table uploads of the solve, post-processing and CSR plan
+ * paths) reports hipErrorInvalidValue; the solve then returns info = -9999 and
+ * a CSR create -2.  k <= 0 disarms.  AHIP_FAULT_AT=k arms it at load. */
+void arpack_hip_fault_inject(long k);
 void arpack_hip_profile(int enable);
 int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int nclass);
 

@@ -41,3 +41,29 @@ def test_reference_count_moves_under_one_ulp():
     assert (c0, op0) == (31, 161)
     assert (c1, op1) != (c0, op0)  # one ulp of the start vector moves the count
     np.testing.assert_allclose(d1, d0, rtol=1e-12)  # the answer does not move
+
+
+def test_reference_complex_count_bimodal_under_one_ulp():
+    """Config 5's operator family in mode 1 (M.zrandom(6000, 20, 7, 100), LM,
+    nev 10, ncv 40, tol 1e-10): the reference's restart count is bimodal, 104 /
+    2904 OP*x or 106 / 2947, chosen by one ulp of one start-vector entry (and by
+    OpenBLAS's thread count: pinned to one thread here).  This is the envelope
+    tests/test_gpu_ztraj.py measures on the GPU box's host and holds the engine
+    to."""
+    from threadpoolctl import threadpool_limits
+    n = 6000
+    A = M.to_scipy(*M.zrandom(n, 20, 7, 100.0))
+    v0 = M.dlarnv_uniform(2 * n)[0].view(np.complex128)
+    seen = {}
+    with threadpool_limits(1):
+        for k in range(4):
+            v = v0.copy()
+            if k:
+                i = (k * 997) % n
+                v[i] = complex(np.nextafter(v[i].real, 2.0), v[i].imag)
+            o = ref.znaupd_solve(lambda x, *_: A @ x, n, 10, 40, "LM", 1e-10, v0=v, rvec=False)
+            assert o["info"] == 0 and o["nconv"] == 10
+            seen[(int(o["iparam"][2]), int(o["iparam"][8]))] = np.sort_complex(o["d"][:10])
+    assert set(seen) == {(104, 2904), (106, 2947)}, seen
+    a, b = seen.values()
+    assert np.all(np.abs(a - b) <= 1e-9 * np.abs(a).max())  # the answer does not move
