@@ -91,6 +91,8 @@ def _declare(L):
                                             C.c_int64, C.c_uint32, C.c_int, C.c_int]
     L.arpack_hip_set_stream.argtypes = [C.c_void_p]
     L.arpack_hip_fault_inject.argtypes = [C.c_long]
+    L.arpack_hip_set_deterministic.argtypes = [C.c_int]
+    L.arpack_hip_deterministic.restype = C.c_int
     L.arpack_hip_malloc.argtypes = [C.c_size_t]
     L.arpack_hip_malloc.restype = C.c_void_p
     L.arpack_hip_free.argtypes = [C.c_void_p]
@@ -251,6 +253,17 @@ def profile_read():
     return {c: (float(ms[i]), float(by[i]), int(cnt[i])) for i, c in enumerate(PROF_CLASSES)}
 
 
+def set_deterministic(on: bool = True):
+    """Deterministic mode (arpack_hip_set_deterministic): only fixed-order SpMV
+    forms, so solves are bitwise reproducible run to run.  Set it before
+    CSR.set_symmetric (which then keeps full storage)."""
+    lib().arpack_hip_set_deterministic(1 if on else 0)
+
+
+def deterministic() -> bool:
+    return bool(lib().arpack_hip_deterministic())
+
+
 def fault_inject(k: int):
     """Test hook: the k-th checked HIP call of the engine from now on reports
     hipErrorInvalidValue (arpack_hip_fault_inject); 0 disarms."""
@@ -361,6 +374,9 @@ class CSR:
         fails -- rc = -2 on the ranks whose own plan succeeded."""
         rc = lib().arpack_hip_csr_set_symmetric(self.h, 1 if on else 0)
         self.last_rc = rc
+        if rc == 1:  # deterministic mode: the full-storage (fixed-order) SpMV stays
+            self.symmetric = False
+            return
         if rc != 0:
             raise RuntimeError("symmetric storage not applicable to this matrix (rc=%d)" % rc)
         self.symmetric = bool(on)

@@ -273,12 +273,16 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
     if (csr) S->pause_budget = max_cycles;
     // a failed collective (RCCL / transport error) ends the solve with
     // info = -9999 at the next return to the caller: the ranks' sums no longer
-    // agree.  Every rank's communicator reports the failure of a collective it
-    // took part in, so the ranks stop at the same return.  So does a failed HIP
-    // call of this solve (the sticky S->a.err: a copy, an enqueue, or a kernel
-    // fault surfacing at a sync).
+    // agree.  So does a failed HIP call of this solve (the sticky S->a.err: a
+    // copy, an enqueue, or a kernel fault surfacing at a sync).  Both are
+    // local observations -- a rank keeps joining the collectives after its own
+    // failure, so the ranks stay in step -- and on a multi-rank solve the ranks
+    // agree (one flag allreduce) before any of them leaves, so every rank ends
+    // at the same return.
     auto broken = [&]() {
-        if (!S->a.err.bad() && (!S->dist || !comm_failed(S->dist->comm))) return false;
+        bool bad = S->a.err.bad() || (S->dist && comm_failed(S->dist->comm));
+        if (S->dist && comm_size(S->dist->comm) > 1) bad = !dist_all_ok(S->dist->comm, !bad);
+        if (!bad) return false;
         (void)hipStreamSynchronize(S->a.stream);
         *info = -9999;
         *ido = 99;
@@ -289,7 +293,8 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
-        if (r.ido != -1 && r.ido != 1 && broken()) return;
+        // (the park below drains the stream first, then checks)
+        if (r.ido != -1 && r.ido != 1 && r.ido != SolverT<R>::kPauseIdo && broken()) return;
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
             // it); a row-distributed SpMV also holds its halo exchange: marker mode
@@ -615,6 +620,8 @@ int arpack_hip_dist_set_seed_mode(arpack_hip_dist* D, int mode) {
 }
 
 void arpack_hip_fault_inject(long k) { fault_inject(k); }
+void arpack_hip_set_deterministic(int on) { set_deterministic(on != 0); }
+int arpack_hip_deterministic(void) { return deterministic() ? 1 : 0; }
 
 void arpack_hip_profile(int enable) { dev::prof_enable(enable != 0); }
 

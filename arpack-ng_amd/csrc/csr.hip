@@ -28,6 +28,7 @@
 #include "../../include/arpack_hip.h"
 
 #include "csr_internal.hpp"
+#include "dist.hpp"
 
 namespace ahip::gen {
 
@@ -373,6 +374,11 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
         if (c && !ahip::dist_all_ok(c, 1)) return -2;
         csr_full_storage(A);
         return 0;
+    }
+    if (ahip::deterministic()) {  // the fixed-order full-storage SpMV stays
+        if (c && !ahip::dist_all_ok(c, 1)) return -2;
+        csr_full_storage(A);
+        return 1;
     }
     int rc = 0;
     if (!A->symsell)

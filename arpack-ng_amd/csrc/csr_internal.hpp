@@ -30,10 +30,6 @@ struct arpack_hip_csr {
     arpack_hip_dist* dist = nullptr;
 };
 
-namespace ahip {
-// collective over the ranks of c: 1 if every rank passes ok_local != 0
-int dist_all_ok(const Comm* c, int ok_local);
-}
 
 // the live communicator of A's distribution (nullptr if A is not distributed
 // or, with *stale = true, if that communicator has been destroyed)

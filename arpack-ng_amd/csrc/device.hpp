@@ -22,6 +22,15 @@ namespace ahip {
 hipError_t fault_filter(hipError_t e);
 void fault_inject(long k);
 
+// Deterministic mode (arpack_hip_set_deterministic, ARPACK_HIP_DETERMINISTIC=1):
+// only SpMV forms whose every sum has a fixed order -- a symmetric declaration
+// keeps the full-storage SELL kernel (bitwise SciPy's csr_matvec) instead of the
+// upper-triangle kernel's LDS-atomic transposed terms, and the complex operator
+// takes the column-split kernel instead of the LDS-atomic row tiles.  The rest
+// of the engine (fixed-order partial sums) is deterministic in either mode.
+bool deterministic();
+void set_deterministic(bool on);
+
 // Sticky device-error record of one solve: the first failed HIP call (an
 // enqueue, a copy, or a kernel fault surfacing at a stream sync) is kept, and
 // the driver turns it into info = -9999 at its next return to the caller

@@ -31,6 +31,8 @@ bool comm_alive(const Comm* c, uint64_t gen);
 double* comm_flag(const Comm* c);
 // the communicator has its separate point-to-point communicator (RCCL, > 1 rank)
 bool comm_has_p2p(const Comm* c);
+// collective over the ranks of c: 1 if every rank passes ok_local != 0
+int dist_all_ok(const Comm* c, int ok_local);
 
 // Distributed operator: the local CSR (columns relative to the start of x_ext)
 // plus the halo plan.

@@ -145,6 +145,13 @@ public:
     Task run();     // dsaup2
     Task run_ns();  // dnaup2
 
+    // A failed HIP call of this solve (a.err) ends it with info = -9999.  On a
+    // row distribution the ranks first agree (one flag allreduce, at points
+    // every rank reaches in the same order: once per restart cycle), so they
+    // leave the restart loop together; `halted` holds the agreed verdict.
+    bool halted = false;
+    bool check_halt();
+
 private:
     Task getv0(bool initv, int j, int itry, int& ierr);
     Task saitr(int k, int npk, int& iinfo);

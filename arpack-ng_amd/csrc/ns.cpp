@@ -36,7 +36,7 @@ Task SolverT<R>::run_ns() {
 
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
-    if (a.err.bad()) goto fault;
+    if (check_halt()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
@@ -46,7 +46,7 @@ Task SolverT<R>::run_ns() {
     write_state();
 
     co_await saitr(0, nev, sinfo);
-    if (a.err.bad()) goto fault;
+    if (halted) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -60,7 +60,7 @@ Task SolverT<R>::run_ns() {
         ++iter;
         np = kplusp - nev;
         co_await saitr(nev, np, sinfo);
-        if (a.err.bad()) goto fault;
+        if (halted) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -164,8 +164,7 @@ Task SolverT<R>::run_ns() {
         } else {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
-        read_state();
-        if (a.err.bad()) goto fault;
+        read_state();  // (a failure here is caught by the next cycle's check)
         rnorm = ws.st_host->rnorm;
     }
 done:

@@ -1,12 +1,11 @@
 // Per-kernel-class hipEvent profiler (see device.hpp).  Events are recorded on
 // the stream the kernel is launched on, so the measured duration is the
 // kernel's own device time inside the timed region, not host wall time.
+#include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <thread>
 #include <vector>
-
-#include <atomic>
-#include <cstdlib>
 
 #include "device.hpp"
 
@@ -26,6 +25,16 @@ hipError_t fault_filter(hipError_t e) {
 }
 
 void fault_inject(long k) { g_fault_at.store(k > 0 ? k : 0); }
+
+namespace {
+std::atomic<bool> g_det{[] {
+    const char* e = getenv("ARPACK_HIP_DETERMINISTIC");
+    return e && e[0] == '1';
+}()};
+}  // namespace
+
+bool deterministic() { return g_det.load(std::memory_order_relaxed); }
+void set_deterministic(bool on) { g_det.store(on); }
 
 }  // namespace ahip
 

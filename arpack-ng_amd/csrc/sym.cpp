@@ -155,6 +155,14 @@ bool SolverT<R>::overlap_ready() {
 }
 
 template <class R>
+bool SolverT<R>::check_halt() {
+    bool bad = a.err.bad();
+    if (dist && comm_size(dist->comm) > 1) bad = !dist_all_ok(dist->comm, !bad);
+    halted = halted || bad;
+    return halted;
+}
+
+template <class R>
 RciAwait SolverT<R>::rci(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = nullptr;
     op_y = nullptr;
@@ -497,7 +505,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             }
         }
         read_state();
-        if (a.err.bad()) co_return;  // run() ends the solve with info = -9999
+        if (check_halt()) co_return;  // run() ends the solve with info = -9999
         // a park inside a folded cycle leaves resid = r of the step before the
         // parked one, BEFORE its DGKS sweep (st.fold: the sweep was taken)
         const bool was_folded = fold_ok;
@@ -638,7 +646,7 @@ Task SolverT<R>::run() {
 
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
-    if (a.err.bad()) goto fault;
+    if (check_halt()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
@@ -648,7 +656,7 @@ Task SolverT<R>::run() {
     write_state();
 
     co_await saitr(0, nev0, sinfo);
-    if (a.err.bad()) goto fault;
+    if (halted) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -661,7 +669,7 @@ Task SolverT<R>::run() {
         if (pause_budget > 0) --pause_budget;
         ++iter;
         co_await saitr(nev, np, sinfo);
-        if (a.err.bad()) goto fault;
+        if (halted) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -746,12 +754,11 @@ Task SolverT<R>::run() {
         } else {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
-        read_state();
-        if (a.err.bad()) goto fault;
+        read_state();  // (a failure here is caught by the next cycle's check)
         rnorm = ws.st_host->rnorm;
     }
 fault:  // a failed HIP call: the device state is not trustworthy
-    if (a.err.bad()) {
+    if (halted) {
         mxiter = iter;
         info = -9999;
     }

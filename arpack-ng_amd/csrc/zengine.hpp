@@ -167,6 +167,10 @@ public:
 
     ~ZSolverT();
     Task run();  // znaup2
+    // failed HIP call of this solve -> info = -9999, agreed across the ranks of
+    // a distribution once per restart cycle (see SolverT::check_halt)
+    bool halted = false;
+    bool check_halt();
 
 private:
     Task getv0(bool initv, int j, int itry, int& ierr);

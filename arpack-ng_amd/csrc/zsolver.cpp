@@ -36,6 +36,14 @@ ZSolverT<R>::~ZSolverT() {
 }
 
 template <class R>
+bool ZSolverT<R>::check_halt() {
+    bool bad = a.err.bad();
+    if (dist && comm_size(dist->comm) > 1) bad = !dist_all_ok(dist->comm, !bad);
+    halted = halted || bad;
+    return halted;
+}
+
+template <class R>
 RciAwait ZSolverT<R>::rci(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = nullptr;
     op_y = nullptr;
@@ -393,13 +401,13 @@ Task ZSolverT<R>::run() {
     int ierr = 0, sinfo = 0;
     if (initv) a.upload_resid();
     co_await getv0(initv, 1, 1, ierr);
-    if (a.err.bad()) goto fault;
+    if (check_halt()) goto fault;
     if (rnorm == 0.0) {
         info = -9;
         goto done;
     }
     co_await naitr(0, nev, sinfo);
-    if (a.err.bad()) goto fault;
+    if (check_halt()) goto fault;
     if (sinfo > 0) {
         np = sinfo;
         mxiter = iter;
@@ -410,7 +418,7 @@ Task ZSolverT<R>::run() {
         ++iter;
         np = kplusp - nev;
         co_await naitr(nev, np, sinfo);
-        if (a.err.bad()) goto fault;
+        if (check_halt()) goto fault;
         if (sinfo > 0) {
             np = sinfo;
             mxiter = iter;
@@ -498,8 +506,7 @@ Task ZSolverT<R>::run() {
         } else {
             dev::copy(a.stream, 2 * (int64_t)n, a.d_resid, wd(0));
             rnorm = cnorm(a.d_resid);
-        }
-        if (a.err.bad()) goto fault;
+        }  // (a failure here is caught by the next cycle's check)
     }
 done:
     mxiter = iter;
@@ -648,8 +655,11 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         if (r.ido == -1 || r.ido == 1 || r.ido == 2) S->a.h2d_workd(2 * r.y, 2 * (int64_t)n);
     }
     // a failed collective or HIP call: info = -9999 (see sym_aupd)
+    // (agreed across the ranks first, as in sym_aupd)
     auto comm_broken = [&]() {
-        if (!S->a.err.bad() && (!S->dist || !comm_failed(S->dist->comm))) return false;
+        bool bad = S->a.err.bad() || (S->dist && comm_failed(S->dist->comm));
+        if (S->dist && comm_size(S->dist->comm) > 1) bad = !dist_all_ok(S->dist->comm, !bad);
+        if (!bad) return false;
         (void)hipStreamSynchronize(S->a.stream);
         *info = -9999;
         *ido = 99;
@@ -660,7 +670,8 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         S->ctx.leaf.resume();
         if (S->ctx.done) break;
         const RciReq r = S->ctx.req;
-        if (comm_broken()) return;
+        // free-running OP requests stay on the device: no agreement per product
+        if (!(S->csr && (r.ido == -1 || r.ido == 1)) && comm_broken()) return;
         if (S->csr && (r.ido == -1 || r.ido == 1)) {
             if constexpr (!kShadow) {
                 if (!zs) {
@@ -1162,7 +1173,7 @@ struct arpack_hip_zshift {
 
 int arpack_hip_zshift_create(arpack_hip_zshift** out, const arpack_hip_zcsr* A, double sigma_re,
                              double sigma_im, double rtol, int maxit) {
-    if (!A || !(rtol > 0.0) || maxit < 1) return -1;
+    if (!out || !A || !(rtol > 0.0) || maxit < 1) return -1;
     auto* Z = new arpack_hip_zshift;
     if (ahip::zdev::zshift_create(Z->S, &A->A, cd(sigma_re, sigma_im), rtol, maxit) != 0) {
         delete Z;
@@ -1179,19 +1190,21 @@ void arpack_hip_zshift_destroy(arpack_hip_zshift* Z) {
 }
 
 int arpack_hip_zshift_solve(arpack_hip_zshift* Z, const double* x, double* y, double* relres) {
+    if (!Z || !x || !y || x == y) return -2;  // as arpack_hip_dshift_solve
     return ahip::zdev::zshift_apply(Z->S, nullptr, x, y, relres);
 }
 
 int arpack_hip_zshift_stats(const arpack_hip_zshift* Z, long long* solves, long long* iters,
                             long long* failures, double* max_relres, double* ms,
                             double* bytes_per_iter) {
+    if (!Z) return -1;
     const auto& S = Z->S;
-    *solves = S.n_solves;
-    *iters = S.n_iters;
-    *failures = S.n_fail;
-    *max_relres = S.max_relres;
-    *ms = S.ms_total;
-    *bytes_per_iter = ahip::zdev::zshift_iter_bytes(S);
+    if (solves) *solves = S.n_solves;
+    if (iters) *iters = S.n_iters;
+    if (failures) *failures = S.n_fail;
+    if (max_relres) *max_relres = S.max_relres;
+    if (ms) *ms = S.ms_total;
+    if (bytes_per_iter) *bytes_per_iter = ahip::zdev::zshift_iter_bytes(S);
     return 0;
 }
 

@@ -384,7 +384,7 @@ int zcsr_build_split(ZCsr& A) {
 namespace {
 template <int S>
 void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp, const int* gate) {
-    if (A.tile) {
+    if (A.tile && !deterministic()) {  // (LDS-atomic row sums: not bitwise run to run)
         hipLaunchKernelGGL(k_ztile<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
                            A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
         return;

@@ -34,6 +34,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <tuple>
 #include <utility>
 
@@ -94,9 +95,26 @@ void release_binding() {
     g_bound = false;
 }
 
+// V arrays of the solves in progress (from a fresh *aupd call to its ido = 99
+// return): the engine keeps their state next to the communicator binding.
+std::set<const void*> g_live;
+void live_begin(const void* v, const a_int* ido) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (*ido == 0) g_live.erase(v);  // a new solve on V abandons the old one
+}
+void live_end(const void* v, const a_int* ido) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (*ido == 99) g_live.erase(v);
+    else g_live.insert(v);
+}
+
 // Bind the engine's communicator to `fcomm` (collective over it on first use).
+// One communicator at a time: a call on another communicator while a solve is
+// in progress is refused (info = -9999) rather than freeing that solve's
+// distribution under it.
 bool bind_comm(MPI_Fint fcomm) {
     if (g_bound && g_bind.key == fcomm) return true;
+    if (g_bound && !g_live.empty()) return false;
     release_binding();
     MPI_Comm c = MPI_Comm_f2c(fcomm);
     Binding b;
@@ -120,10 +138,12 @@ bool bind_comm(MPI_Fint fcomm) {
     g_bind = b;
     int rc = 0;
     if (b.rccl) {
-        char id[128] = {0};
-        if (b.rank == 0 && arpack_hip_comm_unique_id(id) != 0) rc = -1;
-        MPI_Bcast(id, 128, MPI_CHAR, 0, b.comm);
-        if (rc == 0) rc = arpack_hip_comm_init(b.size, b.rank, id, lrank);
+        // rank 0's RCCL id and whether it got one, in one broadcast: on failure
+        // no rank enters the RCCL bootstrap (which would wait for rank 0)
+        char id[129] = {0};
+        if (b.rank == 0 && arpack_hip_comm_unique_id(id) != 0) id[128] = 1;
+        MPI_Bcast(id, 129, MPI_CHAR, 0, b.comm);
+        rc = id[128] ? -1 : arpack_hip_comm_init(b.size, b.rank, id, lrank);
     } else {
         rc = arpack_hip_comm_init_host(b.size, b.rank, host_allreduce, host_halo, &g_bind,
                                        ndev > 0 ? lrank % ndev : 0);
@@ -238,10 +258,12 @@ extern "C" {
 void pdsaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pdsaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
+    live_end(v, ido);
 }
 void pdseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, double* d,
                double* z, a_int ldz, double sigma, char const* bmat, a_int n, char const* which,
@@ -256,10 +278,12 @@ void pdseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pssaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pssaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
+    live_end(v, ido);
 }
 void psseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, float* d,
                float* z, a_int ldz, float sigma, char const* bmat, a_int n, char const* which,
@@ -273,10 +297,12 @@ void psseupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pdnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, double* resid, a_int ncv, double* v, a_int ldv, a_int* iparam,
                a_int* ipntr, double* workd, double* workl, a_int lworkl, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pdnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
+    live_end(v, ido);
 }
 void pdneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, double* dr,
                double* di, double* z, a_int ldz, double sigmar, double sigmai, double* workev,
@@ -292,10 +318,12 @@ void pdneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void psnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, float* resid, a_int ncv, float* v, a_int ldv, a_int* iparam,
                a_int* ipntr, float* workd, float* workl, a_int lworkl, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_psnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, info);
+    live_end(v, ido);
 }
 void psneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, float* dr,
                float* di, float* z, a_int ldz, float sigmar, float sigmai, float* workev,
@@ -311,10 +339,12 @@ void psneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pznaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                double tol, zc* resid, a_int ncv, zc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                zc* workd, zc* workl, a_int lworkl, double* rwork, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pznaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
+    live_end(v, ido);
 }
 void pzneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, zc* d, zc* z,
                a_int ldz, zc sigma, zc* workev, char const* bmat, a_int n, char const* which,
@@ -328,10 +358,12 @@ void pzneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* selec
 void pcnaupd_c(MPI_Fint comm, a_int* ido, char const* bmat, a_int n, char const* which, a_int nev,
                float tol, cc* resid, a_int ncv, cc* v, a_int ldv, a_int* iparam, a_int* ipntr,
                cc* workd, cc* workl, a_int lworkl, float* rwork, a_int* info) {
+    live_begin(v, ido);
     arpack_hip_dist* D = dist_for(comm, n, *ido == 0);
     if (!D) return fail(ido, info);
     arpack_hip_pcnaupd_c(D, ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd,
                          workl, lworkl, rwork, info);
+    live_end(v, ido);
 }
 void pcneupd_c(MPI_Fint comm, a_int rvec, char const* howmny, a_int const* select, cc* d, cc* z,
                a_int ldz, cc sigma, cc* workev, char const* bmat, a_int n, char const* which,

@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import subprocess
 import sys
 import time
@@ -130,8 +131,19 @@ def cpu_baseline(args, cycles):
     if not args.no_cpu_ttc:
         cmd.append("--ttc")
     try:
-        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        # its own session, killed as a group afterwards: no descendant of the
+        # baseline (BLAS / OpenMP helpers included) outlives bench.py
+        p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True, start_new_session=True)
+        try:
+            stdout, _ = p.communicate(timeout=900)
+        finally:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+            p.wait()
+        line = [ln for ln in stdout.splitlines() if ln.startswith("{")][-1]
         cb = json.loads(line)
         out = dict(value=cb["iters_per_s"], unit="iters/s", cores=threads, kind="reference",
                    sample=cb["sample"], lanczos_steps_per_s=cb["lanczos_steps_per_s"],
@@ -187,6 +199,10 @@ def main():
                          "(1-rank RCCL communicator, DistOp) to price its machinery")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="deterministic mode (arpack_hip_set_deterministic): only fixed-order "
+                         "SpMV forms, so --storage sym keeps the full-storage kernel and every "
+                         "solve is bitwise reproducible")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -195,6 +211,7 @@ def main():
     dist = None
     out_fd = json_stdout()
     pkg = load_pkg()
+    pkg.set_deterministic(args.deterministic)
     n, nev, ncv = args.n, args.nev, args.ncv
     D = None
     if world > 1:
@@ -225,7 +242,7 @@ def main():
             # collective on a distributed operator: every rank ends up in the
             # same mode (all fall back to full storage if any rank's plan fails)
             A.set_symmetric(True)
-            storage = "sym"
+            storage = "sym" if A.symmetric else "full"
         except RuntimeError:
             pass
     gen_s = time.time() - t
@@ -307,12 +324,16 @@ def main():
     # on its last: hipExtLaunchKernel), kept out of the timed region above; if that solve has
     # finished, min(K, 10) cycles of a fresh one after its warmup.
     prof = None
+    prof_cycles = None
     if not args.no_profile:
         pk = args.steps
+        prof_cycles = "the %d cycles after the timed ones, same solve" % pk
         if ido != 98:
             del s
             s, _ = warm_solve(min(args.warmup, 5))
             pk = min(args.steps, 10)
+            prof_cycles = ("%d cycles of a fresh solve after %d warmup cycles (the timed solve "
+                           "had converged)" % (pk, min(args.warmup, 5)))
         pkg.profile(True)
         pkg.profile_read()
         cycles(s, pk)
@@ -423,6 +444,10 @@ def main():
                    "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
                    "which": "LA", "tol": "eps (a solve that converges inside the timed window is followed by a fresh one)",
                    "spmv_storage": "symmetric (upper triangle)" if storage == "sym" else "full CSR",
+                   # sym: the transposed terms meet in LDS in wave order (Ritz values
+                   # reproducible to ~6e-15, not bitwise); full: fixed-order sums
+                   "bitwise_reproducible": storage == "full",
+                   "deterministic_mode": bool(args.deterministic),
                    "parallelism": "single GPU" if world == 1 else
                    f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
                    f"REHEARSAL row-block x{world} on one GPU, host-staged gloo transport"},
@@ -455,6 +480,11 @@ def main():
                                      "each, + 4n row map"),
                      "reference_model": None,
                      "bytes_per_launch": spmv_bytes, "avg_launch_ms": spmv_avg_ms,
+                     # the per-kernel profile is not the timed cycles themselves:
+                     # later cycles run more Lanczos steps per cycle as nev grows
+                     "profiled_cycles": prof_cycles,
+                     "profiled_steps_per_cycle": (cnt / pk) if cnt and not args.no_profile else None,
+                     "timed_steps_per_cycle": nopx / args.steps,
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
         "kernels": kernels,

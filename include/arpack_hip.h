@@ -234,7 +234,8 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * allreduce) and if any rank's plan fails every rank keeps the full-storage
  * kernel and returns nonzero (its own plan error, or -2 when only another
  * rank's plan failed); -3 if the distribution's communicator has been
- * destroyed. */
+ * destroyed.  In deterministic mode (arpack_hip_set_deterministic) on = 1
+ * keeps the full-storage kernel and returns 1. */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
@@ -523,6 +524,13 @@ void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
  * paths) reports hipErrorInvalidValue; the solve then returns info = -9999 and
  * a CSR create -2.  k <= 0 disarms.  AHIP_FAULT_AT=k arms it at load. */
 void arpack_hip_fault_inject(long k);
+/* Deterministic mode: every SpMV sum in a fixed order, so a solve is bitwise
+ * reproducible run to run.  A later arpack_hip_csr_set_symmetric(A, 1) then
+ * keeps the full-storage kernel (bitwise SciPy's csr_matvec) and returns 1,
+ * and the complex operator uses its column-split kernel instead of the
+ * LDS-atomic row tiles.  Off by default (ARPACK_HIP_DETERMINISTIC=1: on). */
+void arpack_hip_set_deterministic(int on);
+int arpack_hip_deterministic(void);
 void arpack_hip_profile(int enable);
 int arpack_hip_profile_read(double* ms, double* bytes, long long* count, int nclass);
 

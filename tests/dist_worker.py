@@ -13,7 +13,9 @@ CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
       declared symmetric: upper-triangle SpMV + forward spill exchange; also
       checks one distributed SpMV against SciPy), ns_csr (pdnaupd_csr_cycles),
       sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather),
-      lap3d (FIXTURE m<m>_cap<k>: config 4's 3-D Laplacian, capped run).
+      lap3d (FIXTURE m<m>_cap<k>: config 4's 3-D Laplacian, capped run),
+      fault_csr / fault_rci (sym_csr / sym_rci with a HIP failure injected on
+      rank 1 only: every rank must end with info = -9999).
 Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
 import os
 import sys
@@ -124,6 +126,9 @@ def lap3d(pkg, out, rank, world, m, cap):
 def main():
     case, fixture, out = sys.argv[1], sys.argv[2], sys.argv[3]
     info0 = len(sys.argv) > 4 and sys.argv[4] == "info0"
+    fault = case.startswith("fault_")
+    if fault:
+        case = "sym_" + case[len("fault_"):]
     import torch
     import torch.distributed as dist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -174,10 +179,14 @@ def main():
                                np.abs(val[rp[r0]:rp[r1]]), n) @ np.abs(x)
             err = np.abs(yd.numpy() - Aloc @ x)
             res["spmv_ok"] = np.array([bool(np.all(err <= 64 * np.finfo(float).eps * scale))])
+        if fault and rank == 1:
+            pkg.fault_inject(40)
         assert pkg.pdsaupd_cycles(s, D, -1) == 99
     else:
         D = pkg.DistRows(nloc, r0, n)
         Aloc = M.to_scipy(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]], n)
+        if fault and rank == 1:
+            pkg.fault_inject(40)
         while True:
             ido = pkg.pxaupd(s, D)
             if ido in (-1, 1):  # gloo all_gather wants equal sizes: pad to the largest block
@@ -193,6 +202,15 @@ def main():
                 break
             else:
                 raise AssertionError(ido)
+    pkg.fault_inject(0)
+    if fault:  # the solve ended early on every rank: nothing to post-process
+        np.savez(os.path.join(out, "rank%d.npz" % rank), iparam=s.iparam.copy(), info=s.info.copy(),
+                 failed=np.array([pkg.comm_failed()]))
+        dist.barrier()
+        del D
+        pkg.comm_destroy()
+        dist.destroy_process_group()
+        return
     if ns:
         dr, di, z, nconv = s.eupd(dist=D)
         res.update(d=dr, di=di)

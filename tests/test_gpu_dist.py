@@ -242,3 +242,16 @@ def test_sym_csr_many_ranks(tmp_path, golden, P):
     np.testing.assert_allclose(np.sort(ranks[0]["d"]), np.sort(g["d"]), rtol=1e-10)
     assert _resid(A, _z(ranks), ranks[0]["d"]) <= 1e-8
 
+
+
+@pytest.mark.parametrize("case", ["fault_csr", "fault_rci"])
+def test_one_rank_device_failure_ends_every_rank(tmp_path, case):
+    """A HIP failure on ONE rank (the fault-injection hook armed on rank 1 only)
+    ends the solve with info = -9999 on EVERY rank at the same return: the ranks
+    agree on the failure (a flag allreduce once per restart cycle and at each
+    return to the caller) instead of rank 1 leaving while the others wait in
+    the next collective (comm_broken was rank-local)."""
+    for P in (2, 3):
+        ranks = _run(tmp_path, case, "g4_banded", P)
+        for r in ranks:
+            assert int(r["info"][0]) == -9999, (case, P, [int(q["info"][0]) for q in ranks])
