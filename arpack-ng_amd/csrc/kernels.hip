@@ -262,15 +262,13 @@ __device__ int refine_decision(int phase, const double* ss, int jm, int jj, int 
 // m slots of `part`; region 2: m2 slots of `part2`, only for kFinCgsChained)
 // and the phase logic.  from_sums: the m + m2 sums are already in `sums`
 // (reduced, and allreduced across ranks).
-// The kernel body; st is the block's LDS copy of the state (k_finalize).
-__device__ __forceinline__ void fin_body(const double* __restrict__ part, int nblk, int from_sums,
-                                         int m, int phase, int j, int rstart,
-                                         double* __restrict__ sums, double* __restrict__ coef,
-                                         int cstride, double* __restrict__ rec, LzState* st,
-                                         double* __restrict__ hcol, int hld,
-                                         const double* __restrict__ part2, int m2,
-                                         int rstart_prev, double* s_rec,
-                                         const double* s_h = nullptr) {
+// Stage 1 (fin_sums): the m + m2 sums into the dynamic-LDS s_sum.  It reads
+// nothing of the state, so k_finalize issues it before the state load has
+// returned (the two memory round trips overlap); the caller's barrier
+// publishes s_sum.
+__device__ __forceinline__ void fin_sums(const double* __restrict__ part, int nblk, int from_sums,
+                                         int m, const double* __restrict__ sums,
+                                         const double* __restrict__ part2, int m2) {
     // the m + m2 (<= 2 ncv + 4) sums are staged in dynamic LDS sized by the
     // launch, so any ncv the argument checks accept fits
     extern __shared__ double s_sum[];
@@ -295,7 +293,19 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
             if (sub == 0 && k < mt) s_sum[k] = s;
         }
     }
-    __syncthreads();
+}
+
+// Stage 2: the phase logic on s_sum; st is the block's LDS copy of the state
+// (k_finalize), already checked against the gate.
+__device__ __forceinline__ void fin_body(int m, int phase, int j, int rstart,
+                                         double* __restrict__ sums, double* __restrict__ coef,
+                                         int cstride, double* __restrict__ rec, LzState* st,
+                                         double* __restrict__ hcol, int hld, int m2,
+                                         int rstart_prev, double* s_rec,
+                                         const double* s_h = nullptr) {
+    extern __shared__ double s_sum[];
+    const int nt = blockDim.x;
+    const int mt = m + m2;
     const int t = threadIdx.x;
     for (int k = t; k < mt; k += nt) sums[k] = s_sum[k];
     const int jm = m - 1;  // index of the w'u / r'r slot
@@ -405,17 +415,20 @@ __device__ __forceinline__ void fin_body(const double* __restrict__ part, int nb
             st->fold = s_take;
             s_rec[2 * (j - 1)] = st->alpha;
             s_rec[2 * (j - 1) + 1] = st->beta;
-            if (s_take && !hld)  // (Arnoldi: H s below, in parallel)
-                for (int k = 0; k < jm; ++k) {
-                    double tk = s_rec[2 * k] * s_sum[k];
-                    if (k > 0) tk = fma(s_rec[2 * k + 1], s_sum[k - 1], tk);
-                    if (k + 1 < jm) tk = fma(s_rec[2 * (k + 1) + 1], s_sum[k + 1], tk);
-                    coef[3 * cstride + k] = tk;
-                }
         }
     }
     __syncthreads();
     const int take = s_take;
+    if (pfold && take && !hld) {
+        // t = T s, one row per thread (Arnoldi: H s below); the same three
+        // terms in the same order as a serial loop
+        for (int k = t; k < jm; k += nt) {
+            double tk = s_rec[2 * k] * s_sum[k];
+            if (k > 0) tk = fma(s_rec[2 * k + 1], s_sum[k - 1], tk);
+            if (k + 1 < jm) tk = fma(s_rec[2 * (k + 1) + 1], s_sum[k + 1], tk);
+            coef[3 * cstride + k] = tk;
+        }
+    }
     if (pfold && take && hld) {
         // Arnoldi: t = H_j s with the full upper-Hessenberg records (column q of
         // H: hcol rows 0..q, subdiagonal H(q+1,q) = rec[2q+3]); this step's
@@ -475,10 +488,13 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         for (int k = threadIdx.x; k < jm * jm; k += blockDim.x)
             s_h[k] = hcol[(int64_t)(k / jm) * hld + k % jm];
     }
+    // the partials' loads go out with the state's: one memory latency, not two
+    // (a closed gate discards the sums unwritten)
+    fin_sums(part, nblk, from_sums, m, sums, part2, m2);
     __syncthreads();
     if (gate_closed(&s_st, gate)) return;
-    fin_body(part, nblk, from_sums, m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol,
-             hld, part2, m2, rstart_prev, s_rec, HS ? s_h : nullptr);
+    fin_body(m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol, hld, m2, rstart_prev,
+             s_rec, HS ? s_h : nullptr);
     __syncthreads();
     if (threadIdx.x == 0) *st = s_st;
 }

@@ -217,14 +217,11 @@ __global__ void k_zs_zero_if(int64_t n, typename C2<R>::T* r, const LzState* st)
 }
 
 // Single-block finalize over m complex slots (2m real; slot m-1 = the norm).
-__device__ __forceinline__ void zs_fin_body(const double* __restrict__ part, int nblk, int m,
-                                            int phase, int j, int rstart,
-                                            double* __restrict__ sums,
-                                            double2* __restrict__ coef, int cstride,
-                                            double* __restrict__ rec, LzState* st,
-                                            double2* __restrict__ hcol, int hld) {
+// Stage 1: the sums into s_sum (reads no state: issued alongside the state
+// load, as k_finalize does; the caller's barrier publishes them).
+__device__ __forceinline__ void zs_fin_sums(const double* __restrict__ part, int nblk, int m) {
     extern __shared__ double s_sum[];  // 2m doubles
-    const int mt = 2 * m, nt = blockDim.x, t = threadIdx.x;
+    const int mt = 2 * m, t = threadIdx.x;
     {   // 32 slots per round, 32 threads per slot in four chains (as k_finalize)
         const int sub = t & 31;
         for (int k0 = 0; k0 < mt; k0 += 32) {
@@ -238,7 +235,16 @@ __device__ __forceinline__ void zs_fin_body(const double* __restrict__ part, int
             if (sub == 0 && k < mt) s_sum[k] = s;
         }
     }
-    __syncthreads();
+}
+
+// Stage 2: the phase logic (st: the LDS copy of the state, gate checked).
+__device__ __forceinline__ void zs_fin_body(int m, int phase, int j, int rstart,
+                                            double* __restrict__ sums,
+                                            double2* __restrict__ coef, int cstride,
+                                            double* __restrict__ rec, LzState* st,
+                                            double2* __restrict__ hcol, int hld) {
+    extern __shared__ double s_sum[];  // 2m doubles
+    const int mt = 2 * m, nt = blockDim.x, t = threadIdx.x;
     for (int k = t; k < mt; k += nt) sums[k] = s_sum[k];
     const int jm = m - 1;
     const double nrm = sqrt(fabs(s_sum[2 * jm]));
@@ -328,9 +334,10 @@ __global__ __launch_bounds__(1024) void k_zs_finalize(const double* __restrict__
                                                       double2* __restrict__ hcol, int hld) {
     __shared__ LzState s_st;
     if (threadIdx.x == 0) s_st = *st;
+    zs_fin_sums(part, nblk, m);  // overlaps the state load
     __syncthreads();
     if (zgate_closed(&s_st, gate)) return;
-    zs_fin_body(part, nblk, m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol, hld);
+    zs_fin_body(m, phase, j, rstart, sums, coef, cstride, rec, &s_st, hcol, hld);
     __syncthreads();
     if (threadIdx.x == 0) *st = s_st;
 }
