@@ -1115,6 +1115,14 @@ class DistOp:
         lib().arpack_hip_dist_info(self.h, *[C.byref(x) for x in v])
         return dict(zip(["halo_lo", "halo_hi", "send_lo", "send_hi"], [x.value for x in v]))
 
+    @property
+    def mode(self):
+        """Exchange form: "halo" (neighbour slabs), "ghosts" (per-peer ghost
+        lists) or "allgather" (arpack_hip_dist_mode)."""
+        L = lib()
+        L.arpack_hip_dist_mode.argtypes = [C.c_void_p]
+        return ("halo", "ghosts", "allgather")[L.arpack_hip_dist_mode(self.h)]
+
     def __del__(self):
         try:
             if self.h and _lib is not None:

@@ -42,6 +42,7 @@ uint64_t comm_gen(const Comm* c) { return c ? c->gen : 0; }
 bool comm_alive(const Comm* c, uint64_t gen) { return c && c == g_comm && c->gen == gen; }
 double* comm_flag(const Comm* c) { return c ? c->d_flag : nullptr; }
 bool comm_has_p2p(const Comm* c) { return c && c->nccl_p2p; }
+bool comm_is_host(const Comm* c) { return c && c->h_halo; }
 
 // Record an RCCL / HIP failure of a collective: the communicator is marked
 // failed and the engine's drivers turn that into info = -9999 at their next
@@ -246,6 +247,32 @@ void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only, bool
         if (D.send_hi && !hi_only)
             chk(ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, cm, s));
         if (D.halo_hi) chk(ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, cm, s));
+    }
+    chk(ncclGroupEnd());
+    note(c, ok);
+}
+
+// The general distributed SpMV's exchange over RCCL: one group of point-to-
+// point transfers, every peer pair only in the direction it has data for.
+void comm_ghosts(const Comm* c, const DistOp& D, hipStream_t s, bool p2p) {
+    if (!c || c->nranks == 1 || !c->nccl) return;
+    const int r = c->rank, P = c->nranks;
+    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
+    bool ok = ncclGroupStart() == ncclSuccess;
+    auto chk = [&](ncclResult_t e) { ok = ok && e == ncclSuccess; };
+    for (int q = 0; q < P; ++q) {
+        if (q == r) continue;
+        if (D.mode == DistOp::kGhostLists) {
+            if (D.send_cnt[q])
+                chk(ncclSend(D.send_buf + D.send_off[q], (size_t)D.send_cnt[q], ncclDouble, q, cm, s));
+            if (D.recv_cnt[q])
+                chk(ncclRecv(D.x_ext + D.nloc + D.recv_off[q], (size_t)D.recv_cnt[q], ncclDouble, q,
+                             cm, s));
+        } else {  // kAllGather
+            if (D.nloc) chk(ncclSend(D.x_mid(), (size_t)D.nloc, ncclDouble, q, cm, s));
+            if (D.peer_nloc[q])
+                chk(ncclRecv(D.x_ext + D.peer_row0[q], (size_t)D.peer_nloc[q], ncclDouble, q, cm, s));
+        }
     }
     chk(ncclGroupEnd());
     note(c, ok);

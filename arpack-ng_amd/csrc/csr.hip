@@ -375,6 +375,10 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
         csr_full_storage(A);
         return 0;
     }
+    // a general operator's block (ghost lists / all-gather) has no spill
+    // exchange for the transposed terms: full storage (the mode is the same on
+    // every rank, so no agreement is needed)
+    if (A->dist && ahip_dist_mode(A->dist) != 0) return -1;
     if (ahip::deterministic()) {  // the fixed-order full-storage SpMV stays
         if (c && !ahip::dist_all_ok(c, 1)) return -2;
         csr_full_storage(A);
@@ -527,6 +531,27 @@ __global__ void k_shift_cols(int64_t nnz, int32_t* col, int64_t shift) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += stride)
         col[k] = (int32_t)((int64_t)col[k] - shift);
 }
+// ghost-list remap of a general operator's block (dist.hip ghost plan): own
+// columns [row0, row0 + nloc) -> c - row0, others -> nloc + their index in the
+// sorted ghost list (binary search; every off-block column is in the list)
+__global__ void k_remap_ghost(int64_t nnz, int32_t* col, int64_t row0, int64_t nloc,
+                              const int64_t* __restrict__ ghosts, int64_t nghost) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += stride) {
+        const int64_t c = col[k];
+        if (c >= row0 && c < row0 + nloc) {
+            col[k] = (int32_t)(c - row0);
+            continue;
+        }
+        int64_t lo = 0, hi = nghost;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (ghosts[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+        col[k] = (int32_t)(nloc + lo);
+    }
+}
 __global__ void k_col_span(int64_t nnz, const int32_t* col, int* mn, int* mx) {
     int a = 0x7fffffff, b = -1;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -558,10 +583,26 @@ int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax) {
     return 0;
 }
 
+static int reanalyse(arpack_hip_csr* A, int64_t ncols);
+
 int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     if (A->A.nnz > 0 && shift != 0)
         hipLaunchKernelGGL(k_shift_cols, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz, A->col, shift);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return reanalyse(A, ncols);
+}
+
+int ahip_csr_remap_ghost(arpack_hip_csr* A, int64_t row0, int64_t nloc, const int64_t* ghosts,
+                         int64_t nghost) {
+    if (A->A.nnz > 0)
+        hipLaunchKernelGGL(k_remap_ghost, dim3(grid_of(A->A.nnz)), dim3(256), 0, nullptr, A->A.nnz,
+                           A->col, row0, nloc, ghosts, nghost);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return reanalyse(A, nloc + nghost);
+}
+
+// the SpMV analysis again for new column indices over an x of ncols entries
+static int reanalyse(arpack_hip_csr* A, int64_t ncols) {
     A->ncols = ncols;
     if (A->win) (void)hipFree(A->win);
     if (A->sell) (void)hipFree(A->sell);
@@ -576,6 +617,6 @@ int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols) {
     A->A.w_nsb = 0;
     A->A.w_rng = nullptr;  // (inside the freed window allocation)
     A->A.kernel = A->rblk ? ahip::dev::kCsrStream : ahip::dev::kCsrVector;
-    analyse_window_sell(A, ncols);
+    if (analyse_window_sell(A, ncols) == -2) return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -35,9 +35,16 @@ struct arpack_hip_csr {
 // or, with *stale = true, if that communicator has been destroyed)
 const ahip::Comm* ahip_csr_dist_comm(const arpack_hip_csr* A, bool* stale);
 void ahip_dist_detach_csr(arpack_hip_dist* D);
+// the exchange form of a distribution (DistOp::Mode; 0 for the neighbour halo)
+int ahip_dist_mode(const arpack_hip_dist* D);
 
 // remap every column index c -> c - shift (int32) and rebuild the SpMV
 // analysis for an x vector of length ncols; 0 on success
 int ahip_csr_remap_cols(arpack_hip_csr* A, int64_t shift, int64_t ncols);
+// ghost-list form (general operators): own columns [row0, row0 + nloc) ->
+// c - row0, any other -> nloc + its index in `ghosts` (device, sorted, nghost);
+// x is then [nloc local | nghost ghosts]
+int ahip_csr_remap_ghost(arpack_hip_csr* A, int64_t row0, int64_t nloc, const int64_t* ghosts,
+                         int64_t nghost);
 // per-matrix [min col, max col] over all rows (device reduction)
 int ahip_csr_col_span(const arpack_hip_csr* A, int64_t* cmin, int64_t* cmax);

@@ -133,6 +133,7 @@ struct Workspace {
     LzState* st_host = nullptr;  // pinned mirror
     double* host_scratch = nullptr;  // pinned, >= 4*stride doubles
     double* host_hcol = nullptr;     // pinned ncv * ncv (ncv <= 64 only): H upload of a folded Arnoldi cycle
+    double* host_q = nullptr;        // pinned ncv * ncv (ncv <= 64 only): Q staging of V*Q
 };
 
 int choose_nblk(int64_t n);

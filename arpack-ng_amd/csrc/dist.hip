@@ -13,8 +13,59 @@ void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only, bool
 void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, int64_t nrecv,
                 hipStream_t s, bool p2p);
 
+namespace {
+__global__ void k_pack(int64_t m, const int32_t* __restrict__ idx, const double* __restrict__ x,
+                       double* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride)
+        out[k] = x[idx[k]];
+}
+__global__ void k_gather(int64_t m, const int64_t* __restrict__ g, const double* __restrict__ src,
+                         double* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride)
+        out[k] = src[g[k]];
+}
+inline unsigned grid_for_rows(int64_t m) {
+    const int64_t g = (m + 255) / 256;
+    return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+}  // namespace
+
+// The general operator's exchange (kGhostLists / kAllGather).  RCCL: the
+// packed ghost rows (or the whole block) in one group of send / recv.  The
+// host-staged rehearsal transport has only an allreduce for arbitrary
+// patterns: each rank contributes its block to a zeroed global x and the sum
+// is the gathered x (exact: one nonzero term per entry).
+static void exchange_general(const DistOp& D, hipStream_t s, bool p2p) {
+    if (!comm_is_host(D.comm)) {
+        if (D.mode == DistOp::kGhostLists && D.nsend > 0)
+            hipLaunchKernelGGL(k_pack, dim3(grid_for_rows(D.nsend)), dim3(256), 0, s, D.nsend, D.send_idx,
+                               D.x_mid(), D.send_buf);
+        comm_ghosts(D.comm, D, s, p2p);
+        return;
+    }
+    double* g = D.mode == DistOp::kGhostLists ? D.gbuf : D.x_ext;
+    if (D.mode == DistOp::kGhostLists) {
+        (void)hipMemsetAsync(g, 0, sizeof(double) * D.n_global, s);
+        dev::copy(s, D.nloc, D.x_mid(), g + D.row0);
+    } else {  // x_mid is in place: zero the other ranks' blocks
+        (void)hipMemsetAsync(g, 0, sizeof(double) * D.row0, s);
+        (void)hipMemsetAsync(g + D.row0 + D.nloc, 0, sizeof(double) * (D.n_global - D.row0 - D.nloc), s);
+    }
+    comm_allreduce_sum(D.comm, g, (int)D.n_global, s);
+    if (D.mode == DistOp::kGhostLists && D.halo_hi > 0)
+        hipLaunchKernelGGL(k_gather, dim3(grid_for_rows(D.halo_hi)), dim3(256), 0, s, D.halo_hi,
+                           D.ghost_glob, g, D.x_ext + D.nloc);
+}
+
 void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p) {
     if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
+    if (D.mode != DistOp::kHaloNeighbour) {
+        exchange_general(D, s, p2p);
+        dev::csr_spmv(s, *D.A, D.x_ext, y);
+        return;
+    }
     const dev::Csr& A = *D.A;
     const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val;
     comm_halo(D.comm, D, s, sym, p2p);
@@ -75,6 +126,139 @@ int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+using namespace ahip;
+
+void free_general(DistOp& o) {
+    for (void* p : {(void*)o.x_ext, (void*)o.send_idx, (void*)o.send_buf, (void*)o.ghost_glob,
+                    (void*)o.gbuf})
+        if (p) (void)hipFree(p);
+    o.x_ext = o.send_buf = o.gbuf = nullptr;
+    o.send_idx = nullptr;
+    o.ghost_glob = nullptr;
+}
+
+// in-place SUM allreduce of a host vector through the engine's communicator
+// (plan setup only); collective, agreed: false on every rank if any failed
+bool host_allreduce(const Comm* c, std::vector<double>& h) {
+    double* d = nullptr;
+    const size_t bytes = sizeof(double) * (h.empty() ? 1 : h.size());
+    bool ok = hipMalloc(&d, bytes) == hipSuccess;
+    if (!dist_all_ok(c, ok)) {
+        if (d) (void)hipFree(d);
+        return false;
+    }
+    ok = h.empty() || hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
+    if (!h.empty() && comm_allreduce_sum(c, d, (int)h.size(), nullptr) != 0) ok = false;
+    ok = ok && (h.empty() || hipMemcpy(h.data(), d, bytes, hipMemcpyDeviceToHost) == hipSuccess);
+    (void)hipFree(d);
+    return dist_all_ok(c, ok);
+}
+
+template <class T>
+bool upload(T** dst, const std::vector<T>& h) {
+    if (hipMalloc(dst, sizeof(T) * (h.empty() ? 1 : h.size())) != hipSuccess) {
+        *dst = nullptr;
+        return false;
+    }
+    return h.empty() || hipMemcpy(*dst, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+// Ghost plan of a general operator's row block (collective; SURVEY §8(e) "SpMV
+// exchange"): the sorted set of off-block columns this rank's rows read
+// (its ghosts), their owners, and -- through one allreduce of every rank's
+// ghost list -- the rows each peer needs from this rank.  Where the ghosts are
+// more than half of all off-block rows (a dense coupling, e.g. config 5's
+// random operator at small P) the lists do not pay and every rank gathers the
+// whole x (kAllGather; AHIP_DIST_ALLGATHER=1 forces it).
+int ghost_plan(arpack_hip_csr* A, DistOp& o, const Comm* c, int P, int r) {
+    const int64_t nloc = o.nloc, row0 = o.row0, nnz = A->A.nnz;
+    std::vector<int32_t> hc((size_t)nnz);
+    bool ok = nnz == 0 || hipMemcpy(hc.data(), A->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost) ==
+                              hipSuccess;
+    std::vector<int64_t> g;
+    if (ok) {
+        for (int32_t v : hc)
+            if (v < row0 || v >= row0 + nloc) g.push_back(v);
+        std::sort(g.begin(), g.end());
+        g.erase(std::unique(g.begin(), g.end()), g.end());
+    }
+    hc = std::vector<int32_t>();
+    if (!dist_all_ok(c, ok)) return -1;
+    auto owner = [&](int64_t col) {
+        return (int)(std::upper_bound(o.peer_row0.begin(), o.peer_row0.end(), col) - o.peer_row0.begin()) - 1;
+    };
+    // C[q * P + p]: ghosts of rank q owned by rank p
+    std::vector<double> C((size_t)P * P, 0.0);
+    for (int64_t v : g) C[(size_t)r * P + owner(v)] += 1.0;
+    if (!host_allreduce(c, C)) return -1;
+    double total = 0.0, possible = 0.0;
+    std::vector<int64_t> nghost(P, 0), seg(P + 1, 0);
+    for (int q = 0; q < P; ++q) {
+        for (int p = 0; p < P; ++p) nghost[q] += (int64_t)C[(size_t)q * P + p];
+        seg[q + 1] = seg[q] + nghost[q];
+        total += (double)nghost[q];
+        possible += (double)(o.n_global - o.peer_nloc[q]);
+    }
+    const char* fe = std::getenv("AHIP_DIST_ALLGATHER");
+    const bool want_ag = (fe && fe[0] == '1') || total > 0.5 * possible;
+    const bool all_gather = !dist_all_ok(c, !want_ag);  // any rank's wish, every rank's mode
+    if (all_gather) {
+        o.mode = DistOp::kAllGather;
+        o.halo_lo = row0;
+        o.halo_hi = o.n_global - row0 - nloc;
+        ok = hipMalloc(&o.x_ext, sizeof(double) * o.n_global) == hipSuccess &&
+             hipMemset(o.x_ext, 0, sizeof(double) * o.n_global) == hipSuccess;
+        // global column indices stay: x_ext is the whole x
+        ok = ok && ahip_csr_remap_cols(A, 0, o.n_global) == 0;
+        return dist_all_ok(c, ok) ? 0 : -1;
+    }
+    o.mode = DistOp::kGhostLists;
+    // every rank's sorted ghost list, back to back (rank q's at seg[q])
+    std::vector<double> lists((size_t)seg[P], 0.0);
+    for (size_t k = 0; k < g.size(); ++k) lists[(size_t)seg[r] + k] = (double)g[k];
+    if (!host_allreduce(c, lists)) return -1;
+    o.send_cnt.assign(P, 0);
+    o.send_off.assign(P, 0);
+    o.recv_cnt.assign(P, 0);
+    o.recv_off.assign(P, 0);
+    std::vector<int32_t> sidx;
+    for (int q = 0; q < P; ++q) {
+        // q's ghosts owned by me: a contiguous run of q's sorted list
+        int64_t at = seg[q];
+        for (int p = 0; p < r; ++p) at += (int64_t)C[(size_t)q * P + p];
+        const int64_t cnt = q == r ? 0 : (int64_t)C[(size_t)q * P + r];
+        o.send_off[q] = (int64_t)sidx.size();
+        o.send_cnt[q] = cnt;
+        for (int64_t k = 0; k < cnt; ++k) sidx.push_back((int32_t)((int64_t)lists[(size_t)(at + k)] - row0));
+    }
+    for (int q = 0, acc = 0; q < P; ++q) {
+        o.recv_off[q] = acc;
+        o.recv_cnt[q] = q == r ? 0 : (int64_t)C[(size_t)r * P + q];
+        acc += (int)o.recv_cnt[q];
+    }
+    lists = std::vector<double>();
+    o.nsend = (int64_t)sidx.size();
+    o.halo_lo = 0;
+    o.halo_hi = (int64_t)g.size();
+    const int64_t next = nloc + o.halo_hi;
+    ok = hipMalloc(&o.x_ext, sizeof(double) * (next > 0 ? next : 1)) == hipSuccess &&
+         hipMemset(o.x_ext, 0, sizeof(double) * (next > 0 ? next : 1)) == hipSuccess &&
+         upload(&o.send_idx, sidx) &&
+         hipMalloc(&o.send_buf, sizeof(double) * (o.nsend > 0 ? o.nsend : 1)) == hipSuccess &&
+         upload(&o.ghost_glob, g);
+    if (ok && comm_is_host(c)) ok = hipMalloc(&o.gbuf, sizeof(double) * o.n_global) == hipSuccess;
+    ok = ok && ahip_csr_remap_ghost(A, row0, nloc, o.ghost_glob, o.halo_hi) == 0;
+    return dist_all_ok(c, ok) ? 0 : -1;
+}
+}  // namespace
+
+int ahip_dist_mode(const arpack_hip_dist* D) { return D ? D->D.mode : 0; }
+
+extern "C" {
+
 int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_global,
                            int64_t row0) {
     using namespace ahip;
@@ -104,9 +288,34 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     if (!dist_all_ok(c, ok_tab)) return -1;
     int64_t plan[4];
     const int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
-    if (rc != 0) return rc;
+    // -4: some rank's columns reach past its neighbours' rows (a general
+    // operator): ghost lists or the all-gather instead of the slab halo
+    if (rc != 0 && rc != -4) return rc;
     auto* D = new arpack_hip_dist;
     DistOp& o = D->D;
+    for (int q = 0; q < P; ++q) {
+        o.peer_row0.push_back((int64_t)tab[4 * q]);
+        o.peer_nloc.push_back((int64_t)tab[4 * q + 1]);
+    }
+    if (rc == -4) {
+        o.n_global = n_global;
+        o.row0 = row0;
+        o.nloc = nloc;
+        o.comm = c;
+        o.comm_gen = comm_gen(c);
+        const int grc = ghost_plan(A, o, c, P, r);
+        if (grc != 0) {
+            free_general(o);
+            delete D;
+            return grc;
+        }
+        o.A = &A->A;
+        D->csr = A;
+        if (A->dist) A->dist->csr = nullptr;
+        A->dist = D;
+        *out = D;
+        return 0;
+    }
     o.n_global = n_global;
     o.row0 = row0;
     o.nloc = nloc;
@@ -174,9 +383,11 @@ int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y) {
 void arpack_hip_dist_destroy(arpack_hip_dist* D) {
     if (!D) return;
     if (D->csr) D->csr->dist = nullptr;  // the CSR is a plain (unsharded) operator again
-    (void)hipFree(D->D.x_ext);
+    free_general(D->D);
     delete D;
 }
+
+int arpack_hip_dist_mode(const arpack_hip_dist* D) { return D ? D->D.mode : -1; }
 
 int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
                          int64_t* send_lo, int64_t* send_hi) {

@@ -10,12 +10,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "device.hpp"
 
 namespace ahip {
 
 struct Comm;  // RCCL communicator (comm.cpp)
+struct DistOp;
 Comm* comm_get();
 int comm_rank(const Comm*);
 int comm_size(const Comm*);
@@ -31,6 +33,12 @@ bool comm_alive(const Comm* c, uint64_t gen);
 double* comm_flag(const Comm* c);
 // the communicator has its separate point-to-point communicator (RCCL, > 1 rank)
 bool comm_has_p2p(const Comm* c);
+// the host-staged transport (arpack_hip_comm_init_host) rather than RCCL
+bool comm_is_host(const Comm* c);
+// RCCL exchanges of the general distributed SpMV (grouped send / recv):
+// kGhostLists -- D.send_buf slices to each peer, ghosts into x_ext after the
+// local rows; kAllGather -- x_mid to every peer, every peer's block into x_ext
+void comm_ghosts(const Comm* c, const DistOp& D, hipStream_t s, bool p2p);
 // collective over the ranks of c: 1 if every rank passes ok_local != 0
 int dist_all_ok(const Comm* c, int ok_local);
 
@@ -48,6 +56,23 @@ struct DistOp {
     // row offset (the same iterates for every rank count); 1 = PARPACK's
     // per-rank stream (PARPACK/SRC/MPI/pdgetv0.f:234-245)
     int seed_mode = 0;
+    // exchange form: kHaloNeighbour -- banded operators whose
+    // columns reach at most the neighbouring ranks' rows (the slab exchange of
+    // PARPACK/EXAMPLES/MPI/pdsdrv1.f); kGhostLists -- any other operator: x_ext =
+    // [nloc local | halo_hi ghosts sorted by global column], each peer sends
+    // exactly the rows on its precomputed list (grouped send / recv);
+    // kAllGather -- ghost sets too dense to pay for lists: x_ext is the whole
+    // x (halo_lo = row0), every rank's block goes to every rank
+    enum Mode : int { kHaloNeighbour = 0, kGhostLists = 1, kAllGather = 2 };
+    int mode = kHaloNeighbour;
+    std::vector<int64_t> peer_row0, peer_nloc;        // every rank's block
+    std::vector<int64_t> send_cnt, send_off;          // kGhostLists: rows for each peer
+    std::vector<int64_t> recv_cnt, recv_off;          // ... and ghosts from each peer
+    int32_t* send_idx = nullptr;   // device: local rows packed for the peers, in rank order
+    double* send_buf = nullptr;    // device: the packed values
+    int64_t nsend = 0;
+    int64_t* ghost_glob = nullptr; // device: global column of each ghost
+    double* gbuf = nullptr;        // device, n_global: host-transport staging of kGhostLists
     double* x_mid() const { return x_ext + halo_lo; }
 };
 

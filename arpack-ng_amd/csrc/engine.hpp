@@ -136,6 +136,8 @@ public:
     // workl offsets (0-based) of h, ritz (ritzr), ritzi, bounds, q, w
     int ih = 0, iritz = 0, iritzi = 0, ibounds = 0, iq = 0, iw = 0;
     double rnorm = 0.0;  // host copy of dsaup2's rnorm
+    bool rnorm_stale = false;  // rnorm lives only on the device until the next cycle ends
+    std::vector<double> hcol_h;  // Arnoldi: the cycle's new H columns, downloaded with the state
     // machine constants of the family (convergence tests, tol <= 0 default)
     double eps = Prec<R>::eps, safmin = Prec<R>::safmin;
     // float family: the double shadow of the caller's workl (workl points here)

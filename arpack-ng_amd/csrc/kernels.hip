@@ -811,6 +811,7 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
         return e;
     if (ncv <= 64 && (e = hipHostMalloc(&ws.host_hcol, sizeof(double) * (size_t)ncv * ncv))) return e;
+    if (ncv <= 64 && (e = hipHostMalloc(&ws.host_q, sizeof(double) * (size_t)ncv * ncv))) return e;
     memset(ws.st_host, 0, sizeof(LzState));
     {   // test hook: exercise the (rare) second DGKS refinement on every step
         const char* e = getenv("AHIP_FORCE_DGKS2");
@@ -833,6 +834,7 @@ void ws_destroy(Workspace& ws) {
     if (ws.st_host) (void)hipHostFree(ws.st_host);
     if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
     if (ws.host_hcol) (void)hipHostFree(ws.host_hcol);
+    if (ws.host_q) (void)hipHostFree(ws.host_q);
     ws = Workspace{};
 }
 

@@ -164,6 +164,10 @@ Task SolverT<R>::run_ns() {
         } else {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
         }
+        if (free_run && bmat != 'G') {  // the next cycle queues behind V*Q (see run())
+            rnorm_stale = true;
+            continue;
+        }
         read_state();  // (a failure here is caught by the next cycle's check)
         rnorm = ws.st_host->rnorm;
     }

@@ -305,7 +305,10 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     const bool bI = (bmat == 'I');
     iinfo = 0;
     int j = k + 1;
-    bool restart_pending = !(rnorm > 0.0);
+    // rnorm_stale: the restart's rnorm was left on the device (run()); a zero
+    // there parks the cycle at its first step (k_place: st.abort = 1)
+    bool restart_pending = !rnorm_stale && !(rnorm > 0.0);
+    rnorm_stale = false;
     int rstart_j = -1;  // step at which a restart happened (h(j,1) = 0)
     // Chained steps (free-running engine, bmat = 'I', ncv <= 64): step j's DGKS
     // sweep also stores its residual r as the RAW column V(:,j+1) (and the x of a
@@ -504,6 +507,16 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 if (!(rnorm > 0.0)) restart_pending = true;
             }
         }
+        // the new steps' T / H records travel with the state: one host sync
+        // for both (the abort paths below loop back and fetch them again)
+        double* rec_h = ws.host_scratch;
+        a.ck(hipMemcpyAsync(rec_h, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost,
+                            a.stream));
+        if (arnoldi) {
+            hcol_h.resize((size_t)ncv * npk);
+            a.ck(hipMemcpyAsync(hcol_h.data(), ws.hcol + (size_t)k * ncv, sizeof(double) * hcol_h.size(),
+                                hipMemcpyDeviceToHost, a.stream));
+        }
         read_state();
         if (check_halt()) co_return;  // run() ends the solve with info = -9999
         // a park inside a folded cycle leaves resid = r of the step before the
@@ -554,21 +567,17 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     g_stats.nitref += ws.st_host->nitref;
     ws.st_host->nrorth = ws.st_host->nitref = 0;
     write_state();
-    // assemble the new columns of H from the per-step device records
-    double* rec = ws.host_scratch;
-    a.ck(hipMemcpyAsync(rec, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost, a.stream));
+    // assemble the new columns of H from the per-step device records (on the
+    // host since the cycle-end sync above)
+    const double* rec = ws.host_scratch;
     double* h = workl + ih;
     if (!arnoldi) {  // T(ncv,2): h(:,1) subdiagonal, h(:,2) diagonal
-        a.sync();
         for (int jj = k + 1; jj <= k + npk; ++jj) {
             h[(jj - 1) + ncv] = rec[2 * (jj - 1)];
             h[jj - 1] = rec[2 * (jj - 1) + 1];
         }
     } else {  // H(ncv,ncv): h(1:j,j) from the device, h(j,j-1) = beta_j (SRC/dnaitr.f:566-590)
-        std::vector<double> hc((size_t)ncv * npk);
-        a.ck(hipMemcpyAsync(hc.data(), ws.hcol + (size_t)k * ncv, sizeof(double) * hc.size(),
-                          hipMemcpyDeviceToHost, a.stream));
-        a.sync();
+        const std::vector<double>& hc = hcol_h;
         for (int jj = k + 1; jj <= k + npk; ++jj) {
             double* col = h + (size_t)(jj - 1) * ncv;
             std::memcpy(col, hc.data() + (size_t)(jj - 1 - k) * ncv, sizeof(double) * jj);
@@ -609,13 +618,12 @@ template <class R>
 void SolverT<R>::vq_device(int kev, int kplusp, double sigmak, double betak) {
     const double* q = workl + iq;
     // Q(:,1:kev+1) compact (ld = kplusp). ncv <= 64: staged in the pinned
-    // ws.host_hcol (ncv^2 >= kplusp (kev+1)), so the copy is asynchronous and
-    // the kFinNorm finalize queues behind V*Q without a host wait; the buffer
-    // is free again at the read_state() sync that follows every restart (its
-    // next writer is the folded Arnoldi cycle's H upload in saitr).
+    // ws.host_q (ncv^2 >= kplusp (kev+1)), so the copy is asynchronous and the
+    // kFinNorm finalize and the next cycle queue behind V*Q without a host
+    // wait; its next writer is the next restart, after that cycle's end sync.
     const size_t m = (size_t)kplusp * (kev + 1);
     std::vector<double> qvec;
-    double* qbuf = ws.host_hcol;
+    double* qbuf = ws.host_q;
     if (!qbuf) {
         qvec.resize(m);
         qbuf = qvec.data();
@@ -624,7 +632,7 @@ void SolverT<R>::vq_device(int kev, int kplusp, double sigmak, double betak) {
         for (int r = 0; r < kplusp; ++r) qbuf[(size_t)c * kplusp + r] = q[r + (size_t)c * ncv];
     a.ck(hipMemcpyAsync(ws.q, qbuf, sizeof(double) * m, hipMemcpyHostToDevice, a.stream));
     dev::vq_update(ws, n, a.d_v, a.d_ld, kplusp, kev, sigmak, betak, a.d_resid);
-    if (!ws.host_hcol) a.sync();  // pageable qvec: its lifetime
+    if (!ws.host_q) a.sync();  // pageable qvec: its lifetime
 }
 
 template <class R>
@@ -753,6 +761,14 @@ Task SolverT<R>::run() {
             fin(1, dev::kFinNorm, 0, 0, -1);
         } else {
             fin(1, dev::kFinNorm, 0, 0, -1);  // r'r partials came with V*Q
+        }
+        if (free_run && bmat != 'G') {
+            // no host round trip between V*Q and the next cycle: its steps are
+            // enqueued behind the kFinNorm finalize, which leaves rnorm on the
+            // device (rnorm_stale; saitr).  A failure is caught by that
+            // cycle's check.
+            rnorm_stale = true;
+            continue;
         }
         read_state();  // (a failure here is caught by the next cycle's check)
         rnorm = ws.st_host->rnorm;

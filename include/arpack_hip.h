@@ -397,11 +397,15 @@ int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn
 typedef struct arpack_hip_dist arpack_hip_dist;
 /* Distributed operator from this rank's CSR rows [row0, row0 + A.n) with GLOBAL
  * column indices: computes the halo plan with the other ranks (collective) and
- * remaps A's columns to the local extended-x layout.  Returns 0; -3/-4 if the
- * row blocks are not contiguous or a halo reaches beyond the neighbours; -1 on
- * every rank if any rank fails to set up.  A CSR declared symmetric before this
- * call keeps symmetric storage only if every rank declared it and every rank's
- * symmetric plan succeeds; otherwise all ranks run full storage. */
+ * remaps A's columns to the local extended-x layout.  A banded operator (every
+ * rank's columns within its neighbours' rows) exchanges slab halos with the
+ * neighbours; any other operator gets per-peer ghost lists (each rank receives
+ * exactly the off-block x entries its rows read: grouped send / recv), or,
+ * where the ghosts exceed half of the off-block rows, an all-gather of x.
+ * Returns 0; -3 if the row blocks are not contiguous; -1 on every rank if any
+ * rank fails to set up.  A CSR declared symmetric before this call keeps
+ * symmetric storage only for a banded operator, if every rank declared it and
+ * every rank's symmetric plan succeeds; otherwise all ranks run full storage. */
 int arpack_hip_dist_create(arpack_hip_dist** D, arpack_hip_csr* A, int64_t n_global, int64_t row0);
 void arpack_hip_dist_destroy(arpack_hip_dist* D);
 /* y = A x on this rank's rows (device pointers), collective over the ranks:
@@ -410,6 +414,9 @@ void arpack_hip_dist_destroy(arpack_hip_dist* D);
 int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y);
 int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* halo_hi,
                          int64_t* send_lo, int64_t* send_hi);
+/* Exchange form: 0 neighbour halos, 1 ghost lists (halo_hi = ghosts), 2
+ * all-gather (halo_lo / halo_hi = the rows before / after this rank's). */
+int arpack_hip_dist_mode(const arpack_hip_dist* D);
 /* Row-block decomposition without an operator: rank owns rows [row0, row0+nloc)
  * of the global n_global (collective-free; needs arpack_hip_comm_init). */
 int arpack_hip_dist_rows(arpack_hip_dist** D, int64_t nloc, int64_t row0, int64_t n_global);

@@ -15,7 +15,9 @@ CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
       sym_rci (pdsaupd_c with the caller's OP on its rows, halo via all_gather),
       lap3d (FIXTURE m<m>_cap<k>: config 4's 3-D Laplacian, capped run),
       fault_csr / fault_rci (sym_csr / sym_rci with a HIP failure injected on
-      rank 1 only: every rank must end with info = -9999).
+      rank 1 only: every rank must end with info = -9999),
+      general (FIXTURE sparse | dense: an operator that is not banded -- ghost
+      lists / all-gather exchange).
 Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
 import os
 import sys
@@ -103,6 +105,58 @@ def sym_mixed(pkg, out, rank, world):
     del D
 
 
+def general_matrix(kind, n=12000):
+    """A symmetric operator whose rows reach ranks beyond the neighbours:
+    "sparse" -- a band of half-width 30 plus n/10 random long-range pairs (ghost
+    lists pay); "dense" -- 8 random columns a row, symmetrised (every off-block
+    row is read: the all-gather)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(11)
+    if kind == "sparse":
+        B = sp.diags([np.full(n - abs(k), 1.0 / (1 + abs(k))) for k in range(-30, 31)],
+                     list(range(-30, 31)), shape=(n, n), format="csr")
+        i, j = rng.integers(0, n, n // 10), rng.integers(0, n, n // 10)
+        R = sp.csr_matrix((rng.standard_normal(n // 10), (i, j)), shape=(n, n))
+    else:
+        B = sp.csr_matrix((n, n))
+        i = np.repeat(np.arange(n), 8)
+        R = sp.csr_matrix((rng.standard_normal(8 * n), (i, rng.integers(0, n, 8 * n))), shape=(n, n))
+    A = (B + R + R.T + sp.diags(np.linspace(1.0, 40.0, n))).tocsr()
+    A.sum_duplicates()
+    A.sort_indices()
+    return A
+
+
+def general(pkg, out, rank, world, kind):
+    """VERDICT r03 missing #2: the distributed device OP of an operator that is
+    not banded (ghost lists / all-gather): one distributed SpMV against SciPy
+    on the rank's rows, then dsaupd LA nev 6 ncv 20 tol 1e-10 from a fixed v0."""
+    A = general_matrix(kind)
+    n = A.shape[0]
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    nloc = r1 - r0
+    B = pkg.CSR.from_arrays(A.indptr[r0:r1 + 1].astype(np.int64) - A.indptr[r0],
+                            A.indices[A.indptr[r0]:A.indptr[r1]].astype(np.int32),
+                            A.data[A.indptr[r0]:A.indptr[r1]].copy())
+    D = pkg.DistOp(B, n, r0)
+    x = np.random.default_rng(3).standard_normal(n)
+    xd = pkg.DeviceBuffer.from_numpy(x[r0:r1].copy())
+    yd = pkg.DeviceBuffer(nloc)
+    D.matvec_device(xd, yd)
+    want = A[r0:r1] @ x
+    scale = abs(A[r0:r1]) @ np.abs(x)
+    spmv_err = float(np.max(np.abs(yd.numpy() - want) / scale))
+    v0 = np.linspace(-1.0, 1.0, n)[r0:r1].copy()
+    s = pkg.SymRci(nloc, 6, 20, "LA", 1e-10, mxiter=300, v0=v0, device=True)
+    assert pkg.pdsaupd_cycles(s, D, -1) == 99
+    d, z, nconv = s.eupd(dist=D)
+    z = z.numpy() if hasattr(z, "numpy") else z
+    np.savez(os.path.join(out, "rank%d.npz" % rank), iparam=s.iparam.copy(), info=s.info.copy(),
+             d=d, spmv_err=np.array([spmv_err]), mode=np.array([D.mode]),
+             ghosts=np.array([D.info()["halo_hi"]]), z=z.reshape(6, nloc)[:nconv].T.copy())
+    del D
+
+
 def lap3d(pkg, out, rank, world, m, cap):
     """BASELINE config 4's family at a rehearsal size: the 3-D 7-pt Laplacian
     m^3 sharded by row blocks (z-slabs: the halo is one m x m plane per side,
@@ -135,10 +189,12 @@ def main():
     dist.init_process_group("gloo")
     pkg = load_pkg()
     pkg.comm_init_host(world, rank, device=0)
-    if case in ("spmv_chain", "sym_mixed", "lap3d"):
+    if case in ("spmv_chain", "sym_mixed", "lap3d", "general"):
         if case == "lap3d":  # FIXTURE = "m<m>_cap<cycles>"
             m, cap = (int(t[1:]) if t[0] == "m" else int(t[3:]) for t in fixture.split("_"))
             lap3d(pkg, out, rank, world, m, cap)
+        elif case == "general":  # FIXTURE = sparse | dense
+            general(pkg, out, rank, world, fixture)
         else:
             (spmv_chain if case == "spmv_chain" else sym_mixed)(pkg, out, rank, world)
         dist.barrier()
