@@ -287,9 +287,14 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     (void)hipFree(d);
     if (!dist_all_ok(c, ok_tab)) return -1;
     int64_t plan[4];
-    const int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
+    int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
     // -4: some rank's columns reach past its neighbours' rows (a general
-    // operator): ghost lists or the all-gather instead of the slab halo
+    // operator): ghost lists or the all-gather instead of the slab halo.  A
+    // valid slab halo wider than half the block (a few long-range entries
+    // stretch the column span of a sparse coupling; a band is far narrower:
+    // the north star's 4096 rows against a 1.25e6-row share) goes to the
+    // general plan too, on every rank if on any.
+    if (rc == 0 && P > 1 && !dist_all_ok(c, 2 * (plan[0] + plan[1]) <= nloc)) rc = -4;
     if (rc != 0 && rc != -4) return rc;
     auto* D = new arpack_hip_dist;
     DistOp& o = D->D;

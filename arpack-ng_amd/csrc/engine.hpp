@@ -138,6 +138,7 @@ public:
     double rnorm = 0.0;  // host copy of dsaup2's rnorm
     bool rnorm_stale = false;  // rnorm lives only on the device until the next cycle ends
     std::vector<double> hcol_h;  // Arnoldi: the cycle's new H columns, downloaded with the state
+    R* ybuf = nullptr;  // free-running: OP's y on 128-B lines when workd(irj) is not (saitr)
     // machine constants of the family (convergence tests, tol <= 0 default)
     double eps = Prec<R>::eps, safmin = Prec<R>::safmin;
     // float family: the double shadow of the caller's workl (workl points here)

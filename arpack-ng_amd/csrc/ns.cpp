@@ -179,6 +179,7 @@ fault:  // a failed HIP call: the device state is not trustworthy (see sym.cpp)
     mxiter = iter;
     info = -9999;
 fail:
+    if (ybuf) dev::copy(a.stream, n, ybuf, a.d_workd + n);  // workd(irj) = the last OP x (saitr)
     iparam[2] = mxiter;
     co_return;
 }

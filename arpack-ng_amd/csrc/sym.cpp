@@ -124,6 +124,7 @@ SolverT<R>::~SolverT() {
     if (x_ev) (void)hipEventDestroy(x_ev);
     if (y_ev) (void)hipEventDestroy(y_ev);
     if (op_stream) (void)hipStreamDestroy(op_stream);
+    if (ybuf) (void)hipFree(ybuf);
     root.reset();
     dev::ws_destroy(ws);
     a.release();
@@ -304,6 +305,15 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
     const int64_t ipj = 0, irj = nn, ivj = 2 * nn;
     const bool bI = (bmat == 'I');
     iinfo = 0;
+    // OP's output y = workd(irj): at ARPACK's fixed offset n, off the 128-B
+    // lines when n is odd (config 4: n = 215^3), which costs every pass that
+    // streams it.  The free-running engine, whose caller never sees
+    // y between requests, keeps it in an aligned vector of its own instead and
+    // copies it to workd(irj) when the solve ends (run()).
+    if (free_run && bI && !ybuf && (reinterpret_cast<uintptr_t>(wd + irj) & 127) != 0 &&
+        hipMalloc(&ybuf, sizeof(R) * (size_t)nn) != hipSuccess)
+        ybuf = nullptr;
+    R* const yv = (free_run && bI && ybuf) ? ybuf : wd + irj;
     int j = k + 1;
     // rnorm_stale: the restart's rnorm was left on the device (run()); a zero
     // there parks the cycle at its first step (k_place: st.abort = 1)
@@ -408,7 +418,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                            bI ? nullptr : wd + ipj, j);
             // STEP 3: r_j = OP*v_j (SRC/dsaitr.f:461-474)
             g_stats.nopx += 1;
-            co_await op(1, ivj, irj, ipj, xop, wd + irj);
+            co_await op(1, ivj, irj, ipj, xop, yv);
             // STEP 4: B*OP*v_j (skipped in mode 2: WORKD(IVJ) holds A*v_j)
             const R* u;
             if (mode == 2 && !arnoldi) {  // dsaitr only; dnaitr has no mode-2 shortcut
@@ -418,14 +428,14 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 co_await rci(2, irj, ipj);
                 u = wd + ipj;
             } else {
-                u = wd + irj;
+                u = yv;
             }
             // wnorm and the CGS coefficients h = V_j' B r (SRC/dsaitr.f:538-594)
             if (folded) {  // + forms r' = V(:,j) and A r' (see fold_ok)
                 dev::fold_dots(ws, nn, j, a.d_v, a.d_ld, a.d_resid, u);
                 fin(j + 1, dev::kFinCgsFolded, j, rstart, -1, 1, rstart_prev);
             } else {
-                dev::dots(ws, nn, j, a.d_v, a.d_ld, u, wd + irj, -1);
+                dev::dots(ws, nn, j, a.d_v, a.d_ld, u, yv, -1);
                 if (chained)  // + the deferred refinement decision of step j-1 (region 2)
                     fin(j + 1, dev::kFinCgsChained, j, rstart, -1, j, rstart_prev);
                 else
@@ -437,7 +447,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
             // a folded next step's SpMV reads r from resid, or from the
             // distributed operator's x window
             if (folded) {
-                dev::fold_update(ws, nn, j, a.d_v, a.d_ld, wd + irj, a.d_resid,
+                dev::fold_update(ws, nn, j, a.d_v, a.d_ld, yv, a.d_resid,
                                  next_folded ? dist_x() : nullptr);
                 // the next step's SpMV input (the distributed x window) is
                 // complete here: its halo + SpMV may overlap this step's finalize
@@ -447,7 +457,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 dev::UpdateChain<R> x;
                 x.chained = chained;
                 if (next_folded) x.raw2 = dist_x();
-                dev::update(ws, nn, j, a.d_v, a.d_ld, 0, wd + irj, a.d_resid, bI, -1, x);
+                dev::update(ws, nn, j, a.d_v, a.d_ld, 0, yv, a.d_resid, bI, -1, x);
             }
             if (bI && next_folded) {
                 fin(j + 1, dev::kFinPostCgsFold, j, rstart, -1);  // + t = T s, st.fold
@@ -779,6 +789,7 @@ fault:  // a failed HIP call: the device state is not trustworthy
         info = -9999;
     }
 done:
+    if (ybuf) dev::copy(a.stream, n, ybuf, a.d_workd + n);  // workd(irj) = the last OP x (saitr)
     nev0 = nev;
     iparam[2] = mxiter;
     co_return;

@@ -39,9 +39,15 @@ using namespace zc;
 constexpr int kT = 256;      // threads a block
 constexpr int kMaxBlk = 512;  // blocks of the vector kernels (partials per slot)
 
+// a / b by Smith's algorithm (as the host kit's zla::cdiv): no overflow or
+// underflow of |b|^2 for b's components near the range limits
 __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
-    const double d = b.x * b.x + b.y * b.y;
-    return make_double2((a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d);
+    if (fabs(b.x) < fabs(b.y)) {
+        const double ratio = b.x / b.y, denom = b.x * ratio + b.y;
+        return make_double2((a.x * ratio + a.y) / denom, (a.y * ratio - a.x) / denom);
+    }
+    const double ratio = b.y / b.x, denom = b.y * ratio + b.x;
+    return make_double2((a.y * ratio + a.x) / denom, (a.y - a.x * ratio) / denom);
 }
 
 // per-thread accumulators -> one partial per slot for this block
