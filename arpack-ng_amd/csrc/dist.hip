@@ -294,7 +294,10 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     // stretch the column span of a sparse coupling; a band is far narrower:
     // the north star's 4096 rows against a 1.25e6-row share) goes to the
     // general plan too, on every rank if on any.
-    if (rc == 0 && P > 1 && !dist_all_ok(c, 2 * (plan[0] + plan[1]) <= nloc)) rc = -4;
+    // (AHIP_DIST_GHOSTS=0: a valid slab halo is always kept)
+    const char* gv = std::getenv("AHIP_DIST_GHOSTS");
+    const bool price = !(gv && gv[0] == '0');
+    if (rc == 0 && P > 1 && price && !dist_all_ok(c, 2 * (plan[0] + plan[1]) <= nloc)) rc = -4;
     if (rc != 0 && rc != -4) return rc;
     auto* D = new arpack_hip_dist;
     DistOp& o = D->D;

@@ -483,7 +483,9 @@ def main():
                      # the per-kernel profile is not the timed cycles themselves:
                      # later cycles run more Lanczos steps per cycle as nev grows
                      "profiled_cycles": prof_cycles,
-                     "profiled_steps_per_cycle": (cnt / pk) if cnt and not args.no_profile else None,
+                     # (one V*Q a restart: a solve that converges inside the
+                     # profiled window runs fewer than requested)
+                     "profiled_steps_per_cycle": (cnt / prof["vq"][2]) if cnt and prof["vq"][2] else None,
                      "timed_steps_per_cycle": nopx / args.steps,
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
