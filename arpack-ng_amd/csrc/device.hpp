@@ -109,6 +109,23 @@ enum FinPhase : int {
                            // h(j,2) += the last one (refine_decision's take path)
 };
 
+// Arguments of one single-block finalize (finalize.hpp finalize_block).
+struct FinArgs {
+    const double* part;
+    int nblk, from_sums, m, phase, j, rstart, gate;
+    double* sums;
+    double* coef;
+    int cstride;
+    double* rec;
+    LzState* st;
+    double* hcol;
+    int hld;
+    const double* part2;
+    int m2, rstart_prev;
+    int hs;      // the Arnoldi fold's H-staging variant
+    int active;  // 0: nothing to run
+};
+
 struct Workspace {
     hipStream_t stream = nullptr;
     int nblk = 0;        // partial-sum blocks for this n
@@ -188,8 +205,13 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
 // from_sums: the m sums are already in ws.sums (reduced across ranks).
 // m2 > 0 (kFinCgsChained): a second region of m2 partial slots at
 // ws.part + nblk * stride (the deferred DGKS sums of step j-1).
+// defer: do not launch it -- the next symmetric SpMV on ws.stream runs it in
+// its combine kernel's workgroup 0 (one launch fewer a step); any other
+// launcher of csr_spmv, and every stream sync of the engine, flushes it first.
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
-              bool from_sums = false, int m2 = 0, int rstart_prev = 0);
+              bool from_sums = false, int m2 = 0, int rstart_prev = 0, bool defer = false);
+bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds);
+void flush_deferred_finalize(hipStream_t s);
 // resid = 0 if st.zero
 template <class R>
 void zero_if(const Workspace& ws, int64_t n, R* r);

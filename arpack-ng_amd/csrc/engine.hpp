@@ -164,7 +164,8 @@ private:
     RciAwait op(int ido, int64_t x, int64_t y, int64_t bx, const R* xp, R* yp);
     void read_state();
     void write_state();
-    void fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m2 = 0, int rstart_prev = 0);
+    void fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m2 = 0, int rstart_prev = 0,
+             bool defer = false);
     R* vcol(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based column
     R* dist_x();  // the distributed operator's x window (double only)
     void dgks2_tail(int j, int rstart);

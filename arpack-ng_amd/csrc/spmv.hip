@@ -1007,6 +1007,9 @@ static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y,
 }
 
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+    // a finalize deferred into the symmetric SpMV's combine: the other forms
+    // have no combine launch to carry it
+    if (!(A.kernel == kCsrSymSell && A.ss_val)) flush_deferred_finalize(s);
     if (A.kernel == kCsrSymSell && A.ss_val) {
         csr_spmv_sym(s, A, x, y);
         return;

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "device.hpp"
+#include "finalize.hpp"
 
 namespace ahip::dev {
 
@@ -385,6 +386,27 @@ __global__ __launch_bounds__(1024) void k_ssell_combine(const int64_t* __restric
     for (int i = threadIdx.x; i < pre; i += 1024) y[r0 + i] = lo[off + i] + hi[off + i];
 }
 
+// The same combine carrying a deferred finalize of the Lanczos step
+// (kernels.hip finalize(..., defer)): workgroup 0 runs it after its rows.  It
+// reads the partial sums of the pass before the SpMV and writes the step
+// state the pass after it reads -- both across kernel boundaries -- and
+// touches nothing of the SpMV, so the launch it saves (~6 us of a 60-500 us
+// SpMV) costs no ordering.
+template <bool HS>
+__global__ __launch_bounds__(1024) void k_ssell_combine_fin(const int64_t* __restrict__ sb_r0,
+                                                           const int32_t* __restrict__ sb_pre,
+                                                           const int64_t* __restrict__ sb_off,
+                                                           const double* __restrict__ lo,
+                                                           const double* __restrict__ hi,
+                                                           double* __restrict__ y, int chain,
+                                                           FinArgs fa) {
+    const int64_t b = (int64_t)blockIdx.x * chain;
+    const int pre = sb_pre[b];
+    const int64_t off = sb_off[b], r0 = sb_r0[b];
+    for (int i = threadIdx.x; i < pre; i += 1024) y[r0 + i] = lo[off + i] + hi[off + i];
+    if (blockIdx.x == 0) finalize_block<HS>(fa);
+}
+
 }  // namespace
 
 // Superblock plan from the per-row largest upper column cmax[i] (>= i).
@@ -675,9 +697,21 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
 void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
-    if (A.ss_ncomb > 0)
+    if (A.ss_ncomb <= 0) {
+        flush_deferred_finalize(s);
+        return;
+    }
+    FinArgs fa{};
+    size_t lds = 0;
+    if (!take_deferred_finalize(s, &fa, &lds)) {
         AHIP_LAUNCH(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
-                           A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
+                    A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
+        return;
+    }
+    // the step's deferred finalize rides in this launch (workgroup 0)
+    AHIP_LAUNCH(fa.hs ? k_ssell_combine_fin<true> : k_ssell_combine_fin<false>, dim3((unsigned)nch),
+                dim3(1024), lds, s, A.ss_sb_r0, A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain,
+                fa);
 }
 
 void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {

@@ -112,7 +112,10 @@ void ArraysT<R>::download_all() {
 }
 
 template <class R>
-void ArraysT<R>::sync() { ck(hipStreamSynchronize(stream)); }
+void ArraysT<R>::sync() {
+    dev::flush_deferred_finalize(stream);  // (none outlives a sync)
+    ck(hipStreamSynchronize(stream));
+}
 
 // ------------------------------------------------------------- Solver ---
 
@@ -197,18 +200,20 @@ R* SolverT<R>::dist_x() {
 // Finalize of a reduction; with a multi-GPU distribution the local sums are
 // allreduced across ranks (one RCCL collective) before the phase logic runs.
 template <class R>
-void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m2, int rstart_prev) {
+void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m2, int rstart_prev,
+                     bool defer) {
     if (dist && dist->comm) {
         dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate, false, m2);
         comm_allreduce_sum(dist->comm, ws.sums, m + m2, a.stream);
         if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true, m2, rstart_prev);
     } else {
-        dev::finalize(ws, m, ph, j, rstart, gate, false, m2, rstart_prev);
+        dev::finalize(ws, m, ph, j, rstart, gate, false, m2, rstart_prev, defer);
     }
 }
 
 template <class R>
 void SolverT<R>::read_state() {
+    dev::flush_deferred_finalize(a.stream);
     a.ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
@@ -460,7 +465,9 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
                 dev::update(ws, nn, j, a.d_v, a.d_ld, 0, yv, a.d_resid, bI, -1, x);
             }
             if (bI && next_folded) {
-                fin(j + 1, dev::kFinPostCgsFold, j, rstart, -1);  // + t = T s, st.fold
+                // + t = T s, st.fold; free-running, the next step's SpMV follows at
+                // once and carries it (the symmetric SpMV's combine launch)
+                fin(j + 1, dev::kFinPostCgsFold, j, rstart, -1, 0, 0, free_run);
                 chained = false;
                 folded = true;
                 rstart_prev = rstart;
@@ -520,6 +527,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
         // the new steps' T / H records travel with the state: one host sync
         // for both (the abort paths below loop back and fetch them again)
         double* rec_h = ws.host_scratch;
+        dev::flush_deferred_finalize(a.stream);
         a.ck(hipMemcpyAsync(rec_h, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost,
                             a.stream));
         if (arnoldi) {
