@@ -609,6 +609,7 @@ static int reanalyse(arpack_hip_csr* A, int64_t ncols) {
     if (A->symsell) (void)hipFree(A->symsell);
     A->symsell = nullptr;
     A->A.ss_val = nullptr;
+    A->A.ss_pair = nullptr;
     if (A->A.w_colw) (void)hipFree((void*)A->A.w_colw);
     A->A.w_colw = nullptr;
     A->win = nullptr;

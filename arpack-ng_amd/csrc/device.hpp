@@ -210,7 +210,10 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
 // launcher of csr_spmv, and every stream sync of the engine, flushes it first.
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
               bool from_sums = false, int m2 = 0, int rstart_prev = 0, bool defer = false);
-bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds);
+// (false, and the finalize stays deferred, when it needs more than max_lds bytes
+// of LDS or the H-column staging and allow_hs is false)
+bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds, size_t max_lds = (size_t)-1,
+                            bool allow_hs = true);
 void flush_deferred_finalize(hipStream_t s);
 // resid = 0 if st.zero
 template <class R>
@@ -299,6 +302,7 @@ struct Csr {
     // ss_wg0[b * 16 + q] (nsb * 16 + 1 entries) inside slice ss_wsl[b * 16 + q]
     const int64_t* ss_wg0 = nullptr;
     const int32_t* ss_wsl = nullptr;
+    int* ss_pair = nullptr;  // per-chain pair counters of the fused combine (zero between launches)
     double* ss_lo = nullptr;              // spill partials (written by superblock b-1)
     double* ss_hi = nullptr;               // prefix partials (written by superblock b)
     int64_t ss_nsb = 0, ss_nnz = 0, ss_padded = 0, ss_ncomb = 0;

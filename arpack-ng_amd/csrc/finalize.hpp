@@ -13,6 +13,23 @@
 namespace ahip::dev {
 namespace {
 
+constexpr int kFoldRecMax = 2 * 66;  // T records staged for the fold's t (j <= 64)
+constexpr int kFoldHMax = 64;        // HS: H(0:j, 0:j) staged for the Arnoldi fold's t = H s
+
+// The finalize's workgroup-shared state, in LDS the launch provides (dynamic
+// LDS of k_finalize / the combine kernel, or a window of the SpMV kernel that
+// carries a deferred finalize): the state copy, the fold's T records, the
+// decisions, then the m + m2 sums.
+struct FinLds {
+    LzState st;
+    double rec[kFoldRecMax];
+    int take, take2, go, pad_;
+    double sum[1];  // m + m2 doubles from here
+};
+__host__ __device__ constexpr size_t fin_lds_bytes(int mt) {
+    return sizeof(FinLds) + sizeof(double) * (size_t)(mt > 1 ? mt - 1 : 0);
+}
+
 // One refinement decision (SRC/dsaitr.f:634-781) on the sums of [V'r ; r'r]
 // (jm = index of r'r) for step jj; returns `take` (which coefficient slot the
 // next sweep uses, 0 for none).  Thread 0 only.
@@ -72,10 +89,10 @@ __device__ int refine_decision(int phase, const double* ss, int jm, int jj, int 
 // publishes s_sum.
 __device__ __forceinline__ void fin_sums(const double* __restrict__ part, int nblk, int from_sums,
                                          int m, const double* __restrict__ sums,
-                                         const double* __restrict__ part2, int m2) {
-    // the m + m2 (<= 2 ncv + 4) sums are staged in dynamic LDS sized by the
-    // launch, so any ncv the argument checks accept fits
-    extern __shared__ double s_sum[];
+                                         const double* __restrict__ part2, int m2,
+                                         double* s_sum) {
+    // the m + m2 (<= 2 ncv + 4) sums are staged in LDS sized by the launch, so
+    // any ncv the argument checks accept fits
     const int nt = blockDim.x;
     const int mt = m + m2;
     if (from_sums) {  // already reduced (and allreduced across ranks) in `sums`
@@ -105,9 +122,13 @@ __device__ __forceinline__ void fin_body(int m, int phase, int j, int rstart,
                                          double* __restrict__ sums, double* __restrict__ coef,
                                          int cstride, double* __restrict__ rec, LzState* st,
                                          double* __restrict__ hcol, int hld, int m2,
-                                         int rstart_prev, double* s_rec,
+                                         int rstart_prev, FinLds* L,
                                          const double* s_h = nullptr) {
-    extern __shared__ double s_sum[];
+    double* const s_sum = L->sum;
+    double* const s_rec = L->rec;
+    int& s_take2 = L->take2;
+    int& s_go = L->go;
+    int& s_take = L->take;
     const int nt = blockDim.x;
     const int mt = m + m2;
     const int t = threadIdx.x;
@@ -117,7 +138,6 @@ __device__ __forceinline__ void fin_body(int m, int phase, int j, int rstart,
         // (1) the first DGKS refinement of step j-1, deferred to here: region 2
         //     holds its [V_{j-1}' r ; r'r] (SRC/dsaitr.f:730-771) -- folded: r'r only
         const bool folded = phase == kFinCgsFolded;
-        __shared__ int s_take2, s_go;
         if (t == 0) {
             s_take2 = 0;
             if (st->dgks == 1)
@@ -208,7 +228,6 @@ __device__ __forceinline__ void fin_body(int m, int phase, int j, int rstart,
         return;
     }
     // refinement phases share the "speculative coefficients" layout
-    __shared__ int s_take;
     const bool pfold = phase == kFinPostCgsFold;
     if (t == 0) {
         s_take = refine_decision(pfold ? (int)kFinPostCgs : phase, s_sum, jm, j, rstart, st, rec);
@@ -265,24 +284,16 @@ __device__ __forceinline__ void fin_body(int m, int phase, int j, int rstart,
 // once: the phase logic is one thread's chain of dependent accesses, which on
 // the global copy (last written by another XCD's finalize) cost a memory
 // latency each.
-constexpr int kFoldRecMax = 2 * 66;  // T records staged for the fold's t (j <= 64)
-constexpr int kFoldHMax = 64;        // HS: H(0:j, 0:j) staged for the Arnoldi fold's t = H s
 // The whole finalize, as the single workgroup of k_finalize runs it -- also
 // run by workgroup 0 of the symmetric SpMV's combine kernel when a finalize is
 // deferred into it (spmv_sym.hip; FinArgs).  Any block size; its loops stride
-// by blockDim.x.  Dynamic LDS: m + m2 doubles (s_sum).
+// by blockDim.x.  L: fin_lds_bytes(m + m2) of LDS; s_h (HS only): the Arnoldi
+// fold's H(0:jm, 0:jm), kFoldHMax^2 doubles of LDS.
 template <bool HS>
-__device__ __forceinline__ void finalize_block(const FinArgs& a) {
-    __shared__ LzState s_st;
-    __shared__ double s_rec[kFoldRecMax];
-    // HS (Arnoldi kFinPostCgsFold, j <= kFoldHMax): H's first j columns and rows,
-    // read once in parallel (coalesced) for the t = H s loop; the 32 KB are
-    // static, so only this variant carries them (the generic finalize keeps the
-    // whole 64 KB for its dynamic sums)
-    __shared__ double s_h[HS ? kFoldHMax * kFoldHMax : 1];
-    if (threadIdx.x == 0) s_st = *a.st;
+__device__ __forceinline__ void finalize_block(const FinArgs& a, FinLds* L, double* s_h) {
+    if (threadIdx.x == 0) L->st = *a.st;
     if (a.phase == kFinPostCgsFold && 2 * (a.j + 1) <= kFoldRecMax)
-        for (int k = threadIdx.x; k < 2 * (a.j + 1); k += blockDim.x) s_rec[k] = a.rec[k];
+        for (int k = threadIdx.x; k < 2 * (a.j + 1); k += blockDim.x) L->rec[k] = a.rec[k];
     if constexpr (HS) {
         const int jm = a.m - 1;
         for (int k = threadIdx.x; k < jm * jm; k += blockDim.x)
@@ -290,13 +301,24 @@ __device__ __forceinline__ void finalize_block(const FinArgs& a) {
     }
     // the partials' loads go out with the state's: one memory latency, not two
     // (a closed gate discards the sums unwritten)
-    fin_sums(a.part, a.nblk, a.from_sums, a.m, a.sums, a.part2, a.m2);
+    fin_sums(a.part, a.nblk, a.from_sums, a.m, a.sums, a.part2, a.m2, L->sum);
     __syncthreads();
-    if (gate_closed(&s_st, a.gate)) return;
-    fin_body(a.m, a.phase, a.j, a.rstart, a.sums, a.coef, a.cstride, a.rec, &s_st, a.hcol, a.hld,
-             a.m2, a.rstart_prev, s_rec, HS ? s_h : nullptr);
+    if (gate_closed(&L->st, a.gate)) return;
+    fin_body(a.m, a.phase, a.j, a.rstart, a.sums, a.coef, a.cstride, a.rec, &L->st, a.hcol, a.hld,
+             a.m2, a.rstart_prev, L, HS ? s_h : nullptr);
     __syncthreads();
-    if (threadIdx.x == 0) *a.st = s_st;
+    if (threadIdx.x == 0) *a.st = L->st;
+}
+
+// The launch's dynamic LDS as the finalize's (k_finalize, the combine kernel);
+// HS (Arnoldi kFinPostCgsFold, j <= kFoldHMax): H's first j columns and rows,
+// read once in parallel (coalesced) for the t = H s loop; the 32 KB are static,
+// so only that variant carries them.
+template <bool HS>
+__device__ __forceinline__ void finalize_block_dyn(const FinArgs& a) {
+    extern __shared__ double fin_dyn[];
+    __shared__ double s_h[HS ? kFoldHMax * kFoldHMax : 1];
+    finalize_block<HS>(a, reinterpret_cast<FinLds*>(fin_dyn), s_h);
 }
 
 }  // namespace

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const double* __restrict__
 }
 
 template <bool HS>
-__global__ __launch_bounds__(1024) void k_finalize(FinArgs a) { finalize_block<HS>(a); }
+__global__ __launch_bounds__(1024) void k_finalize(FinArgs a) { finalize_block_dyn<HS>(a); }
 
 template <class R>
 __global__ void k_zero_if(int64_t n, R* r, const LzState* st) {
@@ -671,12 +671,20 @@ struct Deferred {
 Deferred g_deferred;
 
 void launch_fin(hipStream_t s, const FinArgs& a, size_t lds) {
+    // ncv up to kMaxNcv: the state and records plus 8002 sums pass 64 KB
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)k_finalize<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        return true;
+    }();
+    (void)attr;
     AHIP_LAUNCH(a.hs ? k_finalize<true> : k_finalize<false>, dim3(1), dim3(1024), lds, s, a);
 }
 }  // namespace
 
-bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds) {
+bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds, size_t max_lds, bool allow_hs) {
     if (!g_deferred.set || g_deferred.s != s) return false;
+    if (g_deferred.lds > max_lds || (g_deferred.a.hs && !allow_hs)) return false;
     *a = g_deferred.a;
     *lds = g_deferred.lds;
     g_deferred.set = false;
@@ -704,7 +712,7 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
         return !(e && e[0] == '0');
     }();
     const double* part2 = ws.part + (size_t)ws.nblk * ws.stride;  // region 2 (chained steps)
-    const size_t lds = sizeof(double) * (size_t)(m + m2);  // s_sum (m + m2 <= 2 kMaxNcv + 4)
+    const size_t lds = fin_lds_bytes(m + m2);  // state, records, sums (m + m2 <= kMaxNcv + 67)
     const bool hs = ph == kFinPostCgsFold && ws.hld && m - 1 <= kFoldHMax;
     auto args = [&](int fs) {
         return FinArgs{ws.part, ws.nblk, fs, m, (int)ph, j, rstart, gate, ws.sums, ws.coef,

@@ -116,7 +116,17 @@ __device__ __forceinline__ T ldg(const T* p) {
 // with another workgroup's (or rank's) spill through the slots, and only its
 // last superblock's spill leaves through a slot.  Each wave streams its slices
 // with the next slice's first chunk in flight, across superblock boundaries.
-template <int U, bool NT, bool YNT = false>
+// FUSE (one GPU; AHIP_SPMV_FUSE=0 turns it off): the chain-head combine
+// y = lo + hi happens here instead of in k_ssell_combine.  Each chain's head
+// rows pair two workgroups (the previous chain's, whose last spill is lo, and
+// this chain's, whose first superblock's head rows are hi); both store their
+// part with sc1 stores, wait for them, and add to the pair's counter; the one
+// whose add returns 1 arrived second and combines, reading both parts with sc1
+// loads -- MI355X_MICROARCH.md's hand-off row for one workgroup a CU (this
+// kernel's occupancy): no fence, no waiting, so no workgroup ever blocks on
+// another.  The deferred finalize of the step (fa, kernels.hip) then runs in
+// workgroup 0 over its spent x window.
+template <int U, bool NT, bool YNT = false, bool FUSE = false>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
     const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
@@ -124,7 +134,7 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
     const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
     double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff, int chain,
-    int64_t nsb) {
+    int64_t nsb, int* __restrict__ pair, FinArgs fa) {
     __shared__ double xw[kSymWin];
     __shared__ double yw[kSymWin];
     constexpr int NW = kSymThreads / 64;
@@ -221,16 +231,54 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         const int64_t off = sb_off[b];
         for (int i = t; i < R; i += kSymThreads) {
             const double v = yw[i];
-            if (i < head) slot_hi[off + i] = v;
-            else if constexpr (YNT) __builtin_nontemporal_store(v, y + r0 + i);
-            else y[r0 + i] = v;
+            if (i < head) {
+                if constexpr (FUSE) __hip_atomic_store(slot_hi + off + i, v, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                else slot_hi[off + i] = v;
+            } else if constexpr (YNT) {
+                __builtin_nontemporal_store(v, y + r0 + i);
+            } else {
+                y[r0 + i] = v;
+            }
         }
         if (b == b1 - 1) {  // the chain's last spill leaves through a slot
             const int64_t offn = sb_off[b + 1];
-            for (int i = R + t; i < span; i += kSymThreads) slot_lo[offn + (i - R)] = yw[i];
+            for (int i = R + t; i < span; i += kSymThreads) {
+                if constexpr (FUSE) __hip_atomic_store(slot_lo + offn + (i - R), yw[i], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                else slot_lo[offn + (i - R)] = yw[i];
+            }
         }
         R_prev = R;
         span_prev = span;
+    }
+    if constexpr (FUSE) {
+        const int64_t nch = gridDim.x;
+        int* flag = reinterpret_cast<int*>(xw);  // the x window is spent
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slot stores
+        __syncthreads();
+        if (t == 0) {
+            flag[0] = ch > 0 ? __hip_atomic_fetch_add(pair + ch, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) : 0;
+            flag[1] = ch + 1 < nch ? __hip_atomic_fetch_add(pair + ch + 1, 1, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT) : 0;
+        }
+        __syncthreads();
+        for (int side = 0; side < 2; ++side) {
+            if (flag[side] != 1) continue;  // first of its pair: the partner combines
+            const int64_t c = ch + side;     // the chain whose head rows are combined
+            const int64_t bh = c * chain;
+            const int pre = sb_pre[bh];
+            const int64_t off = sb_off[bh], rh = sb_r0[bh];
+            for (int i = t; i < pre; i += kSymThreads)
+                y[rh + i] = __hip_atomic_load(slot_lo + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                            __hip_atomic_load(slot_hi + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) pair[c] = 0;  // both parties are done with it (next launch: kernel order)
+        }
+        if (fa.active && blockIdx.x == 0) {
+            __syncthreads();  // flag[] read by every wave before the window is reused
+            finalize_block<false>(fa, reinterpret_cast<FinLds*>(xw), nullptr);
+        }
     }
 }
 
@@ -404,7 +452,7 @@ __global__ __launch_bounds__(1024) void k_ssell_combine_fin(const int64_t* __res
     const int pre = sb_pre[b];
     const int64_t off = sb_off[b], r0 = sb_r0[b];
     for (int i = threadIdx.x; i < pre; i += 1024) y[r0 + i] = lo[off + i] + hi[off + i];
-    if (blockIdx.x == 0) finalize_block<HS>(fa);
+    if (blockIdx.x == 0) finalize_block_dyn<HS>(fa);
 }
 
 }  // namespace
@@ -568,11 +616,12 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
                  b_val = sizeof(double) * (size_t)std::max<int64_t>(padded, 1),
                  b_cw = sizeof(uint16_t) * (size_t)std::max<int64_t>(padded, 1),
                  b_slot = sizeof(double) * (size_t)std::max<int64_t>(nslot, 1),
-                 b_wg0 = sizeof(int64_t) * wg0.size(), b_wsl = sizeof(int32_t) * wsl.size();
+                 b_wg0 = sizeof(int64_t) * wg0.size(), b_wsl = sizeof(int32_t) * wsl.size(),
+                 b_pair = sizeof(int32_t) * (nsb + 2);
     char* d = nullptr;
     if (fault_filter(hipMalloc(&d, up(b_r0) + up(b_sp) + up(b_pre) + up(b_off) + up(b_s0) + up(b_ptr) +
                                        up(b_row) + up(b_val) + up(b_cw) + 2 * up(b_slot) + up(b_wg0) +
-                                       up(b_wsl))) != hipSuccess)
+                                       up(b_wsl) + up(b_pair))) != hipSuccess)
         return -2;
     char* p = d;
     auto take = [&](size_t bytes) {
@@ -593,6 +642,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     auto* d_hi = (double*)take(b_slot);
     auto* d_wg0 = (int64_t*)take(b_wg0);
     auto* d_wsl = (int32_t*)take(b_wsl);
+    auto* d_pair = (int*)take(b_pair);
     auto h2d = [](void* dst, const void* src, size_t bytes) {
         return fault_filter(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)) == hipSuccess;
     };
@@ -611,6 +661,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     }
     // the outgoing spill's tail past the last window is never written: zero it once
     ok = ok && fault_filter(hipMemset(d_lo, 0, b_slot)) == hipSuccess;
+    ok = ok && fault_filter(hipMemset(d_pair, 0, b_pair)) == hipSuccess;  // (FUSE pair counters)
     ok = ok && fault_filter(hipDeviceSynchronize()) == hipSuccess;
     if (d_sr0) (void)hipFree(d_sr0);
     if (!ok) {
@@ -630,6 +681,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_hi = d_hi;
     A.ss_wg0 = d_wg0;
     A.ss_wsl = d_wsl;
+    A.ss_pair = d_pair;
     A.ss_nsb = nsb;
     // chains of consecutive superblocks, one workgroup per CU (k_csr_ssell);
     // the in-LDS window shift needs span <= 2R (true for the balanced plan)
@@ -662,7 +714,8 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
         const int64_t nch = (A.ss_nsb + chain - 1) / chain;
         AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
-                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb);
+                           A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb,
+                           (int*)nullptr, FinArgs{});
     };
     // measured on the NS operator (tools/spmv_sym_time.py, one process, before
     // chaining): U = 8 with non-temporal val/col loads 0.594 ms incl. the
@@ -703,7 +756,8 @@ void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
     }
     FinArgs fa{};
     size_t lds = 0;
-    if (!take_deferred_finalize(s, &fa, &lds)) {
+    if (!take_deferred_finalize(s, &fa, &lds, 64 * 1024)) {
+        flush_deferred_finalize(s);  // (one too large for this launch's LDS)
         AHIP_LAUNCH(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
                     A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
         return;
@@ -714,9 +768,38 @@ void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
                 fa);
 }
 
+// AHIP_SPMV_FUSE=0: the combine (and a deferred finalize) as a launch of its own
+static bool spmv_fuse() {
+    static const bool on = [] {
+        const char* e = getenv("AHIP_SPMV_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
-    csr_spmv_sym_main(s, A, x, y);
-    csr_spmv_sym_combine(s, A, y);
+    // one GPU (coff = spill = 0), the default kernel, counters allocated
+    const bool fuse = spmv_fuse() && A.ss_pair && A.ss_coff == 0 && A.ss_spill_out == 0 &&
+                      (A.ss_variant == 0 || A.ss_variant == 7) && !spmv_ynt();
+    if (!fuse) {
+        csr_spmv_sym_main(s, A, x, y);
+        csr_spmv_sym_combine(s, A, y);
+        return;
+    }
+    // the step's deferred finalize rides along when it fits the spent x window
+    // (without the H-column staging: k_finalize<false>'s form)
+    FinArgs fa{};
+    size_t lds = 0;
+    if (!take_deferred_finalize(s, &fa, &lds, sizeof(double) * kSymWin, false)) {
+        flush_deferred_finalize(s);
+        fa = FinArgs{};
+    }
+    const int chain = sym_chain(A);
+    const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+    AHIP_LAUNCH((k_csr_ssell<8, true, false, true>), dim3((unsigned)nch), dim3(kSymThreads), 0, s,
+                A.ss_sb_r0, A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
+                A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_pair,
+                fa);
 }
 
 }  // namespace ahip::dev
