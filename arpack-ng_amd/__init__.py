@@ -1123,6 +1123,14 @@ class DistOp:
         L.arpack_hip_dist_mode.argtypes = [C.c_void_p]
         return ("halo", "ghosts", "allgather")[L.arpack_hip_dist_mode(self.h)]
 
+    @property
+    def spill(self):
+        """True when the symmetric-storage SpMV sends a forward spill
+        (arpack_hip_dist_spill); False for full storage or the spill-free form."""
+        L = lib()
+        L.arpack_hip_dist_spill.argtypes = [C.c_void_p]
+        return L.arpack_hip_dist_spill(self.h) == 1
+
     def __del__(self):
         try:
             if self.h and _lib is not None:

@@ -394,6 +394,14 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     }
     if (rc != 0) return rc;
     A->A.kernel = ahip::dev::kCsrSymSell;
+    // a distributed block: the spill-free exchange when every rank's lower ghost
+    // rows lie inside its incoming spill's rows (structurally symmetric
+    // coupling); AHIP_DIST_SPILL=1 keeps the spill
+    if (A->dist) {
+        const char* e = std::getenv("AHIP_DIST_SPILL");
+        const bool want = !(e && e[0] == '1');
+        A->A.ss_lg = ahip::dist_all_ok(c, want && A->A.ss_lg_rows <= A->A.ss_pre0) ? 1 : 0;
+    }
     return 0;
 }
 

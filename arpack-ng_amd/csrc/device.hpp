@@ -310,6 +310,9 @@ struct Csr {
     int ss_chain = 1;                      // consecutive superblocks per workgroup
     int64_t ss_coff = 0;                   // x index of local row 0's diagonal (halo_lo)
     int64_t ss_spill_out = 0;              // rows of the next rank reached by the last window
+    int64_t ss_pre0 = 0;                   // head rows of superblock 0 (the incoming spill's)
+    int64_t ss_lg_rows = 0;                // 1 + last row with a column in the low halo
+    int ss_lg = 0;                         // spill-free distributed form (k_ssell_combine_lg)
 };
 enum CsrKernel : int {
     kCsrVector = 0,
@@ -339,7 +342,8 @@ void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y);
 // main kernel, then y(prefix rows) = lo + hi.  The outgoing spill is
 // ss_lo + ss_ncomb (ss_spill_out doubles); the incoming one lands in ss_lo[0, spill_in).
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y);
-void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y);
+// x_ext (a distributed block's extended x): the spill-free form when A.ss_lg
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext = nullptr);
 // Build the SELL-64 layout from a matrix with window tables; *owned receives the
 // single device allocation.  0 on success.
 int csr_build_sell(Csr& A, void** owned);

@@ -68,14 +68,16 @@ void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool 
     }
     const dev::Csr& A = *D.A;
     const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val;
-    comm_halo(D.comm, D, s, sym, p2p);
+    // spill-free symmetric form (A.ss_lg, agreed by every rank): one two-sided
+    // halo, and the leading rows' lower ghost terms from the rank's own rows
+    comm_halo(D.comm, D, s, sym && !A.ss_lg, p2p);
     if (sym) {
-        // symmetric storage: my rows' upper entries reach the next rank's first
-        // rows -- those transposed terms (the spill) travel forward and are
-        // combined into the receiver's leading rows (a reverse halo)
         dev::csr_spmv_sym_main(s, A, D.x_ext, y);
-        comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
-        dev::csr_spmv_sym_combine(s, A, y);
+        // otherwise my rows' upper entries reach the next rank's first rows --
+        // those transposed terms (the spill) travel forward and are combined
+        // into the receiver's leading rows (a reverse halo)
+        if (!A.ss_lg) comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
+        dev::csr_spmv_sym_combine(s, A, y, D.x_ext);
         return;
     }
     dev::csr_spmv(s, A, D.x_ext, y);
@@ -404,6 +406,13 @@ int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* ha
     *send_lo = D->D.send_lo;
     *send_hi = D->D.send_hi;
     return 0;
+}
+
+int arpack_hip_dist_spill(const arpack_hip_dist* D) {
+    if (!D || !D->csr || !D->D.A) return -1;
+    const ahip::dev::Csr& A = *D->D.A;
+    const bool sym = D->D.mode == ahip::DistOp::kHaloNeighbour && A.kernel == ahip::dev::kCsrSymSell && A.ss_val;
+    return sym && !A.ss_lg ? 1 : 0;
 }
 
 }  // extern "C"

@@ -58,15 +58,16 @@ __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict
                               int32_t* __restrict__ cmax) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        int32_t c = 0, m = (int32_t)i;
+        int32_t c = 0, m = (int32_t)i, low = 0;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
             const int32_t j = (int32_t)(col[k] - coff);
             if (j >= i) {
                 ++c;
                 m = max(m, j);
             }
+            low |= j < 0;  // a column of the previous rank's block (halo_lo)
         }
-        cnt[i] = c;
+        cnt[i] = c | (low << 30);
         cmax[i] = m;
     }
 }
@@ -455,6 +456,47 @@ __global__ __launch_bounds__(1024) void k_ssell_combine_fin(const int64_t* __res
     if (blockIdx.x == 0) finalize_block_dyn<HS>(fa);
 }
 
+// Spill-free distributed combine (Csr::ss_lg): the rank's first pre[0] rows
+// take their lower ghost terms (columns in the low halo, x_ext[0, coff)) from
+// their own full CSR rows instead of the previous rank's spill -- the same
+// products, since A is symmetric, with x from the two-sided halo.  Workgroups
+// [0, nch) combine chains 1.. as above (workgroup 0 carries a deferred
+// finalize); workgroups nch.. take 256 head rows each, four lanes a row, the
+// lanes' partials summed in lane order.
+template <bool HS>
+__global__ __launch_bounds__(1024) void k_ssell_combine_lg(
+    const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_pre,
+    const int64_t* __restrict__ sb_off, const double* __restrict__ lo, const double* __restrict__ hi,
+    double* __restrict__ y, int chain, int nch, const int64_t* __restrict__ rp,
+    const int32_t* __restrict__ col, const double* __restrict__ val, const double* __restrict__ xe,
+    int64_t coff, FinArgs fa) {
+    if ((int)blockIdx.x < nch) {
+        if (blockIdx.x > 0) {
+            const int64_t b = (int64_t)blockIdx.x * chain;
+            const int pre = sb_pre[b];
+            const int64_t off = sb_off[b], r0 = sb_r0[b];
+            for (int i = threadIdx.x; i < pre; i += 1024) y[r0 + i] = lo[off + i] + hi[off + i];
+        } else if (fa.active) {
+            finalize_block_dyn<HS>(fa);
+        }
+        return;
+    }
+    const int64_t i = (int64_t)(blockIdx.x - nch) * 256 + (threadIdx.x >> 2);
+    const int q = threadIdx.x & 3;
+    const int pre = sb_pre[0];
+    double s = 0.0;
+    if (i < pre) {
+        for (int64_t k = rp[i] + q; k < rp[i + 1]; k += 4) {
+            const int64_t c = col[k];
+            if (c < coff) s += val[k] * xe[c];
+        }
+    }
+    const double s1 = __shfl_down(s, 1, 4);
+    const double s2 = __shfl_down(s, 2, 4);
+    const double s3 = __shfl_down(s, 3, 4);
+    if (i < pre && q == 0) y[i] = hi[sb_off[0] + i] + (((s + s1) + s2) + s3);
+}
+
 }  // namespace
 
 // Superblock plan from the per-row largest upper column cmax[i] (>= i).
@@ -559,6 +601,13 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     (void)hipFree(dcnt);
     (void)hipFree(dcm);
     if (!got) return -2;
+    // rows with columns before the block (a distributed block's low halo): the
+    // spill-free exchange computes their lower ghost terms locally
+    int64_t lg_rows = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (cnt[i] >> 30) lg_rows = i + 1;
+        cnt[i] &= (1 << 30) - 1;
+    }
     std::vector<int64_t> r0s, off;
     std::vector<int32_t> spans, pre;
     int ncu = 0;
@@ -693,6 +742,9 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_ncomb = ncomb;
     A.ss_coff = coff;
     A.ss_spill_out = spill_out;
+    A.ss_lg_rows = lg_rows;
+    A.ss_pre0 = pre[0];
+    A.ss_lg = 0;  // (set by arpack_hip_csr_set_symmetric when every rank can)
     *owned = d;
     return 0;
 }
@@ -747,9 +799,24 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
     }
 }
 
-void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y) {
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+    if (x_ext && A.ss_lg) {  // spill-free form: the head rows' lower ghost terms here
+        FinArgs fa{};
+        size_t lds = 0;
+        if (!take_deferred_finalize(s, &fa, &lds, 64 * 1024)) {
+            flush_deferred_finalize(s);
+            fa = FinArgs{};
+            lds = 0;
+        }
+        const int64_t nlg = (A.ss_pre0 + 255) / 256;  // (ss_lg: lg_rows <= pre[0])
+        AHIP_LAUNCH(fa.hs ? k_ssell_combine_lg<true> : k_ssell_combine_lg<false>,
+                    dim3((unsigned)(nch + nlg)), dim3(1024), lds, s, A.ss_sb_r0, A.ss_sb_pre,
+                    A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain, (int)nch, A.rowptr, A.col, A.val,
+                    x_ext, A.ss_coff, fa);
+        return;
+    }
     if (A.ss_ncomb <= 0) {
         flush_deferred_finalize(s);
         return;

@@ -417,6 +417,12 @@ int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* ha
 /* Exchange form: 0 neighbour halos, 1 ghost lists (halo_hi = ghosts), 2
  * all-gather (halo_lo / halo_hi = the rows before / after this rank's). */
 int arpack_hip_dist_mode(const arpack_hip_dist* D);
+// 1: the block's symmetric-storage SpMV sends its transposed terms for the next
+// rank's leading rows forward as a spill exchange after the SpMV, under
+// AHIP_DIST_SPILL=1 or a structurally unsymmetric coupling; 0: no spill -- full
+// storage, or the spill-free symmetric form: one two-sided halo, the leading
+// rows' lower ghost terms from the rank's own rows; -1: no operator.
+int arpack_hip_dist_spill(const arpack_hip_dist* D);
 /* Row-block decomposition without an operator: rank owns rows [row0, row0+nloc)
  * of the global n_global (collective-free; needs arpack_hip_comm_init). */
 int arpack_hip_dist_rows(arpack_hip_dist** D, int64_t nloc, int64_t row0, int64_t n_global);

@@ -54,6 +54,7 @@ def spmv_chain(pkg, out, rank, world):
     DA = pkg.DistOp(A, n, r0)
     DB = pkg.DistOp(B, n, r0)
     B.set_symmetric(True)
+    spill = DB.spill
     x = np.random.default_rng(5).standard_normal(n)[r0:r1].copy()
     xd = pkg.DeviceBuffer.from_numpy(x)
     ya = pkg.DeviceBuffer(nloc)
@@ -63,7 +64,7 @@ def spmv_chain(pkg, out, rank, world):
     a, b = ya.numpy(), yb.numpy()
     ok = np.all(np.abs(a - b) <= 64 * np.finfo(float).eps * (np.abs(a) + 128.0 * 4.0))
     np.savez(os.path.join(out, "rank%d.npz" % rank), spmv_ok=np.array([bool(ok)]),
-             maxdiff=np.array([float(np.abs(a - b).max())]))
+             maxdiff=np.array([float(np.abs(a - b).max())]), spill=np.array([spill]))
     del DA, DB
 
 
@@ -231,6 +232,7 @@ def main():
         res["halo"] = np.array(list(D.info().values()))
         if case == "sym_csr_s":
             A.set_symmetric(True)
+            res["spill"] = np.array([D.spill])
             x = np.random.default_rng(7).standard_normal(n)
             xd = pkg.DeviceBuffer.from_numpy(x[r0:r1].copy())
             yd = pkg.DeviceBuffer(nloc)

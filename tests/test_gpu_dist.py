@@ -34,14 +34,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(tmp_path, case, fixture, P, info0=False):
+def _run(tmp_path, case, fixture, P, info0=False, extra_env=None):
     out = tmp_path / f"{case}_{fixture}_{P}_{int(info0)}"
     out.mkdir()
     port = _port()
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
         args = [sys.executable, os.path.join(HERE, "dist_worker.py"), case, fixture, str(out)]
         procs.append(subprocess.Popen(args + (["info0"] if info0 else []), env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
@@ -97,20 +97,27 @@ def test_sym_csr_ranks(tmp_path, golden, fixture):
     assert h[1][0] > 0 and h[1][1] > 0 and h[0][0] == 0 and h[2][1] == 0
 
 
+SPILL_FORMS = {"spill_free": {}, "spill": {"AHIP_DIST_SPILL": "1"}}
+
+
+@pytest.mark.parametrize("form", sorted(SPILL_FORMS))
 @pytest.mark.parametrize("fixture", ["g4_banded", "g3_anderson3d"])
-def test_sym_csr_symmetric_storage_ranks(tmp_path, golden, fixture):
-    """Local blocks declared symmetric (upper-triangle SpMV, transposed terms for
-    the next rank's rows sent forward as a spill): the distributed SpMV matches
-    SciPy row by row and the solve gives the reference's cycles and values."""
+def test_sym_csr_symmetric_storage_ranks(tmp_path, golden, fixture, form):
+    """Local blocks declared symmetric (upper-triangle SpMV; the transposed terms
+    for the next rank's rows either sent forward as a spill, or -- the default
+    spill-free form -- recomputed by the receiver from its own rows' lower ghost
+    entries over a two-sided halo): the distributed SpMV matches SciPy row by
+    row and the solve gives the reference's cycles and values."""
     g = golden(fixture)
     spec = g["spec"]
     rp, col, val = (M.banded_sym(*[int(x) for x in spec[1:]]) if str(spec[0]) == "banded_sym"
                     else M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4])))
     A = M.to_scipy(rp, col, val)
     for P in (1, 2, 3):
-        ranks = _run(tmp_path, "sym_csr_s", fixture, P)
+        ranks = _run(tmp_path, "sym_csr_s", fixture, P, extra_env=SPILL_FORMS[form])
         for r in ranks:
             assert bool(r["spmv_ok"][0])
+            assert bool(r["spill"][0]) == (form == "spill")
             assert int(r["info"][0]) == 0
             assert int(r["iparam"][2]) == int(g["iparam"][2]), (P, r["iparam"][2])
             assert int(r["iparam"][4]) == int(g["iparam"][4])
@@ -119,11 +126,14 @@ def test_sym_csr_symmetric_storage_ranks(tmp_path, golden, fixture):
         assert _resid(A, _z(ranks), d) <= 1e-8
 
 
-def test_symmetric_storage_chained_blocks(tmp_path):
+@pytest.mark.parametrize("form", sorted(SPILL_FORMS))
+def test_symmetric_storage_chained_blocks(tmp_path, form):
     """2 ranks x 3e6 rows: each rank's plan chains superblocks; the distributed
-    symmetric SpMV (forward spill) equals the full-storage one to rounding."""
-    for r in _run(tmp_path, "spmv_chain", "-", 2):
+    symmetric SpMV (forward spill, or the spill-free form) equals the
+    full-storage one to rounding."""
+    for r in _run(tmp_path, "spmv_chain", "-", 2, extra_env=SPILL_FORMS[form]):
         assert bool(r["spmv_ok"][0]), r["maxdiff"]
+        assert bool(r["spill"][0]) == (form == "spill")
 
 
 def test_sym_csr_random_start(tmp_path, golden):
