@@ -457,9 +457,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": ("csr_spmv symmetric storage (k_csr_ssell + k_ssell_combine: "
-                                "upper-triangle SELL-64 slices over LDS x/y windows, LDS atomic "
-                                "transposed terms, 16-bit window-relative cols)") if storage == "sym"
+                     "kernel": ("csr_spmv symmetric storage (k_csr_ssell: upper-triangle SELL-64 "
+                                "slices over LDS x/y windows, LDS atomic transposed terms, 16-bit "
+                                "window-relative cols; on one GPU the chain-head combine and the "
+                                "step's deferred finalize run inside it, else k_ssell_combine "
+                                "follows)") if storage == "sym"
                                else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "
                                      "x windows, 16-bit window-relative cols, XCD-contiguous "
                                      "superblocks)"),
