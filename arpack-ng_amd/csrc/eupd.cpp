@@ -191,11 +191,14 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
     }
 
     const bool zdev = is_device_pointer(z);
+    // M is the source of an asynchronous copy from pageable memory: it lives
+    // until the a.sync() below (a run of 8 processes on one GPU read it freed)
+    std::vector<double> M;
     if (rvec && howmny == 'A') {
         std::vector<double> work(ncv + 1);
         la::geqr2(ncv, nconv, workl + iq, ldq, workl + iw + ncv, work.data());
         // M = H_1 ... H_nconv * I(:, 1:nconv)  (ncv x nconv), then V <- V*M on device
-        std::vector<double> M((size_t)ncv * nconv, 0.0);
+        M.assign((size_t)ncv * nconv, 0.0);
         for (int j = 0; j < nconv; ++j) M[(size_t)j * ncv + j] = 1.0;
         la::orm2r('L', 'N', ncv, nconv, nconv, workl + iq, ldq, workl + iw + ncv, M.data(), ncv,
                   work.data());
@@ -235,8 +238,10 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
             a.ck(hipMemcpy2DAsync(zd, sizeof(R) * ldz, a.d_v, sizeof(R) * a.d_ld,
                                    sizeof(R) * n, nconv, hipMemcpyDeviceToDevice, a.stream));
         } else {
-            if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess)
+            if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess) {
+                a.sync();  // (the pending copies read M)
                 return -9999;
+            }
             a.ck(hipMemcpyAsync(zd, a.d_v, sizeof(R) * (size_t)a.d_ld * nconv,
                                  hipMemcpyDeviceToDevice, a.stream));
         }

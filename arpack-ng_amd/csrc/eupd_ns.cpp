@@ -283,8 +283,10 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out
         zd = z;
         ldzd = ldz;
     } else {
-        if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess)
+        if (hipMallocAsync(&zd, sizeof(R) * (size_t)a.d_ld * nconv, a.stream) != hipSuccess) {
+            a.sync();  // (the pending copy reads Qh)
             return -9999;
+        }
     }
     if (howmny == 'A') {
         a.sync();  // ws.q (Qh) consumed before it is overwritten
