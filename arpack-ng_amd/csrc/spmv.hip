@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "device.hpp"
+#include "finalize.hpp"
 
 namespace ahip::dev {
 
@@ -370,14 +371,19 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_wvecp(
 // SELL-64 over the LDS x window: one workgroup per superblock, each wave takes
 // whole slices (lane = row); a column step is one coalesced 512-B val load and
 // one 128-B colw load per wave.  Each row is summed sequentially in its CSR
-// (column) order.
-template <int U, bool XCD, bool NTL = false, bool MR = false>
-__global__ __launch_bounds__(kWinThreads) void k_csr_sell(
+// (column) order.  FIN (1, or 2 with the Arnoldi H staging): the step's
+// deferred finalize (kernels.hip finalize(..., defer)) runs in workgroup 0
+// after its rows, over the spent x window -- it reads the partial sums of the
+// pass before the SpMV and writes the state the pass after it reads, so the
+// launch it saves costs no ordering.  (k_csr_sell_fin below: its own kernel,
+// held to 64 VGPRs so two workgroups still share a CU.)
+template <int U, bool XCD, bool NTL, bool MR, int FIN>
+__device__ __forceinline__ void csr_sell_body(
     const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
     const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
     const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
     const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
-    const int64_t* __restrict__ rng) {
+    const int64_t* __restrict__ rng, const FinArgs& fa) {
     // unfused multiply-add: each row is summed exactly as a sequential CSR loop
     // (y_i = ((0 + a_i1 x_1) + a_i2 x_2) + ...) -- SciPy's csr_matvec, the OP
     // the reference's RCI callers use -- so y is bitwise the CPU result
@@ -448,6 +454,37 @@ __global__ __launch_bounds__(kWinThreads) void k_csr_sell(
         base = nbase;
         w = nw;
     }
+    if constexpr (FIN > 0) {
+        if (blockIdx.x == 0) {
+            __syncthreads();  // every wave is done with the x window
+            finalize_block<FIN == 2>(fa, reinterpret_cast<FinLds*>(lds), lds + kWinX - kFoldHMax * kFoldHMax);
+        }
+    }
+}
+
+template <int U, bool XCD, bool NTL = false, bool MR = false>
+__global__ __launch_bounds__(kWinThreads) void k_csr_sell(
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
+    const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
+    const int64_t* __restrict__ rng) {
+    csr_sell_body<U, XCD, NTL, MR, 0>(sb_slice0, sptr, srow, sb_c0, sb_span, scolw, sval, x, y, rng,
+                                      FinArgs{});
+}
+
+// The default form (U = 4, XCD order, non-temporal val/col) carrying a deferred
+// finalize.  waves_per_eu(8): the finalize's code must not raise the kernel's
+// VGPRs past 64, or one workgroup a CU would fit instead of two.
+template <bool MR, int FIN>
+__global__ __launch_bounds__(kWinThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_csr_sell_fin(
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const int64_t* __restrict__ sb_c0,
+    const int32_t* __restrict__ sb_span, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
+    const int64_t* __restrict__ rng, FinArgs fa) {
+    csr_sell_body<4, true, true, MR, FIN>(sb_slice0, sptr, srow, sb_c0, sb_span, scolw, sval, x, y,
+                                          rng, fa);
 }
 
 // Two slices per wave at once (s and s + NW): twice the independent column
@@ -1006,16 +1043,51 @@ static void launch_wvec(hipStream_t s, const Csr& A, const double* x, double* y,
     else launch_wvec1<L, U, false, false>(s, A, x, y);
 }
 
+// AHIP_SELL_FIN=0: a finalize deferred into the SpMV gets a launch of its own
+// before the full-storage SELL kernel instead of riding in it
+static bool sell_fin() {
+    static const bool on = [] {
+        const char* e = getenv("AHIP_SELL_FIN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
-    // a finalize deferred into the symmetric SpMV's combine: the other forms
-    // have no combine launch to carry it
-    if (!(A.kernel == kCsrSymSell && A.ss_val)) flush_deferred_finalize(s);
-    if (A.kernel == kCsrSymSell && A.ss_val) {
+    if (A.kernel == kCsrSymSell && A.ss_val) {  // (carries a deferred finalize itself)
         csr_spmv_sym(s, A, x, y);
         return;
     }
+    // the full-storage SELL kernel's default form (NT loads, U = 4) and its
+    // multi-range form carry a deferred finalize in workgroup 0 (k_csr_sell
+    // FIN); every other form has it launched first
+    const bool sell_carry = A.kernel == kCsrSell && A.s_val && (A.w_rng || A.s_unroll == 10) && sell_fin();
+    FinArgs fa{};
+    size_t fin_lds = 0;
+    // it must fit the window below the Arnoldi H staging (kFoldHMax^2 doubles)
+    const bool carried =
+        sell_carry && take_deferred_finalize(s, &fa, &fin_lds,
+                                             sizeof(double) * (kWinX - kFoldHMax * kFoldHMax));
+    if (!carried) flush_deferred_finalize(s);
     if (A.kernel == kCsrSell && A.s_val) {
         const size_t lds = sizeof(double) * kWinX;
+        if (carried) {
+            auto gof = [&](auto kern) {
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds);
+                AHIP_LAUNCH(kern, dim3((unsigned)A.w_nsb), dim3(kWinThreads), lds, s, A.s_sb_slice0,
+                            A.s_ptr, A.s_row, A.w_sb_c0, A.w_sb_span, A.s_colw, A.s_val, x, y,
+                            (const int64_t*)A.w_rng, fa);
+            };
+            if (A.w_rng) {
+                if (fa.hs) gof(k_csr_sell_fin<true, 2>);
+                else gof(k_csr_sell_fin<true, 1>);
+            } else {
+                if (fa.hs) gof(k_csr_sell_fin<false, 2>);
+                else gof(k_csr_sell_fin<false, 1>);
+            }
+            return;
+        }
         auto go = [&](auto kern) {  // k_csr_sell (one window range: no range table)
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
