@@ -719,8 +719,9 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
                        ws.stride, ws.rec, ws.st, ws.hcol, ws.hld, part2, m2, rstart_prev,
                        hs ? 1 : 0, 1};
     };
-    if (defer && defer_on && !from_sums && fused) {
-        g_deferred = Deferred{ws.stream, args(0), lds, true};
+    // (from_sums: the distributed path's phase logic on allreduced sums)
+    if (defer && defer_on && (from_sums || fused)) {
+        g_deferred = Deferred{ws.stream, args(from_sums ? 1 : 0), lds, true};
         return;
     }
     ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * (m + m2));

@@ -205,7 +205,10 @@ void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m
     if (dist && dist->comm) {
         dev::finalize(ws, m, dev::kFinRaw, j, rstart, gate, false, m2);
         comm_allreduce_sum(dist->comm, ws.sums, m + m2, a.stream);
-        if (ph != dev::kFinRaw) dev::finalize(ws, m, ph, j, rstart, gate, true, m2, rstart_prev);
+        // the phase logic on the allreduced sums may ride in the next SpMV too
+        // (not with the overlapped SpMV: that one runs on op_stream)
+        if (ph != dev::kFinRaw)
+            dev::finalize(ws, m, ph, j, rstart, gate, true, m2, rstart_prev, defer && !op_stream);
     } else {
         dev::finalize(ws, m, ph, j, rstart, gate, false, m2, rstart_prev, defer);
     }
