@@ -171,6 +171,58 @@ def test_symsell_plan_row_distribution(pkg, P):
     assert np.all(np.abs(y - yref) <= 1e-13 * scale)
 
 
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_symsell_spill_free_row_distribution(pkg, P):
+    """The spill-free distributed form (spmv_sym.hip k_ssell_combine_lg, agreed
+    at arpack_hip_csr_set_symmetric): no spill crosses ranks; each block's
+    leading pre[0] rows add their lower ghost terms -- the entries of the rank's
+    own full rows whose columns lie before the block, over the low halo of x --
+    and the rank's own spill past its end is dropped.  Its condition: every row
+    with such an entry lies inside pre[0] (the rows the previous rank reaches);
+    then the blocks reproduce the global A @ x."""
+    n, B = 6000, 300
+    rp, col, val = M.banded_sym(n, 1234, B, 9)
+    x = np.random.default_rng(9).standard_normal(n)
+    yref = M.to_scipy(rp, col, val) @ x
+    scale = M.to_scipy(rp, col, np.abs(val)) @ np.abs(x)
+    bounds = [(q * n // P, (q + 1) * n // P) for q in range(P)]
+    reach = []
+    for a, b in bounds:
+        c = col[rp[a]:rp[b]]
+        reach.append(max(0, int(c.max()) - (b - 1)))
+    y = np.zeros(n)
+    for q, (a, b) in enumerate(bounds):
+        lrp = rp[a:b + 1] - rp[a]
+        lcol = col[rp[a]:rp[b]].astype(np.int64) - a
+        lval = val[rp[a]:rp[b]]
+        sin = reach[q - 1] if q > 0 else 0
+        sout = reach[q] if q < P - 1 else 0
+        rc, r0s, spans, pre = _plan(pkg, _upper_cmax(lrp, lcol), 2048, sin, sout)
+        assert rc == 0 and pre[0] == sin
+        m = b - a
+        rows = np.repeat(np.arange(m), np.diff(lrp))
+        low = lcol < 0
+        lg_rows = int(rows[low].max()) + 1 if low.any() else 0
+        assert lg_rows <= pre[0]                   # the form's agreement condition
+        yl = np.zeros(m + sout)
+        for i in range(m):    # upper rows of the block, transposed terms included
+            for k in range(lrp[i], lrp[i + 1]):
+                j = lcol[k]
+                if j < i:
+                    continue
+                yl[i] += lval[k] * x[a + j]
+                if j != i:
+                    yl[j] += lval[k] * x[a + i]
+        for i in range(pre[0]):   # the leading rows' lower ghost terms, CSR order
+            s = 0.0
+            for k in range(lrp[i], lrp[i + 1]):
+                if lcol[k] < 0:
+                    s += lval[k] * x[a + lcol[k]]
+            yl[i] += s
+        y[a:b] = yl[:m]           # yl[m:] (the spill) is not sent
+    assert np.all(np.abs(y - yref) <= 1e-13 * scale)
+
+
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
 def test_symsell_plan_bench_sizes(pkg, P):
     """The bench's row blocks (n = 1e7 over P ranks, band 4096): every rank gets a
