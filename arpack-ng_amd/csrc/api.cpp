@@ -687,11 +687,21 @@ void* arpack_hip_malloc(size_t bytes) {
 void arpack_hip_free(void* p) {
     if (p) (void)hipFree(p);
 }
+// Both complete before they return: hipMemset and a device-to-device
+// hipMemcpy may still be in flight on the null stream when they return, and the
+// engine's non-blocking stream does not order against it (a memset of a fresh
+// Z landed after dseupd had written it: zero rows on one rank of an 8-process
+// rehearsal).
 int arpack_hip_memcpy(void* dst, const void* src, size_t bytes) {
-    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? 0 : -1;
+    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess &&
+                   hipStreamSynchronize(nullptr) == hipSuccess
+               ? 0
+               : -1;
 }
 int arpack_hip_memset(void* dst, int value, size_t bytes) {
-    return hipMemset(dst, value, bytes) == hipSuccess ? 0 : -1;
+    return hipMemset(dst, value, bytes) == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess
+               ? 0
+               : -1;
 }
 int arpack_hip_synchronize(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
 

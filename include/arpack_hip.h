@@ -206,8 +206,8 @@ void arpack_hip_set_stream(void* stream);
 /* Device memory helpers (so callers need no other GPU runtime binding). */
 void* arpack_hip_malloc(size_t bytes);
 void arpack_hip_free(void* p);
-int arpack_hip_memcpy(void* dst, const void* src, size_t bytes); /* any direction */
-int arpack_hip_memset(void* dst, int value, size_t bytes);
+int arpack_hip_memcpy(void* dst, const void* src, size_t bytes); /* any direction; complete on return */
+int arpack_hip_memset(void* dst, int value, size_t bytes); /* complete on return */
 int arpack_hip_synchronize(void);
 
 /* Register a CSR matrix (rowptr int64[n+1], col int32[nnz], val f64[nnz]).

@@ -274,6 +274,9 @@ def main():
         pkg.comm_destroy()
         dist.destroy_process_group()
         return
+    # diagnostics for the residual checks: this rank's basis before *eupd
+    vv = s.v.numpy() if hasattr(s.v, "numpy") else np.asarray(s.v)
+    res["vnorm"] = np.linalg.norm(vv.reshape(-1, s.ldv)[:, :nloc], axis=1)
     if ns:
         dr, di, z, nconv = s.eupd(dist=D)
         res.update(d=dr, di=di)
@@ -286,6 +289,7 @@ def main():
     ncols = int(g["nev"]) + (1 if ns else 0)
     res.update(iparam=s.iparam.copy(), info=s.info.copy(), ritz=np.asarray(ritz),
                z=z.reshape(ncols, nloc)[:nconv].T.copy(), rows=np.array([r0, r1]))
+    res["znorm"] = np.linalg.norm(res["z"], axis=0)
     np.savez(os.path.join(out, "rank%d.npz" % rank), **res)
     dist.barrier()
     del D
