@@ -172,6 +172,16 @@ def device_count() -> int:
     return lib().arpack_hip_device_count()
 
 
+def pci_bus_id(device: int = 0) -> str:
+    """PCI bus id of a device (arpack_hip_device_pci_bus_id); "" if unknown."""
+    buf = C.create_string_buffer(64)
+    L = lib()
+    L.arpack_hip_device_pci_bus_id.argtypes = [C.c_int, C.c_char_p, C.c_int]
+    if L.arpack_hip_device_pci_bus_id(int(device), buf, 64) != 0:
+        return ""
+    return buf.value.decode()
+
+
 # ----------------------------------------------------------------------------- arrays
 class DeviceBuffer:
     """A float64 buffer in HBM, allocated through the engine's own HIP runtime
@@ -1024,17 +1034,18 @@ def comm_init(nranks: int, rank: int, uid: bytes, device: int = 0):
 
 
 _HOST_ALLREDUCE = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int, C.c_void_p)
-_HOST_HALO = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
-                         C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
-                         C.c_void_p)
+_HOST_P2P = C.CFUNCTYPE(None, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                        C.POINTER(C.POINTER(C.c_double)), C.POINTER(C.c_int64), C.c_void_p)
 _host_cbs = None
 
 
 def comm_init_host(nranks: int, rank: int, device: int = 0):
     """Engine communicator over the host-staged transport: every allreduce and
-    halo exchange goes through torch.distributed (the default process group,
-    e.g. gloo) instead of RCCL -- for rehearsing several ranks where RCCL
-    cannot run them (more ranks than GPUs).  arpack_hip_comm_init_host."""
+    every point-to-point group of the distributed SpMV goes through
+    torch.distributed (the default process group, e.g. gloo) instead of RCCL --
+    for rehearsing several ranks where RCCL cannot run them (more ranks than
+    GPUs).  The groups are the ones RCCL runs (same device slices, counts and
+    offsets); only the wire differs.  arpack_hip_comm_init_host."""
     import torch
     import torch.distributed as dist
     global _host_cbs
@@ -1045,25 +1056,29 @@ def comm_init_host(nranks: int, rank: int, device: int = 0):
         dist.all_reduce(t)
         a[:] = t.numpy()
 
-    def halo(slo, nsl, rlo, nrl, shi, nsh, rhi, nrh, ctx):
-        reqs, recv, sent = [], [], []
-        for peer, sp, ns, rp_, nr in ((rank - 1, slo, nsl, rlo, nrl), (rank + 1, shi, nsh, rhi, nrh)):
-            if ns:
-                sent.append(torch.from_numpy(np.ctypeslib.as_array(sp, (ns,)).copy()))
-                reqs.append(dist.isend(sent[-1], peer))
-            if nr:
-                t = torch.empty(nr, dtype=torch.float64)
-                reqs.append(dist.irecv(t, peer))
-                recv.append((rp_, nr, t))
-        for q in reqs:
+    def p2p(nops, peer, is_send, bufs, count, ctx):
+        # every transfer posted non-blocking, then all completed (arpack_hip.h:
+        # transfers between a pair match in posting order)
+        reqs, recv = [], []
+        for k in range(nops):
+            cnt = int(count[k])
+            a = np.ctypeslib.as_array(bufs[k], (cnt,))
+            if is_send[k]:
+                t = torch.from_numpy(a.copy())
+                reqs.append((dist.isend(t, int(peer[k])), t))
+            else:
+                t = torch.empty(cnt, dtype=torch.float64)
+                reqs.append((dist.irecv(t, int(peer[k])), t))
+                recv.append((a, t))
+        for q, _ in reqs:
             q.wait()
-        for rp_, nr, t in recv:
-            np.ctypeslib.as_array(rp_, (nr,))[:] = t.numpy()
+        for a, t in recv:
+            a[:] = t.numpy()
 
     L = lib()
     _declare_dist(L)
-    cbs = (_HOST_ALLREDUCE(allreduce), _HOST_HALO(halo))
-    L.arpack_hip_comm_init_host.argtypes = [C.c_int, C.c_int, _HOST_ALLREDUCE, _HOST_HALO,
+    cbs = (_HOST_ALLREDUCE(allreduce), _HOST_P2P(p2p))
+    L.arpack_hip_comm_init_host.argtypes = [C.c_int, C.c_int, _HOST_ALLREDUCE, _HOST_P2P,
                                             C.c_void_p, C.c_int]
     if L.arpack_hip_comm_init_host(nranks, rank, cbs[0], cbs[1], None, device) != 0:
         raise RuntimeError("arpack_hip_comm_init_host failed")
@@ -1072,6 +1087,11 @@ def comm_init_host(nranks: int, rank: int, device: int = 0):
 
 def comm_destroy():
     lib().arpack_hip_comm_destroy()
+
+
+def comm_size() -> int:
+    """Ranks of the engine's communicator (arpack_hip_comm_size; 1 without one)."""
+    return lib().arpack_hip_comm_size()
 
 
 def comm_failed() -> bool:

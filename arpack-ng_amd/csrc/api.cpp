@@ -234,6 +234,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         }
         if (dist) {
             S->dist = dist;
+            S->dist_gen = dist->comm_gen;
             S->row0 = dist->row0;
         }
         S->tol = *tol;
@@ -252,6 +253,16 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             return;
         }
         S = it->second.get();
+        // the decomposition this solve started on must still be the caller's:
+        // a distribution that was freed and rebuilt (PARPACK rebinding to
+        // another communicator) may even reuse the address, so the generation
+        // of its communicator is checked too
+        if (S->dist != dist || (dist && dist->comm && !comm_alive(dist->comm, S->dist_gen))) {
+            g_sym.erase(it);
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
         S->tol = *tol;  // the ICB passes tol by value on every call (SRC/icbads.F90:14)
         S->iparam = iparam;
         S->ipntr = ipntr;
@@ -675,6 +686,17 @@ int arpack_hip_device_count(void) {
         return 0;
     }
     return c;
+}
+
+// PCI bus id ("dddd:bb:dd.f") of a device: bench.py reports which GPU every rank
+// of a multi-GPU run drove
+int arpack_hip_device_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13) return -1;
+    if (hipDeviceGetPCIBusId(buf, len, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return 0;
 }
 
 void arpack_hip_set_stream(void* stream) { g_stream = (hipStream_t)stream; }

@@ -25,9 +25,9 @@ struct Comm {
     double* d_flag = nullptr;  // device scratch of dist_all_ok (allocated at init)
     int failed = 0;            // sticky: a collective or the transport reported an error
     // host-staged transport (arpack_hip_comm_init_host): the launcher's own
-    // collectives move the scalars and halos through host memory
+    // collectives move the scalars and the SpMV's exchanges through host memory
     arpack_hip_host_allreduce_fn h_allreduce = nullptr;
-    arpack_hip_host_halo_fn h_halo = nullptr;
+    arpack_hip_host_p2p_fn h_p2p = nullptr;
     void* h_ctx = nullptr;
     std::vector<double> h_buf;
 };
@@ -42,7 +42,7 @@ uint64_t comm_gen(const Comm* c) { return c ? c->gen : 0; }
 bool comm_alive(const Comm* c, uint64_t gen) { return c && c == g_comm && c->gen == gen; }
 double* comm_flag(const Comm* c) { return c ? c->d_flag : nullptr; }
 bool comm_has_p2p(const Comm* c) { return c && c->nccl_p2p; }
-bool comm_is_host(const Comm* c) { return c && c->h_halo; }
+bool comm_is_host(const Comm* c) { return c && c->h_p2p; }
 
 // Record an RCCL / HIP failure of a collective: the communicator is marked
 // failed and the engine's drivers turn that into info = -9999 at their next
@@ -147,13 +147,13 @@ int arpack_hip_comm_init(int nranks, int rank, const char* id, int device) {
 }
 
 int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn allreduce,
-                              arpack_hip_host_halo_fn halo, void* ctx, int device) {
-    if (!allreduce || !halo || nranks < 1 || rank < 0 || rank >= nranks) return -1;
+                              arpack_hip_host_p2p_fn p2p, void* ctx, int device) {
+    if (!allreduce || !p2p || nranks < 1 || rank < 0 || rank >= nranks) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
     auto* c = ahip::comm_new(nranks, rank, device);
     if (!c) return -2;
     c->h_allreduce = allreduce;
-    c->h_halo = halo;
+    c->h_p2p = p2p;
     c->h_ctx = ctx;
     if (ahip::g_comm) arpack_hip_comm_destroy();
     ahip::g_comm = c;
@@ -181,25 +181,63 @@ int arpack_hip_comm_allreduce(double* dev, int count) {
 
 namespace ahip {
 
-// Halo exchange of the distributed SpMV (grouped point-to-point over xGMI).
-static void comm_halo_host(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only) {
-    const int r = c->rank, P = c->nranks;
-    const int64_t slo = r > 0 ? D.send_lo : 0, shi = r < P - 1 && !hi_only ? D.send_hi : 0;
-    const int64_t hlo = r > 0 && !hi_only ? D.halo_lo : 0, hhi = r < P - 1 ? D.halo_hi : 0;
-    std::vector<double> b((size_t)(slo + shi + hlo + hhi));
-    double *bsl = b.data(), *bsh = bsl + slo, *brl = bsh + shi, *brh = brl + hlo;
-    bool ok = true;
-    if (slo) ok = ok && hipMemcpyAsync(bsl, D.x_mid(), 8 * slo, hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (shi)
-        ok = ok && hipMemcpyAsync(bsh, D.x_mid() + D.nloc - shi, 8 * shi, hipMemcpyDeviceToHost, s) ==
-                       hipSuccess;
-    ok = ok && hipStreamSynchronize(s) == hipSuccess;
-    c->h_halo(bsl, slo, brl, hlo, bsh, shi, brh, hhi, c->h_ctx);  // collective: always joined
-    if (hlo) ok = ok && hipMemcpyAsync(D.x_ext, brl, 8 * hlo, hipMemcpyHostToDevice, s) == hipSuccess;
-    if (hhi)
-        ok = ok && hipMemcpyAsync(D.x_mid() + D.nloc, brh, 8 * hhi, hipMemcpyHostToDevice, s) ==
-                       hipSuccess;
-    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+// One group of point-to-point transfers: every exchange of the distributed
+// SpMV (the neighbour halo, the symmetric form's forward spill, the ghost
+// lists, the all-gather) is built as such a list by the functions below and run
+// by either transport -- RCCL (ncclSend / ncclRecv between ncclGroupStart and
+// ncclGroupEnd, on the stream) or the host-staged one (the send slices copied
+// to host memory, the launcher's per-peer send / recv, the received slices
+// copied back).  So the host rehearsal moves exactly the device slices, counts
+// and offsets the RCCL path moves; only the wire differs.
+struct P2pOp {
+    int peer;
+    int send;      // 1: send `count` doubles from buf to peer; 0: receive into buf
+    double* buf;   // device
+    int64_t count;
+};
+
+static void comm_group(const Comm* c, const std::vector<P2pOp>& ops, hipStream_t s, bool p2p) {
+    if (c->h_p2p) {
+        int64_t tot = 0;
+        for (const P2pOp& o : ops) tot += o.count;
+        std::vector<double> h((size_t)tot);
+        std::vector<int> peer, kind;
+        std::vector<double*> hb;
+        std::vector<int64_t> cnt;
+        bool ok = true;
+        int64_t at = 0;
+        for (const P2pOp& o : ops) {
+            double* hp = h.data() + at;
+            at += o.count;
+            if (o.send)
+                ok = ok && hipMemcpyAsync(hp, o.buf, sizeof(double) * o.count, hipMemcpyDeviceToHost, s) ==
+                               hipSuccess;
+            peer.push_back(o.peer);
+            kind.push_back(o.send);
+            hb.push_back(hp);
+            cnt.push_back(o.count);
+        }
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
+        // the transport is joined even after a local copy failure, so the peers
+        // are not left waiting; the failure is recorded
+        c->h_p2p((int)ops.size(), peer.data(), kind.data(), hb.data(), cnt.data(), c->h_ctx);
+        for (size_t k = 0; k < ops.size(); ++k)
+            if (!ops[k].send)
+                ok = ok && hipMemcpyAsync(ops[k].buf, hb[k], sizeof(double) * ops[k].count,
+                                          hipMemcpyHostToDevice, s) == hipSuccess;
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
+        note(c, ok);
+        return;
+    }
+    if (!c->nccl) return;
+    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (const P2pOp& o : ops) {
+        const ncclResult_t e = o.send ? ncclSend(o.buf, (size_t)o.count, ncclDouble, o.peer, cm, s)
+                                      : ncclRecv(o.buf, (size_t)o.count, ncclDouble, o.peer, cm, s);
+        ok = ok && e == ncclSuccess;
+    }
+    ok = ncclGroupEnd() == ncclSuccess && ok;
     note(c, ok);
 }
 
@@ -209,73 +247,49 @@ void comm_spill(const Comm* c, const double* send, int64_t nsend, double* recv, 
                 hipStream_t s, bool p2p) {
     if (!c || c->nranks == 1) return;
     const int r = c->rank, P = c->nranks;
-    const int64_t ns = r < P - 1 ? nsend : 0, nr = r > 0 ? nrecv : 0;
-    if (c->h_halo) {
-        std::vector<double> b((size_t)(ns + nr));
-        bool ok = true;
-        if (ns) ok = hipMemcpyAsync(b.data(), send, 8 * ns, hipMemcpyDeviceToHost, s) == hipSuccess;
-        ok = ok && hipStreamSynchronize(s) == hipSuccess;
-        c->h_halo(nullptr, 0, b.data() + ns, nr, b.data(), ns, nullptr, 0, c->h_ctx);
-        if (nr)
-            ok = ok && hipMemcpyAsync(recv, b.data() + ns, 8 * nr, hipMemcpyHostToDevice, s) == hipSuccess;
-        ok = ok && hipStreamSynchronize(s) == hipSuccess;
-        note(c, ok);
-        return;
-    }
-    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
-    bool ok = ncclGroupStart() == ncclSuccess;
-    if (ns) ok = ncclSend(send, (size_t)ns, ncclDouble, r + 1, cm, s) == ncclSuccess && ok;
-    if (nr) ok = ncclRecv(recv, (size_t)nr, ncclDouble, r - 1, cm, s) == ncclSuccess && ok;
-    ok = ncclGroupEnd() == ncclSuccess && ok;
-    note(c, ok);
+    std::vector<P2pOp> ops;
+    if (r < P - 1 && nsend) ops.push_back({r + 1, 1, const_cast<double*>(send), nsend});
+    if (r > 0 && nrecv) ops.push_back({r - 1, 0, recv, nrecv});
+    comm_group(c, ops, s, p2p);
 }
 
-// hi_only: the symmetric-storage SpMV reads x only at and above its own rows,
+// Halo exchange of the banded distributed SpMV: my first send_lo rows to
+// rank-1 and my last send_hi rows to rank+1; halo_lo rows from rank-1 into the
+// head of x_ext, halo_hi rows from rank+1 after my rows.  hi_only: the
+// symmetric-storage SpMV with the spill reads x only at and above its own rows,
 // so only the hi halo travels (my first rows to rank-1, rank+1's to me).
 void comm_halo(const Comm* c, const DistOp& D, hipStream_t s, bool hi_only, bool p2p) {
     if (!c || c->nranks == 1) return;
-    if (c->h_halo) return comm_halo_host(c, D, s, hi_only);
     const int r = c->rank, P = c->nranks;
-    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
-    bool ok = ncclGroupStart() == ncclSuccess;
-    auto chk = [&](ncclResult_t e) { ok = ok && e == ncclSuccess; };
+    std::vector<P2pOp> ops;
     if (r > 0) {
-        if (D.send_lo) chk(ncclSend(D.x_mid(), (size_t)D.send_lo, ncclDouble, r - 1, cm, s));
-        if (D.halo_lo && !hi_only) chk(ncclRecv(D.x_ext, (size_t)D.halo_lo, ncclDouble, r - 1, cm, s));
+        if (D.send_lo) ops.push_back({r - 1, 1, D.x_mid(), D.send_lo});
+        if (D.halo_lo && !hi_only) ops.push_back({r - 1, 0, D.x_ext, D.halo_lo});
     }
     if (r < P - 1) {
-        if (D.send_hi && !hi_only)
-            chk(ncclSend(D.x_mid() + D.nloc - D.send_hi, (size_t)D.send_hi, ncclDouble, r + 1, cm, s));
-        if (D.halo_hi) chk(ncclRecv(D.x_mid() + D.nloc, (size_t)D.halo_hi, ncclDouble, r + 1, cm, s));
+        if (D.send_hi && !hi_only) ops.push_back({r + 1, 1, D.x_mid() + D.nloc - D.send_hi, D.send_hi});
+        if (D.halo_hi) ops.push_back({r + 1, 0, D.x_mid() + D.nloc, D.halo_hi});
     }
-    chk(ncclGroupEnd());
-    note(c, ok);
+    comm_group(c, ops, s, p2p);
 }
 
-// The general distributed SpMV's exchange over RCCL: one group of point-to-
-// point transfers, every peer pair only in the direction it has data for.
+// The general distributed SpMV's exchange: one group of point-to-point
+// transfers, every peer pair only in the direction it has data for.
 void comm_ghosts(const Comm* c, const DistOp& D, hipStream_t s, bool p2p) {
-    if (!c || c->nranks == 1 || !c->nccl) return;
+    if (!c || c->nranks == 1) return;
     const int r = c->rank, P = c->nranks;
-    ncclComm_t cm = p2p && c->nccl_p2p ? c->nccl_p2p : c->nccl;
-    bool ok = ncclGroupStart() == ncclSuccess;
-    auto chk = [&](ncclResult_t e) { ok = ok && e == ncclSuccess; };
+    std::vector<P2pOp> ops;
     for (int q = 0; q < P; ++q) {
         if (q == r) continue;
         if (D.mode == DistOp::kGhostLists) {
-            if (D.send_cnt[q])
-                chk(ncclSend(D.send_buf + D.send_off[q], (size_t)D.send_cnt[q], ncclDouble, q, cm, s));
-            if (D.recv_cnt[q])
-                chk(ncclRecv(D.x_ext + D.nloc + D.recv_off[q], (size_t)D.recv_cnt[q], ncclDouble, q,
-                             cm, s));
+            if (D.send_cnt[q]) ops.push_back({q, 1, D.send_buf + D.send_off[q], D.send_cnt[q]});
+            if (D.recv_cnt[q]) ops.push_back({q, 0, D.x_ext + D.nloc + D.recv_off[q], D.recv_cnt[q]});
         } else {  // kAllGather
-            if (D.nloc) chk(ncclSend(D.x_mid(), (size_t)D.nloc, ncclDouble, q, cm, s));
-            if (D.peer_nloc[q])
-                chk(ncclRecv(D.x_ext + D.peer_row0[q], (size_t)D.peer_nloc[q], ncclDouble, q, cm, s));
+            if (D.nloc) ops.push_back({q, 1, D.x_mid(), D.nloc});
+            if (D.peer_nloc[q]) ops.push_back({q, 0, D.x_ext + D.peer_row0[q], D.peer_nloc[q]});
         }
     }
-    chk(ncclGroupEnd());
-    note(c, ok);
+    comm_group(c, ops, s, p2p);
 }
 
 }  // namespace ahip

@@ -351,6 +351,9 @@ int arpack_hip_csr_download(const arpack_hip_csr* A, int64_t* rowptr, int32_t* c
 }
 
 int arpack_hip_csr_spmv(const arpack_hip_csr* A, const double* x, double* y) {
+    // x may come from the caller's own GPU work on a non-blocking stream, which
+    // the null stream does not order against: complete it first
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
     ahip::dev::csr_spmv(nullptr, A->A, x, y);
     // synchronous like the reference callers' OP: y is complete on return
     return hipStreamSynchronize(nullptr) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -1;
@@ -376,9 +379,14 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
         return 0;
     }
     // a general operator's block (ghost lists / all-gather) has no spill
-    // exchange for the transposed terms: full storage (the mode is the same on
-    // every rank, so no agreement is needed)
-    if (A->dist && ahip_dist_mode(A->dist) != 0) return -1;
+    // exchange for the transposed terms: full storage stays, reported as kept
+    // (1, as in deterministic mode) -- the mode is the same on every rank, so no
+    // agreement is needed.  (A banded block declared symmetric before
+    // arpack_hip_dist_create keeps the neighbour halo and symmetric storage.)
+    if (A->dist && ahip_dist_mode(A->dist) != 0) {
+        csr_full_storage(A);
+        return 1;
+    }
     if (ahip::deterministic()) {  // the fixed-order full-storage SpMV stays
         if (c && !ahip::dist_all_ok(c, 1)) return -2;
         csr_full_storage(A);

@@ -20,43 +20,21 @@ __global__ void k_pack(int64_t m, const int32_t* __restrict__ idx, const double*
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride)
         out[k] = x[idx[k]];
 }
-__global__ void k_gather(int64_t m, const int64_t* __restrict__ g, const double* __restrict__ src,
-                         double* __restrict__ out) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride)
-        out[k] = src[g[k]];
-}
 inline unsigned grid_for_rows(int64_t m) {
     const int64_t g = (m + 255) / 256;
     return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 }  // namespace
 
-// The general operator's exchange (kGhostLists / kAllGather).  RCCL: the
-// packed ghost rows (or the whole block) in one group of send / recv.  The
-// host-staged rehearsal transport has only an allreduce for arbitrary
-// patterns: each rank contributes its block to a zeroed global x and the sum
-// is the gathered x (exact: one nonzero term per entry).
+// The general operator's exchange (kGhostLists / kAllGather): the requested
+// rows packed into send_buf (k_pack over send_idx), then one group of
+// point-to-point transfers -- the same group on RCCL and on the host-staged
+// rehearsal transport (comm_ghosts).
 static void exchange_general(const DistOp& D, hipStream_t s, bool p2p) {
-    if (!comm_is_host(D.comm)) {
-        if (D.mode == DistOp::kGhostLists && D.nsend > 0)
-            hipLaunchKernelGGL(k_pack, dim3(grid_for_rows(D.nsend)), dim3(256), 0, s, D.nsend, D.send_idx,
-                               D.x_mid(), D.send_buf);
-        comm_ghosts(D.comm, D, s, p2p);
-        return;
-    }
-    double* g = D.mode == DistOp::kGhostLists ? D.gbuf : D.x_ext;
-    if (D.mode == DistOp::kGhostLists) {
-        (void)hipMemsetAsync(g, 0, sizeof(double) * D.n_global, s);
-        dev::copy(s, D.nloc, D.x_mid(), g + D.row0);
-    } else {  // x_mid is in place: zero the other ranks' blocks
-        (void)hipMemsetAsync(g, 0, sizeof(double) * D.row0, s);
-        (void)hipMemsetAsync(g + D.row0 + D.nloc, 0, sizeof(double) * (D.n_global - D.row0 - D.nloc), s);
-    }
-    comm_allreduce_sum(D.comm, g, (int)D.n_global, s);
-    if (D.mode == DistOp::kGhostLists && D.halo_hi > 0)
-        hipLaunchKernelGGL(k_gather, dim3(grid_for_rows(D.halo_hi)), dim3(256), 0, s, D.halo_hi,
-                           D.ghost_glob, g, D.x_ext + D.nloc);
+    if (D.mode == DistOp::kGhostLists && D.nsend > 0)
+        hipLaunchKernelGGL(k_pack, dim3(grid_for_rows(D.nsend)), dim3(256), 0, s, D.nsend, D.send_idx,
+                           D.x_mid(), D.send_buf);
+    comm_ghosts(D.comm, D, s, p2p);
 }
 
 void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p) {
@@ -115,8 +93,12 @@ int arpack_hip_kit_halo_plan(int P, int r, const double* tab, int64_t* out) {
         return std::max<int64_t>(0, (int64_t)tab[4 * q + 3] - (R0(q) + NL(q) - 1));
     };
     if (P < 1 || r < 0 || r >= P) return -1;
-    for (int q = 0; q < P; ++q) {  // contiguous blocks, halos only from the neighbours
-        if (q > 0 && R0(q) != R0(q - 1) + NL(q - 1)) return -3;
+    // contiguous blocks in rank order, checked for every rank before any reach
+    // (a -4 sends the caller to the general plan, which needs this layout)
+    if (R0(0) != 0) return -3;
+    for (int q = 1; q < P; ++q)
+        if (R0(q) != R0(q - 1) + NL(q - 1)) return -3;
+    for (int q = 0; q < P; ++q) {  // halos only from the neighbours
         if (q > 0 && HLO(q) > NL(q - 1)) return -4;
         if (q < P - 1 && HHI(q) > NL(q + 1)) return -4;
         if ((q == 0 && HLO(q) > 0) || (q == P - 1 && HHI(q) > 0)) return -4;
@@ -134,10 +116,9 @@ namespace {
 using namespace ahip;
 
 void free_general(DistOp& o) {
-    for (void* p : {(void*)o.x_ext, (void*)o.send_idx, (void*)o.send_buf, (void*)o.ghost_glob,
-                    (void*)o.gbuf})
+    for (void* p : {(void*)o.x_ext, (void*)o.send_idx, (void*)o.send_buf, (void*)o.ghost_glob})
         if (p) (void)hipFree(p);
-    o.x_ext = o.send_buf = o.gbuf = nullptr;
+    o.x_ext = o.send_buf = nullptr;
     o.send_idx = nullptr;
     o.ghost_glob = nullptr;
 }
@@ -175,20 +156,27 @@ bool upload(T** dst, const std::vector<T>& h) {
 // more than half of all off-block rows (a dense coupling, e.g. config 5's
 // random operator at small P) the lists do not pay and every rank gathers the
 // whole x (kAllGather; AHIP_DIST_ALLGATHER=1 forces it).
-int ghost_plan(arpack_hip_csr* A, DistOp& o, const Comm* c, int P, int r) {
-    const int64_t nloc = o.nloc, row0 = o.row0, nnz = A->A.nnz;
+// The sorted distinct off-block columns of a block's rows (its ghosts; global
+// indices).  false if the columns could not be read.
+bool ghost_cols(const arpack_hip_csr* A, int64_t row0, int64_t nloc, std::vector<int64_t>& g) {
+    const int64_t nnz = A->A.nnz;
     std::vector<int32_t> hc((size_t)nnz);
-    bool ok = nnz == 0 || hipMemcpy(hc.data(), A->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost) ==
-                              hipSuccess;
+    g.clear();
+    if (nnz > 0 && hipMemcpy(hc.data(), A->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+    for (int32_t v : hc)
+        if (v < row0 || v >= row0 + nloc) g.push_back(v);
+    std::sort(g.begin(), g.end());
+    g.erase(std::unique(g.begin(), g.end()), g.end());
+    return true;
+}
+
+int ghost_plan(arpack_hip_csr* A, DistOp& o, const Comm* c, int P, int r) {
+    const int64_t nloc = o.nloc, row0 = o.row0;
     std::vector<int64_t> g;
-    if (ok) {
-        for (int32_t v : hc)
-            if (v < row0 || v >= row0 + nloc) g.push_back(v);
-        std::sort(g.begin(), g.end());
-        g.erase(std::unique(g.begin(), g.end()), g.end());
-    }
-    hc = std::vector<int32_t>();
-    if (!dist_all_ok(c, ok)) return -1;
+    const bool ok0 = ghost_cols(A, row0, nloc, g);
+    if (!dist_all_ok(c, ok0)) return -1;
+    bool ok = true;
     auto owner = [&](int64_t col) {
         return (int)(std::upper_bound(o.peer_row0.begin(), o.peer_row0.end(), col) - o.peer_row0.begin()) - 1;
     };
@@ -251,7 +239,6 @@ int ghost_plan(arpack_hip_csr* A, DistOp& o, const Comm* c, int P, int r) {
          upload(&o.send_idx, sidx) &&
          hipMalloc(&o.send_buf, sizeof(double) * (o.nsend > 0 ? o.nsend : 1)) == hipSuccess &&
          upload(&o.ghost_glob, g);
-    if (ok && comm_is_host(c)) ok = hipMalloc(&o.gbuf, sizeof(double) * o.n_global) == hipSuccess;
     ok = ok && ahip_csr_remap_ghost(A, row0, nloc, o.ghost_glob, o.halo_hi) == 0;
     return dist_all_ok(c, ok) ? 0 : -1;
 }
@@ -288,7 +275,23 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
         ok_tab = 0;
     (void)hipFree(d);
     if (!dist_all_ok(c, ok_tab)) return -1;
+    // the layout every plan needs, agreed from the shared table (so every rank
+    // returns the same code): blocks contiguous from row 0 covering
+    // [0, n_global), and every rank's columns inside [0, n_global) -- the
+    // general plan's owner lookup and the remap assume both
     int64_t plan[4];
+    {
+        int64_t tot = 0;
+        for (int q = 0; q < P; ++q) tot += (int64_t)tab[4 * q + 1];
+        if (tot != n_global || (P > 0 && (int64_t)tab[0] != 0)) return -3;
+        for (int q = 0; q < P; ++q) {
+            if (q > 0 && (int64_t)tab[4 * q] != (int64_t)tab[4 * (q - 1)] + (int64_t)tab[4 * (q - 1) + 1])
+                return -3;
+            if ((int64_t)tab[4 * q + 1] > 0 &&
+                ((int64_t)tab[4 * q + 2] < 0 || (int64_t)tab[4 * q + 3] >= n_global))
+                return -1;
+        }
+    }
     int rc = arpack_hip_kit_halo_plan(P, r, tab.data(), plan);
     // -4: some rank's columns reach past its neighbours' rows (a general
     // operator): ghost lists or the all-gather instead of the slab halo.  A
@@ -297,9 +300,34 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
     // the north star's 4096 rows against a 1.25e6-row share) goes to the
     // general plan too, on every rank if on any.
     // (AHIP_DIST_GHOSTS=0: a valid slab halo is always kept)
+    // A block declared symmetric on every rank keeps a valid slab halo whatever
+    // its width: the upper-triangle SpMV it enables halves the matrix stream,
+    // which no saving in halo rows repays, and a ghost-list block could only
+    // run full storage (a wide band at small nloc lost symmetric
+    // storage to the pricing).
+    // A slab is "wide" when its halo rows exceed half of the block; a wide slab
+    // goes to ghost lists only where the block's distinct ghost columns are
+    // fewer than half of the slab's rows (a sparse long-range coupling) -- a
+    // band or stencil reads nearly every slab row anyway (a 3-D stencil at 8
+    // ranks: ghosts = halo planes), and keeps the slab, the symmetric-storage
+    // form and its one neighbour exchange.
     const char* gv = std::getenv("AHIP_DIST_GHOSTS");
-    const bool price = !(gv && gv[0] == '0');
-    if (rc == 0 && P > 1 && price && !dist_all_ok(c, 2 * (plan[0] + plan[1]) <= nloc)) rc = -4;
+    const bool was_sym0 = A->A.kernel == ahip::dev::kCsrSymSell;
+    const bool all_sym = dist_all_ok(c, was_sym0) != 0;  // collective: every rank calls it
+    const bool price = !(gv && gv[0] == '0') && !all_sym;
+    if (rc == 0 && P > 1 && price) {
+        const bool wide = 2 * (plan[0] + plan[1]) > nloc;
+        if (!dist_all_ok(c, !wide)) {  // some rank's slab is wide: count the ghosts
+            std::vector<int64_t> g;
+            bool sparse = false, gok = true;
+            if (wide) {
+                gok = ghost_cols(A, row0, nloc, g);
+                sparse = 2 * (int64_t)g.size() < plan[0] + plan[1];
+            }
+            if (!dist_all_ok(c, gok)) return -1;
+            if (!dist_all_ok(c, !sparse)) rc = -4;
+        }
+    }
     if (rc != 0 && rc != -4) return rc;
     auto* D = new arpack_hip_dist;
     DistOp& o = D->D;
@@ -386,6 +414,7 @@ int arpack_hip_dist_rows(arpack_hip_dist** out, int64_t nloc, int64_t row0, int6
 // runs on the null stream.
 int arpack_hip_dist_spmv(const arpack_hip_dist* D, const double* x, double* y) {
     if (!D || !D->D.A) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;  // the caller's x (see csr_spmv)
     ahip::dist_spmv(D->D, nullptr, x, y);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }

@@ -35,7 +35,8 @@ double* comm_flag(const Comm* c);
 bool comm_has_p2p(const Comm* c);
 // the host-staged transport (arpack_hip_comm_init_host) rather than RCCL
 bool comm_is_host(const Comm* c);
-// RCCL exchanges of the general distributed SpMV (grouped send / recv):
+// exchanges of the general distributed SpMV (one group of send / recv, on
+// RCCL or the host-staged transport):
 // kGhostLists -- D.send_buf slices to each peer, ghosts into x_ext after the
 // local rows; kAllGather -- x_mid to every peer, every peer's block into x_ext
 void comm_ghosts(const Comm* c, const DistOp& D, hipStream_t s, bool p2p);
@@ -71,8 +72,7 @@ struct DistOp {
     int32_t* send_idx = nullptr;   // device: local rows packed for the peers, in rank order
     double* send_buf = nullptr;    // device: the packed values
     int64_t nsend = 0;
-    int64_t* ghost_glob = nullptr; // device: global column of each ghost
-    double* gbuf = nullptr;        // device, n_global: host-transport staging of kGhostLists
+    int64_t* ghost_glob = nullptr; // device: global column of each ghost (the column remap)
     double* x_mid() const { return x_ext + halo_lo; }
 };
 

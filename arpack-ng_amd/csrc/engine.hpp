@@ -124,6 +124,7 @@ public:
     // multi-GPU row-block distribution (nullptr: single GPU): n is then the
     // LOCAL row count and row0 the global index of local row 0
     const DistOp* dist = nullptr;
+    uint64_t dist_gen = 0;  // generation of dist->comm when the solve started
     int64_t row0 = 0;
     const dev::Csr* csr = nullptr;
     // mode 3 free run (arpack_hip_dsaupd_shift): OP = (A - sigma I)^{-1} by the

@@ -191,6 +191,9 @@ static int sym_eupd(int rvec, char howmny, int* select, R* d_out, R* z, int ldz,
     }
 
     const bool zdev = is_device_pointer(z);
+    // a device Z the caller may still be writing on another stream (V / resid /
+    // workd in device memory are ordered at attach): complete it first
+    if (zdev && a.host_mode) a.ck(hipDeviceSynchronize());
     // M is the source of an asynchronous copy from pageable memory: it lives
     // until the a.sync() below (a run of 8 processes on one GPU read it freed)
     std::vector<double> M;

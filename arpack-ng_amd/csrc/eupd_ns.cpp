@@ -277,6 +277,9 @@ static int ns_eupd(bool rvec, char howmny, int* select_out, R* dr_out, R* di_out
     a.ck(hipMemcpyAsync(ws.q, Qh.data(), sizeof(double) * Qh.size(), hipMemcpyHostToDevice, a.stream));
     dev::vq_gemm(ws, n, a.d_v, a.d_ld, ncv, ncv, a.d_v, a.d_ld);
     const bool zdev = is_device_pointer(z);
+    // a device Z the caller may still be writing on another stream (V / resid /
+    // workd in device memory are ordered at attach): complete it first
+    if (zdev && a.host_mode) a.ck(hipDeviceSynchronize());
     R* zd = nullptr;
     int64_t ldzd = a.d_ld;
     if (zdev) {

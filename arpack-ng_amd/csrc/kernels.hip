@@ -903,3 +903,31 @@ AHIP_INST(float)
 #undef AHIP_INST
 
 }  // namespace ahip::dev
+
+// ---- test hook: a caller's in-flight GPU work (arpack_hip.h) -------------------
+namespace {
+__global__ void k_delayed_fill(double* __restrict__ dst, const double* __restrict__ src, double value,
+                               int64_t count, long long ticks) {
+    // every wave waits out the delay on the device wall clock (bounded: the
+    // loop ends when the clock passes the mark), then the grid writes
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += stride)
+        dst[k] = src ? src[k] : value;
+}
+}  // namespace
+
+extern "C" int arpack_hip_test_delayed_fill(double* dst, const double* src, double value, int64_t count,
+                                            int delay_us) {
+    static hipStream_t s = nullptr;  // never destroyed: its last kernel may still run
+    if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1;
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        return -1;
+    const long long ticks = (long long)delay_us * khz / 1000;
+    const int64_t g = std::min<int64_t>(std::max<int64_t>((count + 255) / 256, 1), 1024);
+    hipLaunchKernelGGL(k_delayed_fill, dim3((unsigned)g), dim3(256), 0, s, dst, src, value, count, ticks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -63,6 +63,12 @@ int ArraysT<R>::attach(int64_t nn, int nc, R* resid, R* v, int ldv, R* workd) {
         d_ld = ldv;
         d_resid = resid;
         d_workd = workd;
+        // device-pointer mode: the caller may have written V, resid (info = 1)
+        // or workd with its own GPU work on any stream, still in flight -- the
+        // engine's non-blocking stream does not order behind it, and the RCI
+        // contract (SRC/dsaupd.f:228-234) is that the arrays are complete when
+        // *aupd / *eupd is called: make it so before the engine touches them
+        ck(hipDeviceSynchronize());
     }
     return 0;
 }

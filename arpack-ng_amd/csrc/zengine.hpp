@@ -161,6 +161,7 @@ public:
     std::optional<Task> root;
     const zdev::ZCsr* csr = nullptr;  // free-running OP (mode 1)
     const DistOp* dist = nullptr;      // row block of a distributed solve (or null)
+    uint64_t dist_gen = 0;             // generation of dist->comm when the solve started
     int64_t row0 = 0, n_global = 0;
     const R* op_x = nullptr;
     R* op_y = nullptr;

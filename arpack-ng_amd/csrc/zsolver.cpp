@@ -622,6 +622,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         S->n_global = dist ? dist->n_global : n;
         if (dist) {  // row block of a distributed solve (PARPACK's pznaupd)
             S->dist = dist;
+            S->dist_gen = dist->comm_gen;
             S->row0 = dist->row0;
             S->ws.comm = dist->comm;
         }
@@ -642,6 +643,16 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
             return;
         }
         S = it->second.get();
+        // the decomposition this solve started on must still be the caller's:
+        // a distribution that was freed and rebuilt (PARPACK rebinding to
+        // another communicator) may even reuse the address, so the generation
+        // of its communicator is checked too
+        if (S->dist != dist || (dist && dist->comm && !comm_alive(dist->comm, S->dist_gen))) {
+            g_z.erase(it);
+            *info = -9999;
+            *ido = 99;
+            return;
+        }
         S->tol = *tol;
         S->iparam = iparam;
         S->ipntr = ipntr;
@@ -885,6 +896,9 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
     const int64_t ldc = a.d_ld / 2;
     zdev::gemm(ws, n, a.d_v, ldc, ncv, ncv, Qh.data(), a.d_v, ldc);
     const bool zdevp = is_device_pointer(z);
+    // a device Z the caller may still be writing on another stream (V / resid /
+    // workd in device memory are ordered at attach): complete it first
+    if (zdevp && a.host_mode) a.ck(hipDeviceSynchronize());
     R* zd = nullptr;
     int64_t ldzd = ldc;
     if (zdevp) {
@@ -1114,6 +1128,7 @@ int arpack_hip_zcsr_download(const arpack_hip_zcsr* Z, int64_t* rowptr, int32_t*
 }
 
 int arpack_hip_zcsr_spmv(const arpack_hip_zcsr* Z, const double* x, double* y) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;  // the caller's x (see csr_spmv)
     ahip::zdev::zcsr_spmv(nullptr, Z->A, x, y);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }

@@ -37,6 +37,7 @@
 #include <set>
 #include <tuple>
 #include <utility>
+#include <vector>
 
 #include "../../include/arpack_hip.h"
 
@@ -64,21 +65,18 @@ void host_allreduce(double* buf, int count, void* ctx) {
     MPI_Allreduce(MPI_IN_PLACE, buf, count, MPI_DOUBLE, MPI_SUM, static_cast<Binding*>(ctx)->comm);
 }
 
-// send my first nsl entries to rank-1 and my last nsh to rank+1; receive nrl
-// from rank-1 and nrh from rank+1 (the engine's halo contract, arpack_hip.h)
-void host_halo(const double* slo, int64_t nsl, double* rlo, int64_t nrl, const double* shi,
-               int64_t nsh, double* rhi, int64_t nrh, void* ctx) {
+// one group of the engine's point-to-point transfers (arpack_hip.h's host
+// p2p contract): every transfer posted non-blocking, then all completed; one
+// tag, so transfers between a pair match in posting order
+void host_p2p(int nops, const int* peer, const int* is_send, double* const* buf,
+              const int64_t* count, void* ctx) {
     auto* b = static_cast<Binding*>(ctx);
-    MPI_Request rq[4];
-    int k = 0;
-    if (b->rank > 0 && nrl) MPI_Irecv(rlo, (int)nrl, MPI_DOUBLE, b->rank - 1, 71, b->comm, &rq[k++]);
-    if (b->rank < b->size - 1 && nrh)
-        MPI_Irecv(rhi, (int)nrh, MPI_DOUBLE, b->rank + 1, 72, b->comm, &rq[k++]);
-    if (b->rank > 0 && nsl)
-        MPI_Isend(const_cast<double*>(slo), (int)nsl, MPI_DOUBLE, b->rank - 1, 72, b->comm, &rq[k++]);
-    if (b->rank < b->size - 1 && nsh)
-        MPI_Isend(const_cast<double*>(shi), (int)nsh, MPI_DOUBLE, b->rank + 1, 71, b->comm, &rq[k++]);
-    MPI_Waitall(k, rq, MPI_STATUSES_IGNORE);
+    std::vector<MPI_Request> rq((size_t)nops);
+    for (int k = 0; k < nops; ++k) {
+        if (is_send[k]) MPI_Isend(buf[k], (int)count[k], MPI_DOUBLE, peer[k], 71, b->comm, &rq[k]);
+        else MPI_Irecv(buf[k], (int)count[k], MPI_DOUBLE, peer[k], 71, b->comm, &rq[k]);
+    }
+    if (nops) MPI_Waitall(nops, rq.data(), MPI_STATUSES_IGNORE);
 }
 
 void release_binding() {
@@ -108,13 +106,19 @@ void live_end(const void* v, const a_int* ido) {
     else g_live.insert(v);
 }
 
-// Bind the engine's communicator to `fcomm` (collective over it on first use).
-// One communicator at a time: a call on another communicator while a solve is
-// in progress is refused (info = -9999) rather than freeing that solve's
-// distribution under it.
-bool bind_comm(MPI_Fint fcomm) {
+// Bind the engine's communicator to `fcomm` (collective over it on first use;
+// the caller holds g_mu).  One communicator at a time: a continuing call or an
+// *eupd on another communicator while a solve is in progress is refused
+// (info = -9999) rather than freeing that solve's distribution under it.  A
+// fresh *aupd (ido = 0) on another communicator starts a new solve and
+// abandons the ones in progress, as a fresh call abandons the previous solve
+// in the reference (one SAVEd state per routine): their later calls on the old
+// communicator find no binding and return -9999, so an abandoned solve cannot
+// block rebinding for the rest of the process.
+bool bind_comm(MPI_Fint fcomm, bool fresh) {
     if (g_bound && g_bind.key == fcomm) return true;
-    if (g_bound && !g_live.empty()) return false;
+    if (g_bound && !g_live.empty() && !fresh) return false;
+    g_live.clear();
     release_binding();
     MPI_Comm c = MPI_Comm_f2c(fcomm);
     Binding b;
@@ -145,7 +149,7 @@ bool bind_comm(MPI_Fint fcomm) {
         MPI_Bcast(id, 129, MPI_CHAR, 0, b.comm);
         rc = id[128] ? -1 : arpack_hip_comm_init(b.size, b.rank, id, lrank);
     } else {
-        rc = arpack_hip_comm_init_host(b.size, b.rank, host_allreduce, host_halo, &g_bind,
+        rc = arpack_hip_comm_init_host(b.size, b.rank, host_allreduce, host_p2p, &g_bind,
                                        ndev > 0 ? lrank % ndev : 0);
     }
     int ok = rc == 0 ? 1 : 0, all = 0;
@@ -169,7 +173,7 @@ bool bind_comm(MPI_Fint fcomm) {
 // same solve and the *eupd call after it (no collective per RCI call).
 arpack_hip_dist* dist_for(MPI_Fint fcomm, int64_t nloc, bool fresh) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!bind_comm(fcomm)) return nullptr;
+    if (!bind_comm(fcomm, fresh)) return nullptr;
     const auto cur = std::make_pair(fcomm, nloc);
     if (!fresh) {
         auto it = g_cur.find(cur);

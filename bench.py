@@ -73,6 +73,68 @@ def json_stdout():
     return fd
 
 
+def visible_gpus() -> int:
+    """GPUs this process may drive, counted without creating a HIP context in
+    the launching process (torch.cuda.device_count() does not initialise the
+    runtime on this image; it honours HIP_VISIBLE_DEVICES)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` from a plain command (no WORLD_SIZE): start N rank
+    processes, one per GPU, under torch.distributed.run -- the same form the
+    driver uses for N > 1 -- before this process touches the GPU, wait for them,
+    and forward rank 0's JSON line to stdout (everything else to stderr).
+    Returns the exit status.  N above the visible GPU count is an error, unless
+    --host-transport (a rehearsal: every rank on device 0)."""
+    n = args.gpus
+    if not args.host_transport:
+        ndev = visible_gpus()
+        if n > ndev:
+            print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible (one rank per GPU; "
+                  "--host-transport rehearses N ranks on one GPU)", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True)
+
+    def forward(signum, _frame):  # the launcher's own stop reaches every rank
+        p.send_signal(signum)
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    line = None
+    try:
+        for ln in p.stdout:
+            s = ln.strip()
+            if line is None and s.startswith("{"):
+                try:
+                    if "metric" in json.loads(s):
+                        line = s
+                        continue
+                except ValueError:
+                    pass
+            sys.stderr.write(ln)
+        rc = p.wait()
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print("bench.py: the ranks ended without rank 0's JSON line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of `kernel_substr` from the committed rocprofv3 PMC
     summary (profiles/r*_pmc.json, written by tools/pmc_summary.py from separate
@@ -204,34 +266,67 @@ def main():
                          "SpMV forms, so --storage sym keeps the full-storage kernel and every "
                          "solve is bitwise reproducible")
     args = ap.parse_args()
-
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # a plain `bench.py --gpus N`: become the launcher of N ranks (nothing
+        # in this process has touched the GPU yet)
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(world_env or "1")
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher must start "
+              "one rank per requested GPU", file=sys.stderr)
+        sys.exit(2)
     dist = None
     out_fd = json_stdout()
     pkg = load_pkg()
     pkg.set_deterministic(args.deterministic)
     n, nev, ncv = args.n, args.nev, args.ncv
     D = None
+    transport = "none"
+    device = 0
     if world > 1:
         # control plane: gloo (CPU) hands rank 0's RCCL unique id to every rank;
         # the data path (allreduce of the Gram-Schmidt sums, SpMV halos) is RCCL.
         import torch.distributed as dist
+        ndev = pkg.device_count()
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if not args.host_transport and ndev < local_world:
+            # every rank sees the same counts, so every rank leaves here
+            print(f"bench.py rank {rank}: {local_world} ranks on this node but {ndev} GPUs "
+                  "visible (one rank per GPU; --host-transport rehearses on one GPU)",
+                  file=sys.stderr)
+            sys.exit(2)
         dist.init_process_group("gloo")
         if args.host_transport:
             pkg.comm_init_host(world, rank, device=0)
+            transport = "host-staged (gloo)"
         else:
             box = [pkg.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
             # one GPU per rank; a launcher that narrows each rank's visible
             # devices (HIP_VISIBLE_DEVICES) leaves device 0 = this rank's GPU
-            pkg.comm_init(world, rank, box[0], device=local_rank % max(1, pkg.device_count()))
+            device = local_rank % max(1, ndev)
+            pkg.comm_init(world, rank, box[0], device=device)
+            transport = "rccl"
         r0, r1 = pkg.partition_rows(n, world, rank)
     else:
         r0, r1 = 0, n
         if args.force_dist:
             pkg.comm_init(1, 0, pkg.comm_unique_id(), device=0)
+            transport = "rccl"
+    # which GPU every rank drove, and how many ranks the engine's communicator has
+    comm_ranks = pkg.comm_size() if transport != "none" else 1
+    devices = [dict(rank=rank, device=device, pci_bus_id=pkg.pci_bus_id(device),
+                    comm_ranks=comm_ranks)]
+    if dist:
+        allr = [None] * world
+        dist.all_gather_object(allr, devices[0])
+        devices = allr
     t = time.time()
     A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row, r0, r1)
     if world > 1 or args.force_dist:
@@ -451,6 +546,9 @@ def main():
                    "parallelism": "single GPU" if world == 1 else
                    f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
                    f"REHEARSAL row-block x{world} on one GPU, host-staged gloo transport"},
+        "comm": {"transport": transport, "ranks": comm_ranks,
+                 "distinct_gpus": len({d["pci_bus_id"] for d in devices}), "ranks_devices": devices},
+        "rccl_ranks": comm_ranks if transport == "rccl" else 0,
         "lanczos_steps_per_s": nopx / elapsed,
         "solves_in_timed_region": nsolves,
         "time_to_converge": ttc,

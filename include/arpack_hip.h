@@ -200,6 +200,8 @@ typedef struct arpack_hip_csr arpack_hip_csr;
 const char* arpack_hip_version(void);
 /* Number of visible GPUs (0 on a CPU-only host; never initialises a context). */
 int arpack_hip_device_count(void);
+/* PCI bus id "dddd:bb:dd.f" of `device` into buf (len >= 13); 0 or -1. */
+int arpack_hip_device_pci_bus_id(int device, char* buf, int len);
 /* Share a HIP stream (hipStream_t) with the engine; NULL = engine-owned stream. */
 void arpack_hip_set_stream(void* stream);
 
@@ -382,17 +384,22 @@ int arpack_hip_comm_allreduce(double* dev, int count); /* in-place SUM (test hoo
  * communicator saw the failure. */
 int arpack_hip_comm_failed(void);
 /* Host-staged transport in place of RCCL: the engine stages every allreduce
- * (in-place SUM of `count` host doubles) and every halo exchange (send my first
- * nsl / last nsh local entries to rank-1 / rank+1, receive nrl / nrh entries
- * from them) through the launcher's own collectives.  For rehearsing P ranks
- * where RCCL cannot run them (several ranks on one GPU; CI); the data path is
- * identical to the RCCL one apart from the transport. */
+ * (in-place SUM of `count` host doubles) and every point-to-point group of the
+ * distributed SpMV through the launcher's own collectives.  A group is `nops`
+ * transfers: op k sends count[k] doubles from buf[k] to rank peer[k]
+ * (is_send[k] = 1) or receives count[k] doubles from peer[k] into buf[k]
+ * (is_send[k] = 0); the callback posts them all non-blocking and returns when
+ * every one has completed (between one pair of ranks, transfers in one
+ * direction match in posting order, as MPI / gloo guarantee).  The groups are
+ * exactly the ones RCCL runs (the same device slices, counts and offsets:
+ * neighbour halos, the symmetric form's spill, ghost lists, the all-gather), so
+ * rehearsing P ranks where RCCL cannot run them (several ranks on one GPU; CI)
+ * exercises the whole data path apart from the wire. */
 typedef void (*arpack_hip_host_allreduce_fn)(double* buf, int count, void* ctx);
-typedef void (*arpack_hip_host_halo_fn)(const double* send_lo, int64_t nsl, double* recv_lo,
-                                        int64_t nrl, const double* send_hi, int64_t nsh,
-                                        double* recv_hi, int64_t nrh, void* ctx);
+typedef void (*arpack_hip_host_p2p_fn)(int nops, const int* peer, const int* is_send,
+                                       double* const* buf, const int64_t* count, void* ctx);
 int arpack_hip_comm_init_host(int nranks, int rank, arpack_hip_host_allreduce_fn allreduce,
-                              arpack_hip_host_halo_fn halo, void* ctx, int device);
+                              arpack_hip_host_p2p_fn p2p, void* ctx, int device);
 
 typedef struct arpack_hip_dist arpack_hip_dist;
 /* Distributed operator from this rank's CSR rows [row0, row0 + A.n) with GLOBAL
@@ -537,6 +544,12 @@ void arpack_hip_pdnaupd_csr_cycles(const arpack_hip_dist* D, int max_cycles, int
  * paths) reports hipErrorInvalidValue; the solve then returns info = -9999 and
  * a CSR create -2.  k <= 0 disarms.  AHIP_FAULT_AT=k arms it at load. */
 void arpack_hip_fault_inject(long k);
+/* Test hook standing in for a caller's own in-flight GPU work: on a private
+ * non-blocking stream, a kernel waits `delay_us` microseconds (device wall
+ * clock) and then writes count doubles dst[k] = src[k] (src == NULL: value).
+ * Returns at once (0), without waiting for the kernel. */
+int arpack_hip_test_delayed_fill(double* dst, const double* src, double value, int64_t count,
+                                 int delay_us);
 /* Deterministic mode: every SpMV sum in a fixed order, so a solve is bitwise
  * reproducible run to run.  A later arpack_hip_csr_set_symmetric(A, 1) then
  * keeps the full-storage kernel (bitwise SciPy's csr_matvec) and returns 1,

@@ -3,10 +3,12 @@
 torch.distributed env (RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT).
 
 All ranks share one GPU, so the engine's communicator is the host-staged
-transport (arpack_hip_comm_init_host: allreduce and halo exchange through gloo)
-in place of RCCL -- the data path (local partial sums -> allreduce -> phase
-logic, halo plan + extended-x SpMV, global-offset start vector, row-local V*Q)
-is the one the 8-GPU job runs.
+transport (arpack_hip_comm_init_host: allreduce and per-peer send / recv
+through gloo) in place of RCCL -- the data path (local partial sums ->
+allreduce -> phase logic, halo plan + extended-x SpMV with the very send / recv
+groups RCCL runs -- neighbour slabs, ghost lists packed by k_pack, the
+all-gather --, global-offset start vector, row-local V*Q) is the one the 8-GPU
+job runs.
 
   python tests/dist_worker.py CASE FIXTURE OUTDIR [info0]
 CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
@@ -17,7 +19,8 @@ CASE: sym_csr (pdsaupd_csr_cycles), sym_csr_s (the same with the local CSR
       fault_csr / fault_rci (sym_csr / sym_rci with a HIP failure injected on
       rank 1 only: every rank must end with info = -9999),
       general (FIXTURE sparse | dense: an operator that is not banded -- ghost
-      lists / all-gather exchange).
+      lists / all-gather exchange), bad_layout (FIXTURE col | rows:
+      arpack_hip_dist_create's layout checks).
 Writes OUTDIR/rank<r>.npz: iparam, info, ritz, d (+ di), z (local rows)."""
 import os
 import sys
@@ -163,6 +166,28 @@ def general(pkg, out, rank, world, kind):
     del D
 
 
+def bad_layout(pkg, out, rank, world, kind):
+    """arpack_hip_dist_create validates the layout before any plan.
+    kind "col": the last rank's block reads a column past n_global; "rows": the
+    blocks leave a gap.  Every rank
+    must get the same error code (no rank may enter the ghost plan)."""
+    n = 1000 * world
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    nloc = r1 - r0
+    rp = np.arange(nloc + 1, dtype=np.int64)
+    col = np.arange(r0, r1, dtype=np.int32)
+    if kind == "col" and rank == world - 1:
+        col[-1] = n + 5
+    row0 = r0 + (7 if kind == "rows" and rank == world - 1 else 0)
+    A = pkg.CSR.from_arrays(rp, col, np.ones(nloc))
+    try:
+        pkg.DistOp(A, n, row0)
+        rc = 0
+    except RuntimeError as e:
+        rc = int(str(e).split("(")[-1].rstrip(")"))
+    np.savez(os.path.join(out, "rank%d.npz" % rank), rc=np.array([rc]))
+
+
 def lap3d(pkg, out, rank, world, m, cap):
     """BASELINE config 4's family at a rehearsal size: the 3-D 7-pt Laplacian
     m^3 sharded by row blocks (z-slabs: the halo is one m x m plane per side,
@@ -195,8 +220,10 @@ def main():
     dist.init_process_group("gloo")
     pkg = load_pkg()
     pkg.comm_init_host(world, rank, device=0)
-    if case in ("spmv_chain", "sym_mixed", "lap3d", "general"):
-        if case == "lap3d":  # FIXTURE = "m<m>_cap<cycles>"
+    if case in ("spmv_chain", "sym_mixed", "lap3d", "general", "bad_layout"):
+        if case == "bad_layout":  # FIXTURE = col | rows
+            bad_layout(pkg, out, rank, world, fixture)
+        elif case == "lap3d":  # FIXTURE = "m<m>_cap<cycles>"
             m, cap = (int(t[1:]) if t[0] == "m" else int(t[3:]) for t in fixture.split("_"))
             lap3d(pkg, out, rank, world, m, cap)
         elif case == "general":  # FIXTURE = sparse | dense
@@ -233,6 +260,7 @@ def main():
         if case == "sym_csr_s":
             A.set_symmetric(True)
             res["spill"] = np.array([D.spill])
+            res["sym"] = np.array([int(A.symmetric)])
             x = np.random.default_rng(7).standard_normal(n)
             xd = pkg.DeviceBuffer.from_numpy(x[r0:r1].copy())
             yd = pkg.DeviceBuffer(nloc)

@@ -33,6 +33,9 @@ def test_single_rank_with_rccl_communicator():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _one_json(r.stdout)
     assert d["n_gpus"] == 1
+    # the engine's communicator is a real 1-rank RCCL one, on a GPU with a PCI id
+    assert d["rccl_ranks"] == 1 and d["comm"]["transport"] == "rccl"
+    assert d["comm"]["ranks_devices"][0]["pci_bus_id"]
 
 
 def test_two_ranks_one_json_line():
@@ -44,3 +47,26 @@ def test_two_ranks_one_json_line():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _one_json(r.stdout)
     assert d["n_gpus"] == 2 and "REHEARSAL" in d["config"]["parallelism"]
+    assert d["comm"]["ranks"] == 2 and d["rccl_ranks"] == 0
+
+
+def test_plain_command_launches_n_ranks():
+    """`python bench.py --gpus 2 --host-transport` with no launcher: bench.py
+    starts the two ranks itself (torch.distributed.run) and prints one line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--host-transport", *SMALL],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _one_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["comm"]["ranks"] == 2
+    assert [x["rank"] for x in d["comm"]["ranks_devices"]] == [0, 1]
+
+
+def test_more_gpus_than_present_fails():
+    """On a box with fewer GPUs than --gpus (and no rehearsal switch) the run
+    ends non-zero with the device-count message instead of timing one rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "64", *SMALL], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "needs 64 GPUs" in r.stderr
+    assert r.stdout.strip() == ""

@@ -269,23 +269,29 @@ def test_one_rank_device_failure_ends_every_rank(tmp_path, case):
             assert int(r["info"][0]) == -9999, (case, P, [int(q["info"][0]) for q in ranks])
 
 
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("kind,mode", [("sparse", "ghosts"), ("dense", "allgather")])
 def test_general_operator_ranks(tmp_path, kind, mode):
     """An operator that is NOT banded (VERDICT r03 missing #2): a band plus
     random long-range pairs (per-peer ghost lists) and 8 random columns a row
     (all-gather).  The distributed SpMV equals SciPy on every rank's rows to
-    rounding, and the P = 2 and 4 solves give the P = 1 engine's cycles and
+    rounding, and the P = 2, 4 and 8 solves give the P = 1 engine's cycles and
     OP*x (one dlarnv-free start vector) with Ritz values within 1e-10; the
-    Ritz vectors assembled from the ranks have small residuals."""
+    Ritz vectors assembled from the ranks have small residuals.  The exchange
+    is the RCCL path's own send / recv group (k_pack into the packed per-peer
+    buffer, the send / receive offsets) over gloo.  At
+    P = 2 the dense coupling's slab IS the other block, which the plan keeps
+    (the same rows as the all-gather, one neighbour exchange)."""
     import scipy.sparse  # noqa: F401
     sys.path.insert(0, HERE)
     from dist_worker import general_matrix
     A = general_matrix(kind)
     one = _run(tmp_path, "general", kind, 1)
-    for P in (2, 4):
+    for P in (2, 4, 8):
         ranks = _run(tmp_path, "general", kind, P)
+        want = "halo" if (kind == "dense" and P == 2) else mode
         for r in ranks:
-            assert str(r["mode"][0]) == mode, (P, r["mode"])
+            assert str(r["mode"][0]) == want, (P, r["mode"])
             assert float(r["spmv_err"][0]) <= 1e-14, (P, r["spmv_err"])
             assert int(r["info"][0]) == 0
             assert int(r["iparam"][2]) == int(one[0]["iparam"][2]), P
@@ -294,3 +300,41 @@ def test_general_operator_ranks(tmp_path, kind, mode):
         assert _resid(A, _z(ranks), ranks[0]["d"]) <= 1e-8
     if kind == "sparse":  # ghosts only: far fewer than the other ranks' rows
         assert 0 < int(ranks[1]["ghosts"][0]) < A.shape[0] // 4
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("form", sorted(SPILL_FORMS))
+@pytest.mark.parametrize("fixture,P", [("g4_banded", 4), ("g4_banded", 8), ("g3_anderson3d", 8)])
+def test_symmetric_storage_many_ranks(tmp_path, golden, fixture, P, form):
+    """Symmetric storage over 4 and 8 ranks through the per-peer send / recv
+    groups (the two-sided spill-free halo or halo + spill).  g3 at P = 8 is a
+    wide slab at small blocks (1,000 rows, 400-row halo planes each side: the
+    3-D stencil reads every slab row), which keeps the slab plan and symmetric
+    storage (the width pricing used to send it to ghost lists,
+    where set_symmetric failed)."""
+    g = golden(fixture)
+    spec = g["spec"]
+    rp, col, val = (M.banded_sym(*[int(x) for x in spec[1:]]) if str(spec[0]) == "banded_sym"
+                    else M.anderson(int(spec[1]), int(spec[2]), float(spec[3]), int(spec[4])))
+    A = M.to_scipy(rp, col, val)
+    ranks = _run(tmp_path, "sym_csr_s", fixture, P, extra_env=SPILL_FORMS[form])
+    for r in ranks:
+        assert bool(r["spmv_ok"][0])
+        assert bool(r["spill"][0]) == (form == "spill")
+        assert int(r["sym"][0]) == 1
+        assert int(r["info"][0]) == 0
+        assert int(r["iparam"][2]) == int(g["iparam"][2]), (P, r["iparam"][2])
+        assert int(r["iparam"][4]) == int(g["iparam"][4])
+    d = ranks[0]["d"]
+    np.testing.assert_allclose(np.sort(d), np.sort(g["d"]), rtol=1e-10)
+    assert _resid(A, _z(ranks), d) <= 1e-8
+
+
+@pytest.mark.parametrize("kind,rc", [("col", -1), ("rows", -3)])
+def test_dist_create_rejects_bad_layout(tmp_path, kind, rc):
+    """a column outside [0, n_global) or non-contiguous row blocks
+    fail arpack_hip_dist_create with the same code on every rank before any
+    plan is built (the ghost plan's owner lookup and the remap assume both)."""
+    for P in (2, 3):
+        ranks = _run(tmp_path, "bad_layout", kind, P)
+        assert [int(r["rc"][0]) for r in ranks] == [rc] * P, (kind, P)
