@@ -227,6 +227,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             *ido = 99;
             return;
         }
+        S->a.defq = S->ws.defq;  // (a.sync() launches what is still deferred)
         if (csr) {
             S->free_run = true;
             S->csr = csr;
@@ -329,6 +330,9 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             }
             if constexpr (!kShadow) {
                 if (S->shift) {  // mode 3 (bmat = 'I': B x = x for ido = 1 too)
+                    // the solve's deferred finalize does not ride in the solver's
+                    // products: launch it here, ahead of them in stream order
+                    dev::flush_deferred_finalize(S->ws.defq, S->a.stream);
                     if (dev::dshift_apply(*S->shift, S->a.stream, S->op_x, S->op_y, nullptr) < 0) {
                         // the solve broke down or missed its tolerance: OP is not
                         // what the caller asked for, so the Lanczos run stops
@@ -344,11 +348,14 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             if (S->dist) dev::prof_begin(dev::kProfSpmv, S->a.stream);
             else dev::prof_arm(dev::kProfSpmv, S->a.stream);
             if constexpr (!kShadow) {
-                if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y);
-                else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y);
+                if (S->dist) dist_spmv(*S->dist, S->a.stream, S->op_x, S->op_y, false, S->ws.defq);
+                else dev::csr_spmv(S->a.stream, *S->csr, S->op_x, S->op_y, S->ws.defq);
             }
             if (S->dist) dev::prof_end(dev::kProfSpmv, S->a.stream, by);
             else dev::prof_disarm(dev::kProfSpmv, by);
+            // (an SpMV form that cannot carry it has launched it; nothing may
+            // leave this request with a finalize still pending)
+            dev::flush_deferred_finalize(S->ws.defq, S->a.stream);
             continue;
         }
         if (r.ido == SolverT<R>::kPauseIdo) {  // cycle budget spent: park

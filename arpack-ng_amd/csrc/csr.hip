@@ -637,3 +637,50 @@ static int reanalyse(arpack_hip_csr* A, int64_t ncols) {
     if (analyse_window_sell(A, ncols) == -2) return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// ---- test hook: the fused symmetric SpMV's hand-off under uneven load ---------
+namespace {
+__global__ void k_load_stream(double* __restrict__ a, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
+        a[k] = a[k] * 0.5 + 1.0;
+}
+}  // namespace
+
+extern "C" int arpack_hip_test_symspmv_handoff(const arpack_hip_csr* A, const double* x, double* y,
+                                               int fuse, double* load, int64_t load_n, int64_t* heads,
+                                               int64_t cap, double* lo_out) {
+    using namespace ahip::dev;
+    const Csr& M = A->A;
+    if (M.kernel != kCsrSymSell || !M.ss_val) return -1;
+    if (fuse && !csr_spmv_sym_fusable(M)) return -2;
+    static hipStream_t ls = nullptr;  // the competing stream (never destroyed)
+    if (!ls && hipStreamCreateWithFlags(&ls, hipStreamNonBlocking) != hipSuccess) return -3;
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    // the competing read / write stream is issued first, so the SpMV's
+    // workgroups land on CUs it already occupies (uneven arrival at the pairs)
+    if (load && load_n > 0) hipLaunchKernelGGL(k_load_stream, dim3(4096), dim3(256), 0, ls, load, load_n);
+    csr_spmv_sym_as(nullptr, M, x, y, fuse != 0);
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    // chain-head rows (combined through the slots) and the slot_lo halves they read
+    const int chain = M.ss_chain;
+    const int64_t nch = (M.ss_nsb + chain - 1) / chain;
+    std::vector<int64_t> r0((size_t)M.ss_nsb + 1), off((size_t)M.ss_nsb + 1);
+    std::vector<int32_t> pre((size_t)M.ss_nsb);
+    if (hipMemcpy(r0.data(), M.ss_sb_r0, sizeof(int64_t) * r0.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(off.data(), M.ss_sb_off, sizeof(int64_t) * off.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(pre.data(), M.ss_sb_pre, sizeof(int32_t) * pre.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return -3;
+    int64_t k = 0;
+    for (int64_t c = 0; c < nch && k < cap; ++c) {
+        const int64_t b = c * chain;
+        heads[2 * k] = r0[b];
+        heads[2 * k + 1] = pre[b];
+        if (lo_out && pre[b] > 0 &&
+            hipMemcpy(lo_out + r0[b], M.ss_lo + off[b], sizeof(double) * pre[b], hipMemcpyDeviceToHost) !=
+                hipSuccess)
+            return -3;
+        ++k;
+    }
+    return (int)k;
+}

@@ -126,8 +126,19 @@ struct FinArgs {
     int active;  // 0: nothing to run
 };
 
+// A finalize deferred into the next SpMV on the owning workspace's stream (one
+// at a time: the solver defers only a step's last finalize, which the SpMV
+// immediately follows).  Owned by the Workspace of one solve, so solves on
+// other workspaces or streams never see it.
+struct FinQueue {
+    FinArgs a{};
+    size_t lds = 0;
+    bool set = false;
+};
+
 struct Workspace {
     hipStream_t stream = nullptr;
+    FinQueue* defq = nullptr;  // the solve's deferred finalize (ws_create allocates it)
     int nblk = 0;        // partial-sum blocks for this n
     int stride = 0;      // >= ncv + 2
     double* part = nullptr;   // 2 regions of nblk * stride (region 2: chained steps)
@@ -205,16 +216,18 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
 // from_sums: the m sums are already in ws.sums (reduced across ranks).
 // m2 > 0 (kFinCgsChained): a second region of m2 partial slots at
 // ws.part + nblk * stride (the deferred DGKS sums of step j-1).
-// defer: do not launch it -- the next symmetric SpMV on ws.stream runs it in
-// its combine kernel's workgroup 0 (one launch fewer a step); any other
-// launcher of csr_spmv, and every stream sync of the engine, flushes it first.
+// defer: do not launch it -- it waits in ws.defq and the next SpMV handed that
+// queue runs it in a workgroup of its own launch (one launch fewer a step); an
+// SpMV that cannot carry it, the next finalize, and every stream sync of the
+// solve launch it first.
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate,
               bool from_sums = false, int m2 = 0, int rstart_prev = 0, bool defer = false);
 // (false, and the finalize stays deferred, when it needs more than max_lds bytes
 // of LDS or the H-column staging and allow_hs is false)
-bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds, size_t max_lds = (size_t)-1,
+bool take_deferred_finalize(FinQueue* q, FinArgs* a, size_t* lds, size_t max_lds = (size_t)-1,
                             bool allow_hs = true);
-void flush_deferred_finalize(hipStream_t s);
+// launch q's finalize (if any) on s
+void flush_deferred_finalize(FinQueue* q, hipStream_t s);
 // resid = 0 if st.zero
 template <class R>
 void zero_if(const Workspace& ws, int64_t n, R* r);
@@ -337,13 +350,19 @@ enum CsrKernel : int {
 // that the previous rank's transposed terms reach (its spill_out).
 int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int64_t spill_out,
                       void** owned);
-void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y);
+void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q = nullptr);
+// the same with the in-kernel chain-head combine forced on (where the operator
+// allows it, csr_spmv_sym_fusable) or off (test hook, whatever AHIP_SPMV_FUSE says)
+void csr_spmv_sym_as(hipStream_t s, const Csr& A, const double* x, double* y, bool fuse,
+                     FinQueue* q = nullptr);
+bool csr_spmv_sym_fusable(const Csr& A);
 // the two halves (the row-distributed SpMV exchanges the spills in between):
 // main kernel, then y(prefix rows) = lo + hi.  The outgoing spill is
 // ss_lo + ss_ncomb (ss_spill_out doubles); the incoming one lands in ss_lo[0, spill_in).
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y);
 // x_ext (a distributed block's extended x): the spill-free form when A.ss_lg
-void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext = nullptr);
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext = nullptr,
+                          FinQueue* q = nullptr);
 // Build the SELL-64 layout from a matrix with window tables; *owned receives the
 // single device allocation.  0 on success.
 int csr_build_sell(Csr& A, void** owned);
@@ -360,7 +379,7 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned);
 // matrix, like a sparse-library "analysis" step).  Returns 0, or -1 if a row
 // is longer than the tile (the matrix then keeps the vector kernel).
 int csr_analyse(Csr& A, int tile, int64_t** rblk_dev);
-void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y);
+void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q = nullptr);
 // algorithmic HBM bytes of one SpMV: 12*nnz + 8*(n+1) (int64 rowptr) + 8n (x) + 8n (y)
 double csr_bytes(const Csr& A);
 

@@ -37,11 +37,11 @@ static void exchange_general(const DistOp& D, hipStream_t s, bool p2p) {
     comm_ghosts(D.comm, D, s, p2p);
 }
 
-void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p) {
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p, dev::FinQueue* q) {
     if (x != D.x_mid()) dev::copy(s, D.nloc, x, D.x_mid());
     if (D.mode != DistOp::kHaloNeighbour) {
         exchange_general(D, s, p2p);
-        dev::csr_spmv(s, *D.A, D.x_ext, y);
+        dev::csr_spmv(s, *D.A, D.x_ext, y, q);
         return;
     }
     const dev::Csr& A = *D.A;
@@ -55,10 +55,10 @@ void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool 
         // those transposed terms (the spill) travel forward and are combined
         // into the receiver's leading rows (a reverse halo)
         if (!A.ss_lg) comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
-        dev::csr_spmv_sym_combine(s, A, y, D.x_ext);
+        dev::csr_spmv_sym_combine(s, A, y, D.x_ext, q);
         return;
     }
-    dev::csr_spmv(s, A, D.x_ext, y);
+    dev::csr_spmv(s, A, D.x_ext, y, q);
 }
 
 int dist_all_ok(const Comm* c, int ok_local) {

@@ -81,6 +81,8 @@ struct DistOp {
 // p2p: run the halo / spill exchanges on the communicator's separate
 // point-to-point communicator (the SpMV then may run on a stream of its own,
 // concurrently with the engine stream's allreduces)
-void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p = false);
+// q: the solve's deferred finalize (carried by the SpMV where it can be)
+void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p = false,
+               dev::FinQueue* q = nullptr);
 
 }  // namespace ahip

@@ -56,6 +56,7 @@ struct ArraysT {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     DevErr err;  // first failed HIP call of this solve (sticky)
+    dev::FinQueue* defq = nullptr;  // the solve's deferred finalize, launched by sync()
     void ck(hipError_t e) { err.ck(e); }
 
     // fails with a negative code if pointer kinds are mixed

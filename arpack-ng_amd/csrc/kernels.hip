@@ -520,6 +520,7 @@ static hipError_t ws_alloc(Workspace& ws, int64_t n, int ncv, hipStream_t s) {
     if (ncv > 64 &&  // per-thread output columns of the generic V*Q / gemm kernels
         (e = hipMalloc(&ws.scratch, sizeof(double) * (size_t)ws.nblk * kBlock * (ncv + 1))))
         return e;
+    ws.defq = new FinQueue;
     if ((e = hipMalloc(&ws.st, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.st_host, sizeof(LzState)))) return e;
     if ((e = hipHostMalloc(&ws.host_scratch, sizeof(double) * (4 * (size_t)ws.stride + 2 * (ncv + 1)))))
@@ -549,6 +550,7 @@ void ws_destroy(Workspace& ws) {
     if (ws.host_scratch) (void)hipHostFree(ws.host_scratch);
     if (ws.host_hcol) (void)hipHostFree(ws.host_hcol);
     if (ws.host_q) (void)hipHostFree(ws.host_q);
+    delete ws.defq;
     ws = Workspace{};
 }
 
@@ -660,16 +662,6 @@ void update(const Workspace& ws, int64_t n, int j, const R* V, int64_t ld, int w
 }
 
 namespace {
-// the finalize deferred into the next symmetric SpMV (one at a time: saitr
-// defers only the step's last finalize, which the SpMV immediately follows)
-struct Deferred {
-    hipStream_t s = nullptr;
-    FinArgs a{};
-    size_t lds = 0;
-    bool set = false;
-};
-Deferred g_deferred;
-
 void launch_fin(hipStream_t s, const FinArgs& a, size_t lds) {
     // ncv up to kMaxNcv: the state and records plus 8002 sums pass 64 KB
     static const bool attr = [] {
@@ -682,25 +674,25 @@ void launch_fin(hipStream_t s, const FinArgs& a, size_t lds) {
 }
 }  // namespace
 
-bool take_deferred_finalize(hipStream_t s, FinArgs* a, size_t* lds, size_t max_lds, bool allow_hs) {
-    if (!g_deferred.set || g_deferred.s != s) return false;
-    if (g_deferred.lds > max_lds || (g_deferred.a.hs && !allow_hs)) return false;
-    *a = g_deferred.a;
-    *lds = g_deferred.lds;
-    g_deferred.set = false;
+bool take_deferred_finalize(FinQueue* q, FinArgs* a, size_t* lds, size_t max_lds, bool allow_hs) {
+    if (!q || !q->set) return false;
+    if (q->lds > max_lds || (q->a.hs && !allow_hs)) return false;
+    *a = q->a;
+    *lds = q->lds;
+    q->set = false;
     return true;
 }
 
-void flush_deferred_finalize(hipStream_t s) {
-    if (!g_deferred.set || g_deferred.s != s) return;
-    g_deferred.set = false;
+void flush_deferred_finalize(FinQueue* q, hipStream_t s) {
+    if (!q || !q->set) return;
+    q->set = false;
     ProfScope ps(kProfFinalize, s, 0.0);
-    launch_fin(s, g_deferred.a, g_deferred.lds);
+    launch_fin(s, q->a, q->lds);
 }
 
 void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int gate, bool from_sums,
               int m2, int rstart_prev, bool defer) {
-    flush_deferred_finalize(ws.stream);  // (stream order: an earlier one runs first)
+    flush_deferred_finalize(ws.defq, ws.stream);  // (stream order: an earlier one runs first)
     // AHIP_FIN_DEFER=0: never deferred into the SpMV's combine
     static const bool defer_on = [] {
         const char* e = getenv("AHIP_FIN_DEFER");
@@ -720,8 +712,8 @@ void finalize(const Workspace& ws, int m, FinPhase ph, int j, int rstart, int ga
                        hs ? 1 : 0, 1};
     };
     // (from_sums: the distributed path's phase logic on allreduced sums)
-    if (defer && defer_on && (from_sums || fused)) {
-        g_deferred = Deferred{ws.stream, args(from_sums ? 1 : 0), lds, true};
+    if (defer && defer_on && (from_sums || fused) && ws.defq) {
+        *ws.defq = FinQueue{args(from_sums ? 1 : 0), lds, true};
         return;
     }
     ProfScope ps(kProfFinalize, ws.stream, from_sums ? 0.0 : 8.0 * ws.nblk * (m + m2));

@@ -1053,9 +1053,9 @@ static bool sell_fin() {
     return on;
 }
 
-void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
+void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q) {
     if (A.kernel == kCsrSymSell && A.ss_val) {  // (carries a deferred finalize itself)
-        csr_spmv_sym(s, A, x, y);
+        csr_spmv_sym(s, A, x, y, q);
         return;
     }
     // the full-storage SELL kernel's default form (NT loads, U = 4) and its
@@ -1066,9 +1066,9 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y) {
     size_t fin_lds = 0;
     // it must fit the window below the Arnoldi H staging (kFoldHMax^2 doubles)
     const bool carried =
-        sell_carry && take_deferred_finalize(s, &fa, &fin_lds,
+        sell_carry && take_deferred_finalize(q, &fa, &fin_lds,
                                              sizeof(double) * (kWinX - kFoldHMax * kFoldHMax));
-    if (!carried) flush_deferred_finalize(s);
+    if (!carried) flush_deferred_finalize(q, s);
     if (A.kernel == kCsrSell && A.s_val) {
         const size_t lds = sizeof(double) * kWinX;
         if (carried) {

@@ -264,6 +264,15 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
             flag[1] = ch + 1 < nch ? __hip_atomic_fetch_add(pair + ch + 1, 1, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT) : 0;
         }
+        // Ordering (MI355X_MICROARCH.md, the measured sc1 hand-off row for one
+        // workgroup per CU, this kernel's occupancy): every slot store above is
+        // an agent-scope (sc1) store drained by the vmcnt(0) wait before the
+        // barrier, ONE lane adds to the pair's unsharded counter, and the
+        // second arriver -- told by the value its add returned -- reads both
+        // slots with agent-scope (sc1) loads after the barrier below.  The
+        // barriers also keep the compiler from moving the slot accesses across
+        // the counter (they are workgroup fences); the word-by-word check under
+        // uneven load is tests/test_gpu_symspmv_handoff.py.
         __syncthreads();
         for (int side = 0; side < 2; ++side) {
             if (flag[side] != 1) continue;  // first of its pair: the partner combines
@@ -799,14 +808,14 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
     }
 }
 
-void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext) {
+void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* x_ext, FinQueue* q) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
     if (x_ext && A.ss_lg) {  // spill-free form: the head rows' lower ghost terms here
         FinArgs fa{};
         size_t lds = 0;
-        if (!take_deferred_finalize(s, &fa, &lds, 64 * 1024)) {
-            flush_deferred_finalize(s);
+        if (!take_deferred_finalize(q, &fa, &lds, 64 * 1024)) {
+            flush_deferred_finalize(q, s);
             fa = FinArgs{};
             lds = 0;
         }
@@ -818,13 +827,13 @@ void csr_spmv_sym_combine(hipStream_t s, const Csr& A, double* y, const double* 
         return;
     }
     if (A.ss_ncomb <= 0) {
-        flush_deferred_finalize(s);
+        flush_deferred_finalize(q, s);
         return;
     }
     FinArgs fa{};
     size_t lds = 0;
-    if (!take_deferred_finalize(s, &fa, &lds, 64 * 1024)) {
-        flush_deferred_finalize(s);  // (one too large for this launch's LDS)
+    if (!take_deferred_finalize(q, &fa, &lds, 64 * 1024)) {
+        flush_deferred_finalize(q, s);  // (one too large for this launch's LDS)
         AHIP_LAUNCH(k_ssell_combine, dim3((unsigned)nch), dim3(1024), 0, s, A.ss_sb_r0,
                     A.ss_sb_pre, A.ss_sb_off, A.ss_lo, A.ss_hi, y, chain);
         return;
@@ -844,21 +853,30 @@ static bool spmv_fuse() {
     return on;
 }
 
-void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y) {
+bool csr_spmv_sym_fusable(const Csr& A) {
     // one GPU (coff = spill = 0), the default kernel, counters allocated
-    const bool fuse = spmv_fuse() && A.ss_pair && A.ss_coff == 0 && A.ss_spill_out == 0 &&
-                      (A.ss_variant == 0 || A.ss_variant == 7) && !spmv_ynt();
+    return A.ss_pair && A.ss_coff == 0 && A.ss_spill_out == 0 &&
+           (A.ss_variant == 0 || A.ss_variant == 7) && !spmv_ynt();
+}
+
+void csr_spmv_sym(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q) {
+    csr_spmv_sym_as(s, A, x, y, spmv_fuse(), q);
+}
+
+void csr_spmv_sym_as(hipStream_t s, const Csr& A, const double* x, double* y, bool want_fuse,
+                     FinQueue* q) {
+    const bool fuse = want_fuse && csr_spmv_sym_fusable(A);
     if (!fuse) {
         csr_spmv_sym_main(s, A, x, y);
-        csr_spmv_sym_combine(s, A, y);
+        csr_spmv_sym_combine(s, A, y, nullptr, q);
         return;
     }
     // the step's deferred finalize rides along when it fits the spent x window
     // (without the H-column staging: k_finalize<false>'s form)
     FinArgs fa{};
     size_t lds = 0;
-    if (!take_deferred_finalize(s, &fa, &lds, sizeof(double) * kSymWin, false)) {
-        flush_deferred_finalize(s);
+    if (!take_deferred_finalize(q, &fa, &lds, sizeof(double) * kSymWin, false)) {
+        flush_deferred_finalize(q, s);
         fa = FinArgs{};
     }
     const int chain = sym_chain(A);

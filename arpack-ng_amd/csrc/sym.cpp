@@ -119,7 +119,7 @@ void ArraysT<R>::download_all() {
 
 template <class R>
 void ArraysT<R>::sync() {
-    dev::flush_deferred_finalize(stream);  // (none outlives a sync)
+    dev::flush_deferred_finalize(defq, stream);  // (none outlives a sync)
     ck(hipStreamSynchronize(stream));
 }
 
@@ -222,7 +222,7 @@ void SolverT<R>::fin(int m, dev::FinPhase ph, int j, int rstart, int gate, int m
 
 template <class R>
 void SolverT<R>::read_state() {
-    dev::flush_deferred_finalize(a.stream);
+    dev::flush_deferred_finalize(ws.defq, a.stream);
     a.ck(hipMemcpyAsync(ws.st_host, ws.st, sizeof(dev::LzState), hipMemcpyDeviceToHost, a.stream));
     a.sync();
 }
@@ -536,7 +536,7 @@ Task SolverT<R>::saitr(int k, int npk, int& iinfo) {
         // the new steps' T / H records travel with the state: one host sync
         // for both (the abort paths below loop back and fetch them again)
         double* rec_h = ws.host_scratch;
-        dev::flush_deferred_finalize(a.stream);
+        dev::flush_deferred_finalize(ws.defq, a.stream);
         a.ck(hipMemcpyAsync(rec_h, ws.rec, sizeof(double) * 2 * (k + npk), hipMemcpyDeviceToHost,
                             a.stream));
         if (arnoldi) {

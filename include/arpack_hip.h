@@ -550,6 +550,17 @@ void arpack_hip_fault_inject(long k);
  * Returns at once (0), without waiting for the kernel. */
 int arpack_hip_test_delayed_fill(double* dst, const double* src, double value, int64_t count,
                                  int delay_us);
+/* Test hook (the fused symmetric SpMV's cross-workgroup hand-off): y = A x on a
+ * CSR declared symmetric, with the in-kernel chain-head combine (fuse = 1, the
+ * one-GPU default) or the separate combine launch (fuse = 0), issued while a
+ * read / write stream over `load` (load_n doubles; may be NULL) runs on a
+ * second stream.  Writes the chain-head row ranges as (first row, count)
+ * pairs into heads (at most cap) and, when lo_out (host, n doubles) is given,
+ * the slot halves those rows read from the previous chain into lo_out at
+ * their rows.  Returns the number of ranges, or < 0. */
+int arpack_hip_test_symspmv_handoff(const arpack_hip_csr* A, const double* x, double* y, int fuse,
+                                    double* load, int64_t load_n, int64_t* heads, int64_t cap,
+                                    double* lo_out);
 /* Deterministic mode: every SpMV sum in a fixed order, so a solve is bitwise
  * reproducible run to run.  A later arpack_hip_csr_set_symmetric(A, 1) then
  * keeps the full-storage kernel (bitwise SciPy's csr_matvec) and returns 1,
