@@ -509,6 +509,21 @@ class SymRci:
         self.tol = tol.value
         return int(self.ido[0])
 
+    def aupd_gen(self, G: "DGen"):
+        """Whole loop on the GPU in a generalized mode (construct with bmat="G",
+        mode=G.mode): OP*x and B*x by the device operator pair G
+        (arpack_hip_dsaupd_gen)."""
+        tol = C.c_double(self.tol)
+        L = lib()
+        L.arpack_hip_dsaupd_gen.argtypes = L.arpack_hip_dsaupd_shift.argtypes
+        L.arpack_hip_dsaupd_gen(G.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                self.which.encode(), self.nev, C.byref(tol),
+                                _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
     def slice(self, k):
         """workd slice ipntr[k] (1-based offset) of length n: a numpy view in
         host mode, the device address (int) in device mode."""
@@ -759,6 +774,43 @@ class DShift:
         return dict(solves=a.value, iters=b.value, failures=c.value, max_relres=d.value,
                     ms=e.value, bytes_per_iter=f.value)
 
+
+
+class DGen:
+    """Device operator pair of dsaupd's generalized modes (bmat = 'G', modes
+    2-5; arpack_hip_dgen_create): mode 2 OP = inv[M] A; 3 OP = inv[A - sigma M]
+    M; 4 (buckling, A = K, B = KG) OP = inv[K - sigma KG] K; 5 (Cayley) OP =
+    inv[A - sigma M](A + sigma M).  The inverse is a device CG (method 0) or
+    MINRES (1) to relative residual rtol on C = A - sigma B."""
+
+    def __init__(self, A: CSR, B: CSR, mode: int, sigma: float = 0.0, rtol: float = 1e-12,
+                 maxit: int = 5000, method: int = 0):
+        L = lib()
+        L.arpack_hip_dgen_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_double, C.c_double, C.c_int, C.c_int]
+        L.arpack_hip_dgen_destroy.argtypes = [C.c_void_p]
+        h = C.c_void_p()
+        rc = L.arpack_hip_dgen_create(C.byref(h), A.h, B.h, int(mode), float(sigma), float(rtol),
+                                      int(maxit), int(method))
+        if rc != 0:
+            raise RuntimeError(f"arpack_hip_dgen_create failed ({rc})")
+        self.h, self.A, self.B, self.mode = h, A, B, int(mode)
+
+    def stats(self):
+        L = lib()
+        L.arpack_hip_dgen_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD]
+        v = [C.c_longlong() for _ in range(3)]
+        r = C.c_double()
+        L.arpack_hip_dgen_stats(self.h, *[C.byref(x) for x in v], C.byref(r))
+        return dict(solves=v[0].value, iters=v[1].value, fails=v[2].value, max_relres=r.value)
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_dgen_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
 
 class ZRci:
     """znaupd/zneupd state (SRC/znaupd.f, SRC/zneupd.f): complex128 arrays,

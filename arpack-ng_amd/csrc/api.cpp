@@ -135,10 +135,12 @@ template <class R>
 static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int nev, double* tol,
                      R* resid, int ncv, R* v, int ldv, int* iparam, int* ipntr, R* workd,
                      R* workl, int lworkl, int* info, const dev::Csr* csr, int max_cycles = -1,
-                     const DistOp* dist = nullptr, bool ns = false, dev::DShift* shift = nullptr) {
+                     const DistOp* dist = nullptr, bool ns = false, dev::DShift* shift = nullptr,
+                     dev::DGen* gen = nullptr) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
     if (dist) csr = dist->A;
     if (shift) csr = shift->A;  // mode 3 free run: OP = (A - sigma I)^{-1} on the device
+    if (gen) csr = gen->A;      // modes 2-5, bmat = 'G': OP and B on the device
     if (kShadow && csr) {  // the float family: reverse communication (no device-CSR OP)
         *info = -9999;
         *ido = 99;
@@ -161,10 +163,14 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         // a device OP serves mode 1 (OP = A), or mode 3 through the device solve
         // (symmetric only: CG); bmat = 'I'
         // (dnaupd: a nonsymmetric A needs the general solve, BiCGStab)
-        if (csr && ((shift ? mode != 3 || dist || (ns && shift->method != dev::kDShiftBicgstab)
-                           : mode != 1) ||
-                    bmat[0] != 'I' || csr->n != n))
+        if (gen) {  // the operator pair fixes the mode (bmat = 'G', dsaupd only)
+            if (ns || dist || bmat[0] != 'G' || mode != gen->mode || gen->n != n)
+                ierr = (ierr ? ierr : -11);
+        } else if (csr && ((shift ? mode != 3 || dist || (ns && shift->method != dev::kDShiftBicgstab)
+                                  : mode != 1) ||
+                           bmat[0] != 'I' || csr->n != n)) {
             ierr = (ierr ? ierr : -11);
+        }
         if (dist && dist->nloc != n) ierr = (ierr ? ierr : -1);
         if (ierr != 0) {
             *info = ierr;
@@ -232,6 +238,7 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             S->free_run = true;
             S->csr = csr;
             S->shift = shift;
+            S->gen = gen;
         }
         if (dist) {
             S->dist = dist;
@@ -307,6 +314,27 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         const RciReq r = S->ctx.req;
         // (the park below drains the stream first, then checks)
         if (r.ido != -1 && r.ido != 1 && r.ido != SolverT<R>::kPauseIdo && broken()) return;
+        if (S->gen && (r.ido == -1 || r.ido == 1 || r.ido == 2)) {
+            // generalized modes: OP*x (mode 2 also writes A x back over x) and
+            // B*x on the device; x, y are the request's device pointers, or its
+            // workd slices
+            if constexpr (!kShadow) {
+                double* W = S->a.d_workd;
+                const double* xp = S->op_x ? S->op_x : W + r.x;
+                double* yp = S->op_y ? S->op_y : W + r.y;
+                const double* bxp = (r.ido == 1 && r.bx >= 0) ? W + r.bx : nullptr;
+                dev::flush_deferred_finalize(S->ws.defq, S->a.stream);
+                const int rc = dev::dgen_apply(*S->gen, S->a.stream, r.ido, xp, yp, bxp, W + r.x);
+                if (rc < 0) {  // a solve missed its tolerance: OP is not what was asked
+                    S->a.sync();
+                    *info = -9999;
+                    *ido = 99;
+                    g_sym.erase(v);
+                    return;
+                }
+            }
+            continue;
+        }
         if (S->free_run && (r.ido == -1 || r.ido == 1)) {
             // kernel-mode timing (the SpMV kernels' own execution, as rocprofv3 reports
             // it); a row-distributed SpMV also holds its halo exchange: marker mode
@@ -495,6 +523,55 @@ void arpack_hip_dsaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* 
 struct arpack_hip_dshift {
     ahip::dev::DShift S;
 };
+
+struct arpack_hip_dgen {
+    ahip::dev::DGen G;
+};
+
+int arpack_hip_dgen_create(arpack_hip_dgen** out, const arpack_hip_csr* A, const arpack_hip_csr* B,
+                           int mode, double sigma, double rtol, int maxit, int method) {
+    if (!out || !(rtol > 0.0) || maxit < 1 || method < ahip::dev::kDShiftCg ||
+        method > ahip::dev::kDShiftMinres)
+        return -1;
+    auto* D = new arpack_hip_dgen;
+    const int rc = ahip::dev::dgen_create(D->G, A, B, mode, sigma, rtol, maxit, method);
+    if (rc != 0) {
+        delete D;
+        return rc;
+    }
+    *out = D;
+    return 0;
+}
+
+void arpack_hip_dgen_destroy(arpack_hip_dgen* D) {
+    if (!D) return;
+    ahip::dev::dgen_destroy(D->G);
+    delete D;
+}
+
+int arpack_hip_dgen_stats(const arpack_hip_dgen* D, long long* solves, long long* iters,
+                          long long* fails, double* max_relres) {
+    if (!D) return -1;
+    const ahip::dev::DShift& S = D->G.S;
+    *solves = S.n_solves;
+    *iters = S.n_iters;
+    *fails = S.n_fail;
+    *max_relres = S.max_relres;
+    return 0;
+}
+
+void arpack_hip_dsaupd_gen(arpack_hip_dgen* D, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, double* resid, int ncv, double* v, int ldv,
+                           int* iparam, int* ipntr, double* workd, double* workl, int lworkl,
+                           int* info) {
+    if (!D) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr, -1, nullptr, false, nullptr, &D->G);
+}
 
 int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, double sigma,
                              double rtol, int maxit) {

@@ -12,6 +12,7 @@
 #include "dense.hpp"
 #include "device.hpp"
 #include "dist.hpp"
+#include "dgen.hpp"
 #include "dshift.hpp"
 #include "rci.hpp"
 
@@ -131,6 +132,9 @@ public:
     // mode 3 free run (arpack_hip_dsaupd_shift): OP = (A - sigma I)^{-1} by the
     // device CG of dshift.hip on csr = shift->A
     dev::DShift* shift = nullptr;
+    // generalized modes free run (arpack_hip_dsaupd_gen): OP*x and B*x on the
+    // device (csr = gen->A)
+    dev::DGen* gen = nullptr;
 
     // nonsymmetric Arnoldi (dnaupd): full upper-Hessenberg H (ld ncv)
     bool arnoldi = false;

@@ -366,6 +366,30 @@ void arpack_hip_dnaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, i
                              double* v, int ldv, int* iparam, int* ipntr, double* workd,
                              double* workl, int lworkl, int* info);
 
+/* Generalized modes on the device (bmat = 'G', dsaupd modes 2-5; SRC/dsaupd.f:30-77):
+ * the caller's OP and B of the reverse-communication loop, served on the GPU so
+ * the solve runs without returning for every OP*x / B*x:
+ *   mode 2  OP = inv[M] A,  B = M (and x <- A x)     A = A, B = M
+ *   mode 3  OP = inv[A - sigma M] M,  B = M           A = A, B = M
+ *   mode 4  OP = inv[K - sigma KG] K, B = K           A = K, B = KG
+ *   mode 5  OP = inv[A - sigma M](A + sigma M), B = M
+ * The inverse is a device Krylov solve to relative residual rtol (method 0 CG:
+ * positive-definite C; 1 MINRES: indefinite) on C = A - sigma B formed once
+ * entry by entry over the union pattern (mode 2: on M).  Returns 0, -1 for bad
+ * arguments, -2 on a HIP failure.  arpack_hip_dsaupd_gen takes dsaupd_c's
+ * arguments (bmat 'G', iparam(7) = the operator pair's mode); a solve that
+ * misses rtol ends the run with info = -9999. */
+typedef struct arpack_hip_dgen arpack_hip_dgen;
+int arpack_hip_dgen_create(arpack_hip_dgen** G, const arpack_hip_csr* A, const arpack_hip_csr* B,
+                           int mode, double sigma, double rtol, int maxit, int method);
+void arpack_hip_dgen_destroy(arpack_hip_dgen* G);
+int arpack_hip_dgen_stats(const arpack_hip_dgen* G, long long* solves, long long* iters,
+                          long long* fails, double* max_relres);
+void arpack_hip_dsaupd_gen(arpack_hip_dgen* G, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, double* resid, int ncv, double* v, int ldv,
+                           int* iparam, int* ipntr, double* workd, double* workl, int lworkl,
+                           int* info);
+
 /* ---- multi-GPU (row-block sharding, PARPACK's decomposition) ----------------
  * Reference: ICB/parpack.h:17-33 (pdsaupd_c(MPI_Fint comm, ...), n = LOCAL
  * rows) and PARPACK/SRC/MPI/pdsaitr.f.  One process per GPU; the communicator
