@@ -380,6 +380,9 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned);
 // is longer than the tile (the matrix then keeps the vector kernel).
 int csr_analyse(Csr& A, int tile, int64_t** rblk_dev);
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q = nullptr);
+// the first superblock / chain lighter (its workgroup carries the deferred
+// finalize); false under AHIP_LIGHT_SB=0
+bool light_first_sb();
 // algorithmic HBM bytes of one SpMV: 12*nnz + 8*(n+1) (int64 rowptr) + 8n (x) + 8n (y)
 double csr_bytes(const Csr& A);
 

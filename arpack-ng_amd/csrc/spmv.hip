@@ -619,15 +619,39 @@ __global__ void k_row_span(int64_t n, const int64_t* __restrict__ rp, const int3
 // of ~10^6 rows (a 2-D stencil with m = 1000: 8,240 rows per 10,240-column
 // window) gives ~120 superblocks -- half the CUs idle.  Capped superblocks
 // stage more x (R + band per R rows) but fill the chip.
-int64_t sb_row_cap(int64_t n) {
+static int cu_count() {
     static const int ncu = [] {
         int v = 0;
         return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && v > 0
                    ? v
                    : 256;
     }();
+    return ncu;
+}
+
+int64_t sb_row_cap(int64_t n) {
+    const int ncu = cu_count();
     const int64_t cap = (n + 2 * (int64_t)ncu - 1) / (2 * (int64_t)ncu);
     return cap < 1024 ? 1024 : cap;
+}
+
+// Row caps of the superblocks when the cap binds: superblock 0 -- workgroup 0,
+// which carries the step's deferred finalize after its rows (k_csr_sell_fin)
+// -- gets half the cap, and the others share the remaining rows in the same
+// number of superblocks, so the finalize runs while the other workgroups
+// still stream instead of as a serial tail on an idle chip (one round of
+// workgroups: 2 a CU); cap0 / cap_rest.
+static void sb_row_caps(int64_t n, int64_t& cap0, int64_t& rest) {
+    const int64_t rcap = sb_row_cap(n);
+    const int64_t slots = 2 * (int64_t)cu_count();
+    if (!light_first_sb()) {  // AHIP_LIGHT_SB=0: every superblock at the cap
+        cap0 = rest = rcap;
+        return;
+    }
+    cap0 = rcap / 2 > 256 ? rcap / 2 : rcap;
+    rest = (n - cap0 + slots - 2) / (slots - 1);
+    if (rest < rcap) rest = rcap;  // small n: the 1,024-row floor (fewer superblocks than slots)
+    if (rest < cap0) rest = cap0;
 }
 
 // per row up to kMaxRanges column bands: sorted columns split where two
@@ -686,6 +710,16 @@ __global__ void k_colw_ranges(const int64_t* __restrict__ sb_tile0, const int64_
 }
 
 }  // namespace
+
+// AHIP_LIGHT_SB=0: no lighter first superblock (A/B of the finalize-carrying
+// workgroup's load; read once)
+bool light_first_sb() {
+    static const bool on = [] {
+        const char* e = getenv("AHIP_LIGHT_SB");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
     const int64_t n = A.n;
@@ -750,12 +784,14 @@ int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
         sb_tile0.push_back((int64_t)tiles.size() - 1);
     };
     int64_t sb_start = 0, tile_start = 0;
-    const int64_t rcap = sb_row_cap(n);
+    int64_t cap0 = 0, cap_rest = 0;
+    sb_row_caps(n, cap0, cap_rest);
     for (int64_t i = 0; i < n; ++i) {
         if (cnt[i] < 0 || rp[i + 1] - rp[i] > kWinTile) return -1;
         nxt = cur;
         for (int c = 0; c < cnt[i]; ++c)
             merge_into(nxt, Band{lo[(size_t)i * kMaxRanges + c], hi[(size_t)i * kMaxRanges + c]});
+        const int64_t rcap = sb_c0.empty() ? cap0 : cap_rest;
         if (!fits(nxt) || i - sb_start >= rcap) {
             if (i == sb_start) return -1;  // the row alone does not fit
             tiles.push_back(i);
@@ -835,7 +871,8 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
     std::vector<int32_t> sb_span;
     int64_t sb_start = 0, tile_start = 0;
     int64_t lo = INT64_MAX, hi = -1;
-    const int64_t rcap = sb_row_cap(n);
+    int64_t cap0 = 0, cap_rest = 0;
+    sb_row_caps(n, cap0, cap_rest);
     auto close_sb = [&](int64_t end_row) {
         if (lo > hi) { lo = 0; hi = 0; }
         sb_c0.push_back(lo);
@@ -852,6 +889,7 @@ int csr_analyse_window(Csr& A, int64_t ncols, void** owned) {
             nhi = std::max<int64_t>(hi, mx[i]);
             if (mx[i] - mn[i] + 1 > kWinX) return -1;
         }
+        const int64_t rcap = sb_c0.empty() ? cap0 : cap_rest;
         if (i > sb_start && ((nhi >= nlo && nhi - nlo + 1 > kWinX) || i - sb_start >= rcap)) {
             // close tile and superblock before row i
             tiles.push_back(i);

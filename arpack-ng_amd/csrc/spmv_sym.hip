@@ -562,10 +562,31 @@ int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& 
         for (int64_t b = 0; b <= k; ++b) r0s[b] = b * n / k;
         return plan_check(n, cmax, win, r0s, spans, pre, off, spill_in, spill_out);
     };
+    // k blocks with the first one lighter: workgroup 0 walks chain 0 and then
+    // runs the step's deferred finalize (k_csr_ssell FUSE), so chain 0 gets
+    // ~8% of one chain's rows fewer (~5 us at a 1.25e6-row share, ~3 us at
+    // n = 1e7; the finalize takes 3-6 us) and the finalize overlaps the other
+    // chains instead of trailing them.  Inside a chain the window shift needs
+    // span <= 2R, so the first superblock keeps at least the reach m.
+    auto light_first = [&](int64_t k) {
+        if (!light_first_sb() || kQuantum <= 0 || k % kQuantum != 0 || k < 2) return false;
+        const int64_t chain = k / kQuantum, R = n / k;
+        int64_t d = (R * 2) / (25 * chain);  // 8% of a chain
+        if (chain > 1 && R - d < m + 1) d = R - (m + 1);
+        if (d <= 0) return false;
+        r0s.resize(k + 1);
+        r0s[0] = 0;
+        r0s[1] = R - d;
+        for (int64_t b = 2; b <= k; ++b) r0s[b] = r0s[1] + (b - 1) * (n - r0s[1]) / (k - 1);
+        if (!plan_check(n, cmax, win, r0s, spans, pre, off, spill_in, spill_out)) return false;
+        for (int64_t b = 0; b < k; ++b)  // keep the chained window shift possible
+            if (chain > 1 && spans[b] > 2 * (r0s[b + 1] - r0s[b])) return false;
+        return true;
+    };
     const int64_t rmax = win - m;  // >= 1
     const int64_t k0 = (n + rmax - 1) / rmax;
     const int64_t kq = (k0 + kQuantum - 1) / kQuantum * kQuantum;
-    if (kq <= n && balanced(kq)) return 0;
+    if (kq <= n && (light_first(kq) || balanced(kq))) return 0;
     if (balanced(k0)) return 0;
     // greedy: extend each superblock while its window fits
     r0s.assign(1, 0);

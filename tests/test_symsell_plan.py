@@ -238,3 +238,24 @@ def test_symsell_plan_bench_sizes(pkg, P):
         assert rc == 0 and r0s[-1] == b - a
         assert len(spans) % 256 == 0
         assert pre[0] == sin and spans[-1] - (r0s[-1] - r0s[-2]) <= sout
+
+
+@pytest.mark.parametrize("n", [1_250_000, 10_000_000])
+def test_symsell_plan_light_first_superblock(pkg, n):
+    """Workgroup 0 walks chain 0 and then runs the step's deferred finalize, so
+    the plan gives chain 0's first superblock ~8% of a chain fewer rows (the
+    finalize overlaps the other chains); the superblock count stays a multiple
+    of the 256 CUs, the others stay balanced to one row, and inside chains
+    (n = 1e7: 7 a chain) every window still satisfies the in-LDS shift's
+    span <= 2R."""
+    cm = np.minimum(np.arange(n) + 4095, n - 1).astype(np.int64)
+    rc, r0s, spans, pre = _plan(pkg, cm, 10240)
+    assert rc == 0 and len(spans) % 256 == 0
+    R = np.diff(r0s)
+    chain = len(spans) // 256
+    assert R[1:].max() - R[1:].min() <= 1
+    light = R[1] - R[0]
+    assert 0 < light <= 0.09 * R[1] * chain + 1
+    assert abs(light - 0.08 * R[1] / chain) <= 0.01 * R[1] + 1
+    if chain > 1:
+        assert np.all(spans <= 2 * R)
