@@ -834,7 +834,10 @@ int arpack_hip_larnv_device(char prec, int* iseed, int64_t n, void* x) {
     dev::Workspace ws;
     hipStream_t st = nullptr;
     if (hipStreamCreate(&st) != hipSuccess) return -1;
-    if (dev::ws_create(ws, n, 2, st) != hipSuccess) return -1;
+    if (dev::ws_create(ws, n, 2, st) != hipSuccess) {
+        (void)hipStreamDestroy(st);
+        return -1;
+    }
     const uint64_t s0 = seed48_from_iseed(iseed);
     const uint64_t s1 = prec == 's' ? dev::larnv_uniform(ws, n, s0, (float*)x)
                                     : dev::larnv_uniform(ws, n, s0, (double*)x);
