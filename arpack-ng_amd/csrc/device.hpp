@@ -24,10 +24,12 @@ void fault_inject(long k);
 
 // Deterministic mode (arpack_hip_set_deterministic, ARPACK_HIP_DETERMINISTIC=1):
 // only SpMV forms whose every sum has a fixed order -- a symmetric declaration
-// keeps the full-storage SELL kernel (bitwise SciPy's csr_matvec) instead of the
-// upper-triangle kernel's LDS-atomic transposed terms, and the complex operator
-// takes the column-split kernel instead of the LDS-atomic row tiles.  The rest
-// of the engine (fixed-order partial sums) is deterministic in either mode.
+// takes the upper-triangle kernel's fixed-point form (k_csr_ssell_det: the
+// transposed terms as exact 64-bit integer sums, whose order cannot matter),
+// or, for an operator outside that form, keeps the full-storage SELL kernel
+// (bitwise SciPy's csr_matvec); the complex operator takes the column-split
+// kernel instead of the LDS-atomic row tiles.  The rest of the engine
+// (fixed-order partial sums) is deterministic in either mode.
 bool deterministic();
 void set_deterministic(bool on);
 
@@ -326,6 +328,15 @@ struct Csr {
     int64_t ss_pre0 = 0;                   // head rows of superblock 0 (the incoming spill's)
     int64_t ss_lg_rows = 0;                // 1 + last row with a column in the low halo
     int ss_lg = 0;                         // spill-free distributed form (k_ssell_combine_lg)
+    // deterministic mode's form (k_csr_ssell_det): the transposed terms summed
+    // as 64-bit fixed point scaled by ss_amax (largest |a_ij| off the diagonal
+    // of the upper triangle) times the window's largest |x|, ss_bits bits a
+    // term (headroom for the most transposed terms a row receives); usable when
+    // every window leaves one LDS word free (ss_det = 1)
+    double ss_amax = 0.0;
+    int ss_bits = 0;
+    int ss_det = 0;
+    int ss_detq = 0;  // most slices one wave walks in a superblock
 };
 enum CsrKernel : int {
     kCsrVector = 0,

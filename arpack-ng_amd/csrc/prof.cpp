@@ -12,29 +12,43 @@
 namespace ahip {
 
 namespace {
-// countdown of the fault-injection hook; AHIP_FAULT_AT=k arms it at load
-std::atomic<long> g_fault_at{[] {
-    const char* e = getenv("AHIP_FAULT_AT");
-    return e ? atol(e) : 0L;
-}()};
+// countdown of the fault-injection hook; AHIP_FAULT_AT=k arms it (read on the
+// first checked call, like ARPACK_HIP_DETERMINISTIC below)
+constexpr long kUnread = -1;
+std::atomic<long> g_fault_at{kUnread};
 }  // namespace
 
 hipError_t fault_filter(hipError_t e) {
-    if (g_fault_at.load(std::memory_order_relaxed) <= 0) return e;
+    long v = g_fault_at.load(std::memory_order_relaxed);
+    if (v == kUnread) {
+        const char* s = getenv("AHIP_FAULT_AT");
+        long unread = kUnread;
+        g_fault_at.compare_exchange_strong(unread, s && atol(s) > 0 ? atol(s) : 0L);
+        v = g_fault_at.load(std::memory_order_relaxed);
+    }
+    if (v <= 0) return e;
     return g_fault_at.fetch_sub(1) == 1 ? hipErrorInvalidValue : e;
 }
 
 void fault_inject(long k) { g_fault_at.store(k > 0 ? k : 0); }
 
 namespace {
-std::atomic<bool> g_det{[] {
-    const char* e = getenv("ARPACK_HIP_DETERMINISTIC");
-    return e && e[0] == '1';
-}()};
+// -1: not read yet -- ARPACK_HIP_DETERMINISTIC is read on first use (a value
+// computed in a static initializer read 0 in the built library)
+std::atomic<int> g_det{-1};
 }  // namespace
 
-bool deterministic() { return g_det.load(std::memory_order_relaxed); }
-void set_deterministic(bool on) { g_det.store(on); }
+bool deterministic() {
+    int v = g_det.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("ARPACK_HIP_DETERMINISTIC");
+        int unset = -1;
+        g_det.compare_exchange_strong(unset, e && e[0] == '1' ? 1 : 0);
+        v = g_det.load(std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+void set_deterministic(bool on) { g_det.store(on ? 1 : 0); }
 
 }  // namespace ahip
 

@@ -35,7 +35,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <climits>
+#include <cstring>
 #include <cstdint>
 #include <vector>
 
@@ -53,22 +55,41 @@ constexpr int kSymWin = 10240;  // doubles per LDS window (x and y: 2 x 80 KB = 
 // (at least the row itself, so every row's y slot is inside its window)
 // (columns relative to the diagonal's: j - coff, coff = halo_lo for a rank's
 // block of a row-distributed operator whose x is [halo_lo | local | halo_hi])
+// Also the deterministic form's scale inputs (k_csr_ssell_det): the largest
+// |a_ij| above the diagonal (as the bits of a non-negative double, which order
+// like the unsigned integers) and the most entries left of the diagonal in a
+// row (= the transposed terms that row receives).
 __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict__ rp,
-                              const int32_t* __restrict__ col, int32_t* __restrict__ cnt,
-                              int32_t* __restrict__ cmax) {
+                              const int32_t* __restrict__ col, const double* __restrict__ val,
+                              int32_t* __restrict__ cnt, int32_t* __restrict__ cmax,
+                              unsigned long long* __restrict__ amax, int* __restrict__ lmax) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    double am = 0.0;
+    int lm = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        int32_t c = 0, m = (int32_t)i, low = 0;
+        int32_t c = 0, m = (int32_t)i, low = 0, lower = 0;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
             const int32_t j = (int32_t)(col[k] - coff);
             if (j >= i) {
                 ++c;
                 m = max(m, j);
+                if (j > i) am = fmax(am, fabs(val[k]));
+            } else {
+                ++lower;
             }
             low |= j < 0;  // a column of the previous rank's block (halo_lo)
         }
         cnt[i] = c | (low << 30);
         cmax[i] = m;
+        lm = max(lm, lower);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        am = fmax(am, __shfl_xor(am, o, 64));
+        lm = max(lm, __shfl_xor(lm, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(amax, (unsigned long long)__double_as_longlong(am));
+        atomicMax(lmax, lm);
     }
 }
 
@@ -287,6 +308,232 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         }
         if (fa.active && blockIdx.x == 0) {
             __syncthreads();  // flag[] read by every wave before the window is reused
+            finalize_block<false>(fa, reinterpret_cast<FinLds*>(xw), nullptr);
+        }
+    }
+}
+
+// Deterministic mode's symmetric SpMV (arpack_hip_set_deterministic): the walk
+// of k_csr_ssell with every sum in an order no schedule can change.  The row
+// part stays one lane's sequential sum.  The transposed terms -- whose LDS
+// atomic adds meet in wave-schedule order -- become 64-bit FIXED-POINT
+// integers, and integer addition is exact, so their sum is the same in any
+// order:
+//   q = rint(a_ij x_i 2^(B-E))      (one fma onto 1.5 * 2^52: the low mantissa
+//                                    bits of the result are q, |q| < 2^B <= 2^51)
+//   y_j = (row sum) + (double)(sum of the q) * 2^(E-B)
+// with 2^E >= amax * (largest |x| the chain has staged so far): a running
+// maximum, so E only grows, and a partial sum carried into the next window is
+// rescaled by an arithmetic shift when it does; B = min(51, 62 - bits(L)) for
+// rows that receive at most L transposed terms, so no sum can overflow.  Each
+// term is rounded to 2^(E-B) -- at most 2^-51 of the window's largest product
+// (a double partial sum of such terms rounds each add to 2^-53 of its value).
+// The row sums wait in registers (at most MAXQ slices a wave) until the
+// window's x is spent, then meet the integer sums in the x window.  One LDS
+// word past every window (span <= kSymWin - 1) holds the running maximum.  The
+// chain-head combine, the slots and the deferred finalize are k_csr_ssell's.
+template <int U, bool NT, bool FUSE, int MAXQ>
+__global__ __launch_bounds__(kSymThreads) void k_csr_ssell_det(
+    const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
+    const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
+    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
+    const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
+    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
+    double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff, int chain,
+    int64_t nsb, double amax, int bits, int* __restrict__ pair, FinArgs fa) {
+    __shared__ double xw[kSymWin];
+    __shared__ unsigned long long tw[kSymWin];  // two's-complement fixed-point sums
+    constexpr int NW = kSymThreads / 64;
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+    const unsigned long long kMagicBits = (unsigned long long)__double_as_longlong(kMagic);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
+    unsigned long long* xmax = &tw[kSymWin - 1];  // bits of the running max |x|
+    int ea = 0;
+    (void)frexp(amax, &ea);  // amax < 2^ea
+    struct Chunk {
+        double v[U];
+        int c[U];
+    };
+    auto load = [&](Chunk& c, int64_t base, int w, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < w;
+            c.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
+            c.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
+        }
+    };
+    auto geom = [&](int64_t sl, int64_t& base, int& w) {
+        base = sptr[sl];
+        w = (int)((sptr[sl + 1] - base) >> 6);
+    };
+    Chunk cur, nxt;
+    int64_t cur_s = -1;
+    {
+        const int64_t s = sb_slice0[b0] + wave;
+        if (s < sb_slice0[b0 + 1]) {
+            int64_t base;
+            int w;
+            geom(s, base, w);
+            load(cur, base, w, 0);
+            cur_s = s;
+        }
+    }
+    if (t == 0) *xmax = 0ull;
+    __syncthreads();  // before any wave's first atomicMax (LDS holds the last launch's words)
+    int E = INT_MIN;
+    double inv = 0.0, sc = 0.0;
+    int R_prev = 0, span_prev = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+        const int64_t r0 = sb_r0[b];
+        const int R = (int)(sb_r0[b + 1] - r0);
+        const int span = sb_span[b];
+        const int64_t s1 = sb_slice0[b + 1];
+        int carry = 0;
+        if (b > b0) {
+            carry = span_prev - R_prev;
+            __syncthreads();
+            for (int i = t; i < carry; i += kSymThreads) {
+                xw[i] = xw[R_prev + i];
+                tw[i] = tw[R_prev + i];
+            }
+            __syncthreads();
+        }
+        // stage the new columns; the max over their |x| (as bit patterns, so a
+        // NaN wins and reaches every output of the chain) joins the running max
+        unsigned long long mb = 0;
+        for (int i = carry + t; i < span; i += kSymThreads) {
+            const double v = x[coff + r0 + i];
+            xw[i] = v;
+            tw[i] = 0;
+            mb = max(mb, (unsigned long long)__double_as_longlong(fabs(v)));
+        }
+        for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned long long)__shfl_xor(mb, o, 64));
+        if (lane == 0) atomicMax(xmax, mb);
+        __syncthreads();
+        {
+            const double X = __longlong_as_double((long long)*xmax);
+            int ex = 0;
+            (void)frexp(X, &ex);  // X < 2^ex
+            // (floor: 2^(B-E) <= 2^1000; with 2^-900 <= amax <= 2^900, the
+            // plan's condition, x_i 2^(B-E) then stays finite and every |q| < 2^B)
+            const int En = max(ea + ex, bits - 1000);
+            if (En > E) {  // uniform: X came from LDS after the barrier
+                if (carry > 0) {  // the carried sums were scaled by 2^(B-E): rescale
+                    const int d = min(En - E, 63);
+                    for (int i = t; i < carry; i += kSymThreads)
+                        tw[i] = (unsigned long long)((long long)tw[i] >> d);
+                    __syncthreads();
+                }
+                E = En;
+                inv = ldexp(1.0, bits - E);
+                sc = ldexp(1.0, E - bits);
+            }
+            if (!(X <= DBL_MAX)) sc = __longlong_as_double(0x7ff8000000000000ll);  // NaN / inf in x
+        }
+        double accq[MAXQ];
+        uint32_t rlq[(MAXQ + 1) / 2];  // window rows, two 16-bit halves (0xffff: padding lane)
+        int nq = 0;
+        for (int64_t s = sb_slice0[b] + wave; s < s1; s += NW, ++nq) {
+            int64_t base;
+            int w;
+            geom(s, base, w);
+            if (cur_s != s) load(cur, base, w, 0);
+            const int row = srow[s * 64 + lane];
+            const int rl = row >= 0 ? row - (int)r0 : 0;
+            const double xs = xw[rl] * inv;  // exact: a power-of-two scale
+            int64_t sn = s + NW;
+            if (sn >= s1) sn = b + 1 < b1 ? sb_slice0[b + 1] + wave : -1;
+            if (sn >= 0 && b + 1 < b1 && sn >= s1 && sn >= sb_slice0[b + 2]) sn = -1;
+            int64_t nbase = 0;
+            int nw = 0;
+            if (sn >= 0) geom(sn, nbase, nw);
+            double acc = 0.0;
+            int k = 0;
+            do {
+                if (k + U < w) load(nxt, base, w, k + U);
+                else if (sn >= 0) load(nxt, nbase, nw, 0);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = cur.c[u];
+                    if (c >= 0) {
+                        acc += cur.v[u] * xw[c];
+                        if (c != rl) {
+                            const double f = fma(cur.v[u], xs, kMagic);
+                            atomicAdd(&tw[c], (unsigned long long)__double_as_longlong(f) - kMagicBits);
+                        }
+                    }
+                }
+                cur = nxt;
+                k += U;
+            } while (k < w);
+            cur_s = sn;
+            const uint32_t h = row >= 0 ? (uint32_t)rl : 0xffffu;
+#pragma unroll
+            for (int u = 0; u < MAXQ; ++u)
+                if (u == nq) {
+                    accq[u] = acc;
+                    if (u & 1) rlq[u >> 1] = (rlq[u >> 1] & 0xffffu) | (h << 16);
+                    else rlq[u >> 1] = h;
+                }
+        }
+        __syncthreads();  // x of the window spent, every integer sum complete
+#pragma unroll
+        for (int u = 0; u < MAXQ; ++u) {
+            const uint32_t h = (u & 1) ? rlq[u >> 1] >> 16 : rlq[u >> 1] & 0xffffu;
+            if (u < nq && h != 0xffffu) xw[h] = accq[u];
+        }
+        __syncthreads();
+        const int head = b == b0 ? sb_pre[b] : 0;
+        const int64_t off = sb_off[b];
+        for (int i = t; i < R; i += kSymThreads) {
+            const double v = xw[i] + (double)(long long)tw[i] * sc;
+            if (i < head) {
+                if constexpr (FUSE) __hip_atomic_store(slot_hi + off + i, v, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                else slot_hi[off + i] = v;
+            } else {
+                y[r0 + i] = v;
+            }
+        }
+        if (b == b1 - 1) {
+            const int64_t offn = sb_off[b + 1];
+            for (int i = R + t; i < span; i += kSymThreads) {
+                const double v = (double)(long long)tw[i] * sc;
+                if constexpr (FUSE) __hip_atomic_store(slot_lo + offn + (i - R), v, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                else slot_lo[offn + (i - R)] = v;
+            }
+        }
+        R_prev = R;
+        span_prev = span;
+    }
+    if constexpr (FUSE) {  // k_csr_ssell's hand-off, verbatim in its ordering
+        const int64_t nch = gridDim.x;
+        int* flag = reinterpret_cast<int*>(xw);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            flag[0] = ch > 0 ? __hip_atomic_fetch_add(pair + ch, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) : 0;
+            flag[1] = ch + 1 < nch ? __hip_atomic_fetch_add(pair + ch + 1, 1, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT) : 0;
+        }
+        __syncthreads();
+        for (int side = 0; side < 2; ++side) {
+            if (flag[side] != 1) continue;
+            const int64_t c = ch + side;
+            const int64_t bh = c * chain;
+            const int pre = sb_pre[bh];
+            const int64_t off = sb_off[bh], rh = sb_r0[bh];
+            for (int i = t; i < pre; i += kSymThreads)
+                y[rh + i] = __hip_atomic_load(slot_lo + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                            __hip_atomic_load(slot_hi + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) pair[c] = 0;
+        }
+        if (fa.active && blockIdx.x == 0) {
+            __syncthreads();
             finalize_block<false>(fa, reinterpret_cast<FinLds*>(xw), nullptr);
         }
     }
@@ -615,21 +862,32 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     const int64_t n = A.n;
     if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
     int32_t *dcnt = nullptr, *dcm = nullptr;
+    unsigned long long* dst = nullptr;  // [0]: amax bits, [1]: lower-count max
     if (fault_filter(hipMalloc(&dcnt, sizeof(int32_t) * n)) != hipSuccess) return -2;
     if (fault_filter(hipMalloc(&dcm, sizeof(int32_t) * n)) != hipSuccess) {
         (void)hipFree(dcnt);
         return -2;
     }
+    if (fault_filter(hipMalloc(&dst, 2 * sizeof(unsigned long long))) != hipSuccess) {
+        (void)hipFree(dcnt);
+        (void)hipFree(dcm);
+        return -2;
+    }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
-                       dcnt, dcm);
+    bool got = fault_filter(hipMemset(dst, 0, 2 * sizeof(unsigned long long))) == hipSuccess;
+    if (got)
+        AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
+                    A.val, dcnt, dcm, dst, reinterpret_cast<int*>(dst + 1));
     std::vector<int32_t> cnt(n), cm(n);
-    const bool got =
-        fault_filter(hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
-        fault_filter(hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess;
+    unsigned long long hst[2] = {0, 0};
+    got = got &&
+          fault_filter(hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
+          fault_filter(hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
+          fault_filter(hipMemcpy(hst, dst, sizeof(hst), hipMemcpyDeviceToHost)) == hipSuccess;
     (void)hipFree(dcnt);
     (void)hipFree(dcm);
+    (void)hipFree(dst);
     if (!got) return -2;
     // rows with columns before the block (a distributed block's low halo): the
     // spill-free exchange computes their lower ghost terms locally
@@ -775,6 +1033,25 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     A.ss_lg_rows = lg_rows;
     A.ss_pre0 = pre[0];
     A.ss_lg = 0;  // (set by arpack_hip_csr_set_symmetric when every rank can)
+    // the fixed-point form (k_csr_ssell_det): a free LDS word past every
+    // window, >= 40 bits a term after the headroom for the most transposed
+    // terms a row receives (L < 2^hb), a finite scale
+    {
+        double amax;
+        std::memcpy(&amax, &hst[0], sizeof amax);
+        const int L = (int)(uint32_t)hst[1];
+        int hb = 0;
+        while (hb < 31 && (1ll << hb) <= (long long)L) ++hb;
+        int maxspan = 0;
+        for (int64_t b = 0; b < nsb; ++b) maxspan = std::max(maxspan, (int)spans[b]);
+        A.ss_amax = amax;
+        A.ss_bits = std::min(51, 62 - hb);
+        const bool scaled = amax == 0.0 || (amax >= 0x1p-900 && amax <= 0x1p900);  // (NaN: no)
+        A.ss_det = (maxspan <= kSymWin - 1 && A.ss_bits >= 40 && scaled) ? 1 : 0;
+        int64_t ms = 0;
+        for (int64_t b = 0; b < nsb; ++b) ms = std::max<int64_t>(ms, slice0[b + 1] - slice0[b]);
+        A.ss_detq = (int)((ms + NW - 1) / NW);
+    }
     *owned = d;
     return 0;
 }
@@ -790,7 +1067,27 @@ static bool spmv_ynt() {
     return on;
 }
 
+// deterministic mode takes the fixed-point form where the plan allows it
+static bool sym_det(const Csr& A) { return A.ss_det && deterministic(); }
+// MAXQ: slices a wave walks in one superblock -- at most 10 (rows <= span <=
+// kSymWin - 1); 6 (superblocks of <= 96 slices, the NS operator's 88) keeps
+// the kernel inside 128 VGPRs without spilling
+template <bool FUSE>
+static void launch_det(hipStream_t s, const Csr& A, const double* x, double* y, int* pair,
+                       const FinArgs& fa) {
+    const int chain = sym_chain(A);
+    const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+    auto* kern = A.ss_detq <= 6 ? &k_csr_ssell_det<8, true, FUSE, 6> : &k_csr_ssell_det<8, true, FUSE, 10>;
+    AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0, A.ss_sb_span, A.ss_sb_pre,
+                A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row, A.ss_colw, A.ss_val, x, y, A.ss_lo,
+                A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_amax, A.ss_bits, pair, fa);
+}
+
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) {
+    if (sym_det(A)) {
+        launch_det<false>(s, A, x, y, nullptr, FinArgs{});
+        return;
+    }
     auto go = [&](auto kern) {
         const int chain = sym_chain(A);
         const int64_t nch = (A.ss_nsb + chain - 1) / chain;
@@ -902,6 +1199,10 @@ void csr_spmv_sym_as(hipStream_t s, const Csr& A, const double* x, double* y, bo
     }
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
+    if (sym_det(A)) {
+        launch_det<true>(s, A, x, y, A.ss_pair, fa);
+        return;
+    }
     AHIP_LAUNCH((k_csr_ssell<8, true, false, true>), dim3((unsigned)nch), dim3(kSymThreads), 0, s,
                 A.ss_sb_r0, A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
                 A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_pair,

@@ -263,8 +263,8 @@ def main():
                     help="no per-kernel hipEvents in the timed region (overhead check)")
     ap.add_argument("--deterministic", action="store_true",
                     help="deterministic mode (arpack_hip_set_deterministic): only fixed-order "
-                         "SpMV forms, so --storage sym keeps the full-storage kernel and every "
-                         "solve is bitwise reproducible")
+                         "SpMV forms (--storage sym: the fixed-point symmetric kernel "
+                         "k_csr_ssell_det), so every solve is bitwise reproducible")
     args = ap.parse_args()
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
@@ -540,8 +540,9 @@ def main():
                    "which": "LA", "tol": "eps (a solve that converges inside the timed window is followed by a fresh one)",
                    "spmv_storage": "symmetric (upper triangle)" if storage == "sym" else "full CSR",
                    # sym: the transposed terms meet in LDS in wave order (Ritz values
-                   # reproducible to ~6e-15, not bitwise); full: fixed-order sums
-                   "bitwise_reproducible": storage == "full",
+                   # reproducible to ~6e-15, not bitwise); full, and sym in
+                   # deterministic mode (fixed-point transposed terms): fixed-order sums
+                   "bitwise_reproducible": storage == "full" or bool(args.deterministic),
                    "deterministic_mode": bool(args.deterministic),
                    "parallelism": "single GPU" if world == 1 else
                    f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
@@ -559,7 +560,9 @@ def main():
                                 "slices over LDS x/y windows, LDS atomic transposed terms, 16-bit "
                                 "window-relative cols; on one GPU the chain-head combine and the "
                                 "step's deferred finalize run inside it, else k_ssell_combine "
-                                "follows)") if storage == "sym"
+                                "follows)" + ("; deterministic mode: k_csr_ssell_det, the "
+                                              "transposed terms as 64-bit fixed-point LDS sums"
+                                              if args.deterministic else "")) if storage == "sym"
                                else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "
                                      "x windows, 16-bit window-relative cols, XCD-contiguous "
                                      "superblocks)"),

@@ -237,7 +237,12 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * kernel and returns nonzero (its own plan error, or -2 when only another
  * rank's plan failed); -3 if the distribution's communicator has been
  * destroyed.  In deterministic mode (arpack_hip_set_deterministic) on = 1
- * keeps the full-storage kernel and returns 1. */
+ * selects the fixed-point form of the same kernel (transposed terms summed as
+ * exact 64-bit integers: y bitwise reproducible) and returns 0, or, when the
+ * operator does not fit that form on every rank (no free LDS word past a
+ * window, rows receiving more than 2^22 transposed terms, or a largest
+ * off-diagonal magnitude outside [2^-900, 2^900]), keeps the full-storage
+ * kernel and returns 1. */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);

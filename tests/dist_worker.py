@@ -208,6 +208,32 @@ def lap3d(pkg, out, rank, world, m, cap):
     del D
 
 
+def det_spmv(pkg, out, rank, world):
+    """Deterministic mode's distributed symmetric SpMV repeated: the product of
+    the g4 operator's block, bitwise equal run to run, with products of another
+    scale in between (their LDS state must not leak into the next)."""
+    g = dict(np.load(os.path.join(GOLDEN, "g4_banded.npz"), allow_pickle=False))
+    spec = g["spec"]
+    n = int(spec[1])
+    r0, r1 = pkg.partition_rows(n, world, rank)
+    A = pkg.CSR.banded_sym(n, int(spec[2]), int(spec[3]), int(spec[4]), r0, r1)
+    D = pkg.DistOp(A, n, r0)
+    A.set_symmetric(True)
+    x = np.random.default_rng(3).standard_normal(n)[r0:r1].copy()
+    xd, xb = pkg.DeviceBuffer.from_numpy(x), pkg.DeviceBuffer.from_numpy(x * 1e12)
+    yd = pkg.DeviceBuffer(r1 - r0)
+    ys = []
+    for k in range(6):
+        if k % 2:
+            D.matvec_device(xb, yd)
+        D.matvec_device(xd, yd)
+        ys.append(yd.numpy().copy())
+    same = all(np.array_equal(y.view(np.int64), ys[0].view(np.int64)) for y in ys)
+    np.savez(os.path.join(out, "rank%d.npz" % rank), sym=np.array([int(A.symmetric)]),
+             same=np.array([same]), y=ys[0], det=np.array([pkg.lib().arpack_hip_deterministic()]))
+    del D
+
+
 def main():
     case, fixture, out = sys.argv[1], sys.argv[2], sys.argv[3]
     info0 = len(sys.argv) > 4 and sys.argv[4] == "info0"
@@ -220,8 +246,10 @@ def main():
     dist.init_process_group("gloo")
     pkg = load_pkg()
     pkg.comm_init_host(world, rank, device=0)
-    if case in ("spmv_chain", "sym_mixed", "lap3d", "general", "bad_layout"):
-        if case == "bad_layout":  # FIXTURE = col | rows
+    if case in ("spmv_chain", "sym_mixed", "lap3d", "general", "bad_layout", "det_spmv"):
+        if case == "det_spmv":
+            det_spmv(pkg, out, rank, world)
+        elif case == "bad_layout":  # FIXTURE = col | rows
             bad_layout(pkg, out, rank, world, fixture)
         elif case == "lap3d":  # FIXTURE = "m<m>_cap<cycles>"
             m, cap = (int(t[1:]) if t[0] == "m" else int(t[3:]) for t in fixture.split("_"))
@@ -269,7 +297,15 @@ def main():
             scale = M.to_scipy(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]],
                                np.abs(val[rp[r0]:rp[r1]]), n) @ np.abs(x)
             err = np.abs(yd.numpy() - Aloc @ x)
-            res["spmv_ok"] = np.array([bool(np.all(err <= 64 * np.finfo(float).eps * scale))])
+            tol = 64 * np.finfo(float).eps * scale
+            if os.environ.get("ARPACK_HIP_DETERMINISTIC") == "1" and A.symmetric:
+                # the fixed-point form's transposed terms (k_csr_ssell_det): each
+                # rounded to <= 2^-50 amax max|x|, at most L of them a row
+                rows = np.repeat(np.arange(n), np.diff(rp))
+                L = int(np.bincount(rows[col < rows], minlength=n).max())
+                amax = float(np.abs(val[col > rows]).max())
+                tol = tol + (L + 1) * 2.0 ** -50 * amax * np.abs(x).max()
+            res["spmv_ok"] = np.array([bool(np.all(err <= tol))])
         if fault and rank == 1:
             pkg.fault_inject(40)
         assert pkg.pdsaupd_cycles(s, D, -1) == 99

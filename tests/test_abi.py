@@ -65,6 +65,25 @@ def test_version_and_no_gpu_probe(pkg):
     assert pkg.device_count() >= 0
 
 
+def test_deterministic_env_read_at_load():
+    """ARPACK_HIP_DETERMINISTIC=1 turns deterministic mode on for a fresh
+    process (it was silently ignored before round 5: the library read it in a
+    static initializer that left 0); arpack_hip_set_deterministic overrides it."""
+    import subprocess
+    import sys
+    code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); a = L.arpack_hip_deterministic(); "
+            "L.arpack_hip_set_deterministic(0); print(a, L.arpack_hip_deterministic())")
+    lib = os.path.join(ROOT, "arpack-ng_amd", "libarpack_hip.so")
+    for val, want in (("1", "1 0"), ("0", "0 0"), (None, "0 0")):
+        env = {k: v for k, v in os.environ.items() if k != "ARPACK_HIP_DETERMINISTIC"}
+        if val is not None:
+            env["ARPACK_HIP_DETERMINISTIC"] = val
+        r = subprocess.run([sys.executable, "-c", code, lib], env=env, capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.split() == want.split(), (val, r.stdout)
+
+
 CPP_CALLER = r"""
 #include <complex>
 #include <vector>

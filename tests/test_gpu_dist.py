@@ -330,6 +330,31 @@ def test_symmetric_storage_many_ranks(tmp_path, golden, fixture, P, form):
     assert _resid(A, _z(ranks), d) <= 1e-8
 
 
+@pytest.mark.parametrize("form", sorted(SPILL_FORMS))
+def test_symmetric_storage_deterministic_ranks(tmp_path, golden, form):
+    """Deterministic mode on row blocks (ARPACK_HIP_DETERMINISTIC=1): every
+    rank keeps symmetric storage in its fixed-point form (k_csr_ssell_det; the
+    spill or the spill-free head rows are fixed-order sums), the solve gives
+    the reference's cycles and values, and two runs agree bit for bit --
+    values and every rank's Ritz-vector rows."""
+    g = golden("g4_banded")
+    env = dict(SPILL_FORMS[form], ARPACK_HIP_DETERMINISTIC="1")
+    runs = []
+    for k in range(2):
+        (tmp_path / ("r%d" % k)).mkdir()
+        runs.append(_run(tmp_path / ("r%d" % k), "sym_csr_s", "g4_banded", 2, extra_env=env))
+    for ranks in runs:
+        for r in ranks:
+            assert bool(r["spmv_ok"][0])
+            assert int(r["sym"][0]) == 1
+            assert bool(r["spill"][0]) == (form == "spill")
+            assert int(r["info"][0]) == 0
+            assert int(r["iparam"][2]) == int(g["iparam"][2])
+    np.testing.assert_allclose(np.sort(runs[0][0]["d"]), np.sort(g["d"]), rtol=1e-10)
+    np.testing.assert_array_equal(runs[0][0]["d"], runs[1][0]["d"])
+    np.testing.assert_array_equal(_z(runs[0]), _z(runs[1]))
+
+
 @pytest.mark.parametrize("kind,rc", [("col", -1), ("rows", -3)])
 def test_dist_create_rejects_bad_layout(tmp_path, kind, rc):
     """a column outside [0, n_global) or non-contiguous row blocks

@@ -38,15 +38,21 @@ def reference(tmp_path_factory):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("storage", ["full", "sym"])
+@pytest.mark.parametrize("storage", ["full", "sym", "sym_det"])
 def test_north_star_full_size(pkg, reference, storage):
+    """sym_det: deterministic mode's fixed-point symmetric SpMV (k_csr_ssell_det)."""
     ref = reference
     assert int(ref["info"]) == 0 and int(ref["nconv"]) == NEV
     A = pkg.CSR.banded_sym(N)
-    if storage == "sym":
-        A.set_symmetric(True)
-    s = pkg.SymRci(N, NEV, NCV, "LA", TOL, mxiter=300, v0=dlarnv_fast(N), device=True)
-    s.aupd_csr(A)
+    pkg.set_deterministic(storage == "sym_det")
+    try:
+        if storage != "full":
+            A.set_symmetric(True)
+            assert A.symmetric
+        s = pkg.SymRci(N, NEV, NCV, "LA", TOL, mxiter=300, v0=dlarnv_fast(N), device=True)
+        s.aupd_csr(A)
+    finally:
+        pkg.set_deterministic(False)
     assert int(s.info[0]) == 0 and int(s.iparam[4]) == NEV
     assert int(s.iparam[2]) == int(ref["iparam"][2])
     assert int(s.iparam[8]) == int(ref["nopx"])
