@@ -78,6 +78,14 @@ struct ZCsr {
     int64_t t_nrb = 0;
     uint32_t* t_idx = nullptr;
     double* t_val = nullptr;
+    // deterministic mode's tile form (k_ztile_det: the row sums as 64-bit
+    // fixed-point integers): per-(slice, row block) largest |re|, |im| of the
+    // entries (s_n x t_nrb), 256 block maxima of the bits of |x| of the
+    // product in flight, B bits a term; t_det = 1 when the operator fits
+    double* t_amax = nullptr;
+    unsigned long long* t_xmax = nullptr;
+    int t_bits = 0;
+    int t_det = 0;
 };
 // Build the XCD column split of A when it pays (n >= 2^18: x larger than one
 // XCD's L2; >= 32 entries a row: the partials' 256 B a row stay small against

@@ -15,9 +15,12 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cfloat>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "zcommon.hpp"
 #include "zengine.hpp"
@@ -170,6 +173,134 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int3
     for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
 }
 
+constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid = k_ztile_det's block size
+
+// Deterministic mode's tile product (arpack_hip_set_deterministic): k_ztile
+// with the row sums as 64-bit FIXED-POINT integers (the scheme of
+// spmv_sym.hip's k_csr_ssell_det): every product's real and imaginary part
+// (|.| <= 2 amax max|x| < 2^E, amax of this row block and slice, max|x| over
+// x by k_zabsmax just before) becomes q = rint(p 2^(B-E)) -- one fma onto
+// 1.5 * 2^52 -- and the LDS sums are exact integer adds, the same in any
+// wave order; y_s = (double)(sum q) 2^(E-B).  B = min(51, 62 - bits(L)) for at
+// most L entries a row in a slice.  The slice partials are summed in
+// zc::slice_sum's fixed order as before.
+template <int S>
+__global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const int32_t* __restrict__ srp,
+                                                   const int64_t* __restrict__ base,
+                                                   const uint32_t* __restrict__ idx,
+                                                   const double2* __restrict__ val,
+                                                   const double2* __restrict__ x,
+                                                   double2* __restrict__ yp, const int* __restrict__ gate,
+                                                   const double* __restrict__ amax,
+                                                   const unsigned long long* __restrict__ xmax, int bits,
+                                                   int64_t nrb) {
+    if (gate && *gate) return;
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+    const unsigned long long kMagicBits = (unsigned long long)__double_as_longlong(kMagic);
+    __shared__ unsigned long long ylds[2 * kTileRows];
+    __shared__ unsigned long long wmax[4];
+    const int s = (int)(blockIdx.x % S);
+    const int64_t rb = blockIdx.x / S;
+    const int64_t r0 = rb * kTileRows;
+    const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
+    for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0ull;
+    {  // max|x| from k_zabsmax's kZMaxBlocks block maxima (one a thread)
+        unsigned long long m = xmax[threadIdx.x];
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    }
+    __syncthreads();
+    const double X = __longlong_as_double((long long)max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+    int ea = 0, ex = 0;
+    (void)frexp(amax[s * nrb + rb], &ea);
+    (void)frexp(X, &ex);
+    const int E = max(ea + ex + 1, bits - 1000);
+    const double inv = ldexp(1.0, bits - E);
+    const double sc = X <= DBL_MAX ? ldexp(1.0, E - bits) : __longlong_as_double(0x7ff8000000000000ll);
+    __syncthreads();
+    const int32_t* rp = srp + (int64_t)s * (n + 1);
+    const int64_t e0 = base[s] + rp[r0], e1 = base[s] + rp[r0 + rows];
+    const double2* xs = x + (int64_t)s * sw;
+    auto add = [&](int r, double p, int part) {
+        const double f = fma(p, inv, kMagic);
+        atomicAdd(&ylds[2 * r + part], (unsigned long long)__double_as_longlong(f) - kMagicBits);
+    };
+    int64_t e = e0 + threadIdx.x;
+    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
+        uint32_t id[kTileU];
+        dv2 v[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) {
+            id[u] = __builtin_nontemporal_load(&idx[e + u * 256]);
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+        }
+        double2 xv[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) xv[u] = xs[id[u] & 0xfffffu];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) {
+            const int r = (int)(id[u] >> 20);
+            add(r, v[u].x * xv[u].x - v[u].y * xv[u].y, 0);
+            add(r, v[u].x * xv[u].y + v[u].y * xv[u].x, 1);
+        }
+    }
+    for (; e < e1; e += 256) {
+        const uint32_t id = idx[e];
+        const dv2 v = reinterpret_cast<const dv2*>(val)[e];
+        const double2 xv = xs[id & 0xfffffu];
+        const int r = (int)(id >> 20);
+        add(r, v.x * xv.x - v.y * xv.y, 0);
+        add(r, v.x * xv.y + v.y * xv.x, 1);
+    }
+    __syncthreads();
+    double2* y = yp + (int64_t)s * n + r0;
+    for (int i = threadIdx.x; i < rows; i += 256)
+        y[i] = make_double2((double)(long long)ylds[2 * i] * sc, (double)(long long)ylds[2 * i + 1] * sc);
+}
+
+// bits of max(|re x_i|, |im x_i|) over x (non-negative doubles order as their
+// bit patterns, so a NaN wins): one maximum per block into xmax[block], which
+// k_ztile_det's blocks reduce themselves (no atomics: 4,096 arrivals on one
+// word cost 49 us, MI355X_MICROARCH.md "fanin")
+__global__ __launch_bounds__(256) void k_zabsmax(int64_t n2, const double* __restrict__ x,
+                                                 unsigned long long* __restrict__ xmax,
+                                                 const int* __restrict__ gate) {
+    if (gate && *gate) return;
+    __shared__ unsigned long long w[4];
+    unsigned long long m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256)
+        m = max(m, (unsigned long long)__double_as_longlong(fabs(x[i])));
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) xmax[blockIdx.x] = max(max(w[0], w[1]), max(w[2], w[3]));
+}
+
+// per (slice, row block) segment q: the largest |re|, |im| of its entries;
+// *lmax: the most entries a row has in one slice
+__global__ void k_ztile_amax(const int64_t* __restrict__ seg, const double* __restrict__ tval,
+                             double* __restrict__ amax) {
+    const int64_t q = blockIdx.x;
+    double m = 0.0;
+    for (int64_t k = 2 * seg[q] + threadIdx.x; k < 2 * seg[q + 1]; k += blockDim.x) m = fmax(m, fabs(tval[k]));
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    __shared__ double w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) amax[q] = fmax(fmax(w[0], w[1]), fmax(w[2], w[3]));
+}
+__global__ void k_zslice_lmax(int64_t n, int ns, const int32_t* __restrict__ srp, int* __restrict__ lmax) {
+    int m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        for (int s = 0; s < ns; ++s) {
+            const int32_t* rp = srp + (int64_t)s * (n + 1);
+            m = max(m, rp[r + 1] - rp[r]);
+        }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(lmax, m);
+}
+
 // sort keys (slice column), the row of every entry, and the segment bounds of
 // the (slice, row block) segments in the slice-major entry order
 template <class CT>
@@ -223,8 +354,13 @@ inline int grid1(int64_t n) {
 void zcsr_free_split(ZCsr& A) {
     if (A.t_idx) (void)hipFree(A.t_idx);
     if (A.t_val) (void)hipFree(A.t_val);
+    if (A.t_amax) (void)hipFree(A.t_amax);
+    if (A.t_xmax) (void)hipFree(A.t_xmax);
     A.t_idx = nullptr;
     A.t_val = nullptr;
+    A.t_amax = nullptr;
+    A.t_xmax = nullptr;
+    A.t_det = 0;
     A.tile = false;
     if (A.s_rp) (void)hipFree(A.s_rp);
     if (A.s_base) (void)hipFree(A.s_base);
@@ -287,20 +423,49 @@ static int ztile_build(ZCsr& A) {
             hipLaunchKernelGGL(k_ztile_gather, dim3(grid1(nnz)), dim3(256), 0, nullptr, nnz, perm2, key2, erow,
                                (const double2*)A.s_val, A.t_idx, (double2*)A.t_val);
             if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+            // the deterministic form's scale inputs (optional: without them
+            // deterministic mode keeps the CSR split)
+            int* dl = nullptr;
+            if (rc == 0 && hipMalloc(&A.t_amax, sizeof(double) * (size_t)nseg) == hipSuccess &&
+                hipMalloc(&A.t_xmax, sizeof(unsigned long long) * kZMaxBlocks) == hipSuccess &&
+                hipMalloc(&dl, sizeof(int)) == hipSuccess && hipMemset(dl, 0, sizeof(int)) == hipSuccess) {
+                hipLaunchKernelGGL(k_ztile_amax, dim3((unsigned)nseg), dim3(256), 0, nullptr, seg, A.t_val, A.t_amax);
+                hipLaunchKernelGGL(k_zslice_lmax, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_n, A.s_rp, dl);
+                std::vector<double> am((size_t)nseg);
+                int L = 0;
+                if (hipMemcpy(am.data(), A.t_amax, sizeof(double) * (size_t)nseg, hipMemcpyDeviceToHost) ==
+                        hipSuccess &&
+                    hipMemcpy(&L, dl, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) {
+                    int hb = 0;
+                    while (hb < 31 && (1ll << hb) <= (long long)L) ++hb;
+                    bool scaled = true;
+                    for (double a : am) scaled = scaled && (a == 0.0 || (a >= 0x1p-900 && a <= 0x1p900));
+                    A.t_bits = std::min(51, 62 - hb);
+                    A.t_det = scaled && A.t_bits >= 40 ? 1 : 0;
+                }
+            }
+            if (dl) (void)hipFree(dl);
         }
     }
     cleanup();
     if (rc != 0) {
         if (A.t_idx) (void)hipFree(A.t_idx);
         if (A.t_val) (void)hipFree(A.t_val);
+        if (A.t_amax) (void)hipFree(A.t_amax);
+        if (A.t_xmax) (void)hipFree(A.t_xmax);
         A.t_idx = nullptr;
         A.t_val = nullptr;
+        A.t_amax = nullptr;
+        A.t_xmax = nullptr;
+        A.t_det = 0;
         return rc;
     }
-    (void)hipFree(A.s_col);  // the tiles replace the slice CSR's columns and values
-    (void)hipFree(A.s_val);
-    A.s_col = nullptr;
-    A.s_val = nullptr;
+    if (A.t_det) {  // the tiles replace the slice CSR's columns and values
+        (void)hipFree(A.s_col);
+        (void)hipFree(A.s_val);
+        A.s_col = nullptr;
+        A.s_val = nullptr;
+    }  // (else the CSR split stays: deterministic mode's fixed-order form of this operator)
     A.t_nrb = nrb;
     A.tile = true;
     return 0;
@@ -387,6 +552,14 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
     if (A.tile && !deterministic()) {  // (LDS-atomic row sums: not bitwise run to run)
         hipLaunchKernelGGL(k_ztile<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
                            A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
+        return;
+    }
+    if (A.tile && A.t_det) {  // deterministic: the fixed-point tile form (else the CSR split, kept)
+        hipLaunchKernelGGL(k_zabsmax, dim3(kZMaxBlocks), dim3(256), 0, s, 2 * A.n,
+                           reinterpret_cast<const double*>(x2), A.t_xmax, gate);
+        hipLaunchKernelGGL(k_ztile_det<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w,
+                           A.s_rp, A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate, A.t_amax,
+                           A.t_xmax, A.t_bits, A.t_nrb);
         return;
     }
     const int g = 1024;  // 128 workgroups a slice at S = 8 (tools/zspmv_split.hip)

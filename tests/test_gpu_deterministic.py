@@ -183,3 +183,34 @@ def test_complex_operator_bitwise_repeatable(pkg, det):
         runs.append((int(s.iparam[2]), np.array(s.ritz)))
     assert runs[0][0] == runs[1][0]
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
+def test_complex_tiles_fixed_point_bitwise(pkg, det):
+    """Config 5's operator family at a size that takes the XCD split with
+    column-sorted tiles (n >= 2^18, >= 32 entries a row): deterministic mode
+    runs the tiles' fixed-point form (k_ztile_det: row sums as exact 64-bit
+    integers) -- bitwise equal products with products of another scale in
+    between, within 64 eps (|A||x|) + (L + 1) 2^-49 amax max|x| of SciPy's per
+    component -- and the default mode's LDS-atomic tiles agree to rounding."""
+    import scipy.sparse as sp
+    n = 300_000
+    Z = pkg.ZCSR.random(n, 40, 7, 40.0)
+    rp, col, val = Z.download()
+    S = sp.csr_matrix((val, col, rp), shape=(n, n))
+    rng = np.random.default_rng(4)
+    x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)) * 10.0 ** rng.uniform(-6, 0, n)
+    y0 = Z.matvec(x)
+    for k in range(4):
+        Z.matvec(x * 1e9 if k % 2 else x[::-1].copy())
+        np.testing.assert_array_equal(Z.matvec(x).view(np.int64), y0.view(np.int64))
+    amax = max(np.abs(val.real).max(), np.abs(val.imag).max())
+    L = int(np.diff(rp).max())
+    xm = max(np.abs(x.real).max(), np.abs(x.imag).max())
+    ref = S @ x
+    bound = 64 * np.finfo(float).eps * (abs(S) @ np.abs(x)) + (L + 1) * 2.0 ** -49 * amax * xm
+    assert np.all(np.abs(y0.real - ref.real) <= bound)
+    assert np.all(np.abs(y0.imag - ref.imag) <= bound)
+    pkg.set_deterministic(False)
+    y1 = Z.matvec(x)
+    pkg.set_deterministic(True)
+    assert np.all(np.abs(y1 - y0) <= 2 * bound)
