@@ -174,6 +174,7 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int3
 }
 
 constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid = k_ztile_det's block size
+static_assert(kZMaxBlocks == 256, "k_ztile_det reduces one block maximum a thread");
 
 // Deterministic mode's tile product (arpack_hip_set_deterministic): k_ztile
 // with the row sums as 64-bit FIXED-POINT integers (the scheme of

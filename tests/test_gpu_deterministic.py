@@ -118,6 +118,31 @@ def test_fixed_point_spmv_bitwise_under_uneven_load(pkg, det, fuse):
             np.testing.assert_array_equal(y.view(np.int64), y0.view(np.int64))
 
 
+def test_fixed_point_spmv_wide_superblocks(pkg, det):
+    """A narrow band (16) gives superblocks of ~7,800 rows (123 slices: more
+    than 6 a wave, the kernel's 10-slice instance): bitwise repeatable and
+    within the bound, both with and without the fused combine."""
+    import scipy.sparse as sp
+    n = 2_000_000
+    A = pkg.CSR.banded_sym(n, 11, 16, 6)
+    rp, col, val = A.download()
+    A.set_symmetric(True)
+    assert A.last_rc == 0 and A.symmetric
+    S = sp.csr_matrix((val, col, rp), shape=(n, n))
+    x = np.random.default_rng(2).standard_normal(n)
+    bound = _bound(S, x)
+    xd, yd = pkg.DeviceBuffer.from_numpy(x), pkg.DeviceBuffer(n)
+    heads = np.zeros(2 * 4096, np.int64)
+    f = _hook(pkg)
+    ys = []
+    for fuse in (0, 1, 0, 1):
+        assert f(A.h, xd.ptr, yd.ptr, fuse, None, 0, heads.ctypes.data, 4096, None) > 0
+        ys.append(yd.numpy().copy())
+    assert np.all(np.abs(ys[0] - S @ x) <= bound)
+    for y in ys[1:]:
+        np.testing.assert_array_equal(y.view(np.int64), ys[0].view(np.int64))
+
+
 def test_fixed_point_spmv_propagates_nan(pkg, det):
     """A NaN in x reaches y: every row SciPy's product makes NaN is NaN here
     too (the scale of a window holding a NaN is NaN)."""
