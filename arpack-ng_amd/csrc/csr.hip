@@ -391,24 +391,21 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     if (!A->symsell)
         rc = ahip::dev::csr_build_symsell(A->A, A->ncols, A->sym_coff, A->sym_spill_in,
                                           A->sym_spill_out, &A->symsell);
-    if (ahip::deterministic()) {
-        // the fixed-point form (k_csr_ssell_det) where every rank's plan allows
-        // it; otherwise the fixed-order full-storage SpMV stays (reported as kept)
-        const bool det = rc == 0 && A->A.ss_det;
-        if (c && !ahip::dist_all_ok(c, det)) {
-            csr_full_storage(A);
-            return rc == -2 ? -2 : 1;
-        }
-        if (!det) {
-            csr_full_storage(A);
-            return rc == -2 ? -2 : 1;
-        }
-    }
     if (c && !ahip::dist_all_ok(c, rc == 0)) {
         csr_full_storage(A);
         return rc != 0 ? rc : -2;
     }
     if (rc != 0) return rc;
+    if (ahip::deterministic()) {
+        // the fixed-point form (k_csr_ssell_det) where every rank's plan allows
+        // it (a second agreement); otherwise the fixed-order full-storage SpMV
+        // stays, reported as kept (1) on every rank
+        const bool det = A->A.ss_det != 0;
+        if (c ? !ahip::dist_all_ok(c, det) : !det) {
+            csr_full_storage(A);
+            return 1;
+        }
+    }
     A->A.kernel = ahip::dev::kCsrSymSell;
     // a distributed block: the spill-free exchange when every rank's lower ghost
     // rows lie inside its incoming spill's rows (structurally symmetric

@@ -174,16 +174,20 @@ def test_sym_rci_user_op_ranks(tmp_path, golden):
         np.testing.assert_allclose(np.sort(r["d"]), np.sort(g["d"]), rtol=1e-10)
 
 
-def test_symmetric_storage_mode_agreed(tmp_path):
+@pytest.mark.parametrize("det", ["0", "1"])
+def test_symmetric_storage_mode_agreed(tmp_path, det):
     """arpack_hip_csr_set_symmetric on a distributed block is collective: rank 0's
     symmetric plan fails (one upper entry past the LDS window), rank 1's would
     succeed, and both ranks end in full storage -- rank 0 reports its plan error,
     rank 1 reports -2 -- so their halo/spill exchanges match and the solve runs
     to the same values as one rank (whose single block may or may not fit the
-    symmetric plan: either storage gives the same values to rounding)."""
+    symmetric plan: either storage gives the same values to rounding).  The same
+    in deterministic mode (det = 1), whose fixed-point form is agreed after
+    the plans."""
     import scipy.sparse as sp
-    r2 = _run(tmp_path, "sym_mixed", "-", 2)
-    r1 = _run(tmp_path, "sym_mixed", "-", 1)
+    env = {"ARPACK_HIP_DETERMINISTIC": det}
+    r2 = _run(tmp_path, "sym_mixed", "-", 2, extra_env=env)
+    r1 = _run(tmp_path, "sym_mixed", "-", 1, extra_env=env)
     assert int(r2[0]["sym_rc"][0]) not in (0, -2)
     assert int(r2[1]["sym_rc"][0]) == -2
     for r in r2 + r1:
