@@ -248,7 +248,7 @@ def main():
     ap.add_argument("--steady-cycles", type=int, default=3,
                     help="restart cycles 1..k of one solve timed on GPU and CPU alike")
     ap.add_argument("--no-full-storage", action="store_true",
-                    help="skip the secondary full-storage measurement of --storage sym")
+                    help="skip the secondary full-storage and deterministic-mode measurements of --storage sym")
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: engine collectives over gloo instead of RCCL, so N ranks "
                          "can share one GPU (every rank uses device 0)")
@@ -413,6 +413,17 @@ def main():
                             lanczos_steps_per_s=nopx_f / el_f)
         del s_f
         A.set_symmetric(True)
+    det_mode = None
+    if storage == "sym" and world == 1 and not args.no_full_storage and not args.deterministic:
+        # the same K cycles in deterministic mode (the fixed-point symmetric
+        # kernel k_csr_ssell_det: bitwise reproducible solves), reported beside
+        pkg.set_deterministic(True)
+        s_d, ido_d, el_d, nopx_d, _ = timed_run()
+        det_mode = dict(value=args.steps / el_d, ms_per_step=1e3 * el_d / args.steps,
+                        lanczos_steps_per_s=nopx_d / el_d, bitwise_reproducible=True,
+                        kernel="k_csr_ssell_det (64-bit fixed-point transposed terms)")
+        del s_d
+        pkg.set_deterministic(False)
     s, ido, elapsed, nopx, nsolves = timed_run()
     # Per-kernel roofline: the next K cycles of the same solve with hipEvents on
     # every kernel's dispatch (start event on a span's first kernel, stop event
@@ -596,6 +607,7 @@ def main():
         "gen_s": gen_s,
         "storage": storage,
         "full_storage": full_storage,
+        "deterministic": det_mode,
     }
     # SURVEY.md §8(d)'s byte model of the reference's arithmetic on the same
     # product / cycle, divided by OUR times: an "effective" rate that can exceed
