@@ -590,11 +590,16 @@ int arpack_hip_test_delayed_fill(double* dst, const double* src, double value, i
 int arpack_hip_test_symspmv_handoff(const arpack_hip_csr* A, const double* x, double* y, int fuse,
                                     double* load, int64_t load_n, int64_t* heads, int64_t cap,
                                     double* lo_out);
-/* Deterministic mode: every SpMV sum in a fixed order, so a solve is bitwise
- * reproducible run to run.  A later arpack_hip_csr_set_symmetric(A, 1) then
- * keeps the full-storage kernel (bitwise SciPy's csr_matvec) and returns 1,
- * and the complex operator uses its column-split kernel instead of the
- * LDS-atomic row tiles.  Off by default (ARPACK_HIP_DETERMINISTIC=1: on). */
+/* Deterministic mode: every SpMV sum independent of the wave schedule, so a
+ * solve is bitwise reproducible run to run.  A later
+ * arpack_hip_csr_set_symmetric(A, 1) selects the symmetric kernel's
+ * fixed-point form (transposed terms summed as exact 64-bit integers; the
+ * default kernel's rate) and returns 0, or keeps the full-storage kernel
+ * (bitwise SciPy's csr_matvec) and returns 1 for an operator outside that
+ * form; the complex operator's column-sorted tiles take their fixed-point
+ * form (else the column-split kernel).  Products of operators already
+ * declared symmetric follow the switch when they run.  Off by default
+ * (ARPACK_HIP_DETERMINISTIC=1 in the environment: on, read at first use). */
 void arpack_hip_set_deterministic(int on);
 int arpack_hip_deterministic(void);
 void arpack_hip_profile(int enable);
