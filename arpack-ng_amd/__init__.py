@@ -85,6 +85,8 @@ def _declare(L):
     L.arpack_hip_csr_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.arpack_hip_gen_laplace2d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
     L.arpack_hip_gen_laplace3d.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_double]
+    L.arpack_hip_gen_laplace3d_rows.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64,
+                                                C.c_int64, C.c_double]
     L.arpack_hip_gen_anderson.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int, C.c_double,
                                           C.c_uint32]
     L.arpack_hip_gen_banded_sym.argtypes = [C.POINTER(C.c_void_p), C.c_int64, C.c_int64,
@@ -245,7 +247,8 @@ def _ip(a):
     return a.ctypes.data_as(_PI)
 
 
-PROF_CLASSES = ["spmv", "cgs_dots", "update", "vq", "place", "finalize", "other"]
+PROF_CLASSES = ["spmv", "cgs_dots", "update", "vq", "place", "finalize", "other", "allreduce",
+                "halo"]
 
 
 def profile(enable: bool = True):
@@ -342,10 +345,18 @@ class CSR:
         return cls(h.value)
 
     @classmethod
-    def laplace3d(cls, m, scale=1.0):
+    def laplace3d(cls, m, scale=1.0, r0=0, r1=None):
+        """The m^3 7-pt Laplacian (BASELINE config 4); with r0/r1, only rows
+        [r0, r1) with global columns -- one rank's z-slab block for DistOp
+        (arpack_hip_gen_laplace3d_rows)."""
         h = C.c_void_p()
-        if lib().arpack_hip_gen_laplace3d(C.byref(h), m, scale) != 0:
-            raise RuntimeError("laplace3d generation failed")
+        if r0 == 0 and r1 is None:
+            rc = lib().arpack_hip_gen_laplace3d(C.byref(h), m, scale)
+        else:
+            rc = lib().arpack_hip_gen_laplace3d_rows(C.byref(h), m, r0, m ** 3 if r1 is None else r1,
+                                                     scale)
+        if rc != 0:
+            raise RuntimeError("laplace3d generation failed (rc=%d)" % rc)
         return cls(h.value)
 
     @classmethod

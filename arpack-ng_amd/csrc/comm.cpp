@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/arpack_hip.h"
+#include "device.hpp"
 #include "dist.hpp"
 
 namespace ahip {
@@ -63,8 +64,17 @@ int comm_failed(const Comm* c) {
     return c->failed;
 }
 
-int comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream) {
+static int comm_allreduce_raw(const Comm* c, double* dev, int count, hipStream_t stream);
+
+int comm_allreduce_sum(const Comm* c, double* dev, int count, hipStream_t stream, bool timed) {
     if (!c) return 0;
+    if (timed) dev::prof_begin(dev::kProfAllreduce, stream);
+    const int rc = comm_allreduce_raw(c, dev, count, stream);
+    if (timed) dev::prof_end(dev::kProfAllreduce, stream, 8.0 * count);
+    return rc;
+}
+
+static int comm_allreduce_raw(const Comm* c, double* dev, int count, hipStream_t stream) {
     if (c->h_allreduce) {
         auto* m = const_cast<Comm*>(c);
         m->h_buf.resize((size_t)count);

@@ -104,26 +104,29 @@ __global__ void k_band_fill(int64_t n, int64_t r0, int64_t r1, uint32_t seed, in
 }
 
 // ---- Laplacians -----------------------------------------------------------------
-__global__ void k_lap_count(int64_t m, int dim, int64_t* __restrict__ cnt) {
-    const int64_t n = dim == 2 ? m * m : m * m * m;
+// rows [r0, r0 + rows) of the m^dim grid operator (a row block for the
+// distributed engine: PARPACK/EXAMPLES/MPI/pdsdrv1.f's slab decomposition; the
+// whole operator is r0 = 0, rows = n), columns global
+__global__ void k_lap_count(int64_t m, int dim, int64_t r0, int64_t rows, int64_t* __restrict__ cnt) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < rows; li += stride) {
+        const int64_t i = r0 + li;
         const int64_t x = i % m, y = (i / m) % m, z = dim == 3 ? i / (m * m) : 0;
         int64_t c = 1 + (x > 0) + (x < m - 1) + (y > 0) + (y < m - 1);
         if (dim == 3) c += (z > 0) + (z < m - 1);
-        cnt[i] = c;
+        cnt[li] = c;
     }
 }
 
-__global__ void k_lap_fill(int64_t m, int dim, double scale, double disorder, uint32_t seed,
-                           const int64_t* __restrict__ rp, int32_t* __restrict__ col,
+__global__ void k_lap_fill(int64_t m, int dim, int64_t r0, int64_t rows, double scale, double disorder,
+                           uint32_t seed, const int64_t* __restrict__ rp, int32_t* __restrict__ col,
                            double* __restrict__ val) {
-    const int64_t n = dim == 2 ? m * m : m * m * m;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const double off = -1.0 * scale, dg = (dim == 2 ? 4.0 : 6.0) * scale;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < rows; li += stride) {
+        const int64_t i = r0 + li;
         const int64_t x = i % m, y = (i / m) % m, z = dim == 3 ? i / (m * m) : 0;
-        int64_t k = rp[i];
+        int64_t k = rp[li];
         auto put = [&](int64_t j, double v) { col[k] = (int32_t)j; val[k] = v; ++k; };
         if (dim == 3 && z > 0) put(i - m * m, off);
         if (y > 0) put(i - m, off);
@@ -396,15 +399,15 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
         return rc != 0 ? rc : -2;
     }
     if (rc != 0) return rc;
-    if (ahip::deterministic()) {
-        // the fixed-point form (k_csr_ssell_det) where every rank's plan allows
-        // it (a second agreement); otherwise the fixed-order full-storage SpMV
-        // stays, reported as kept (1) on every rank
-        const bool det = A->A.ss_det != 0;
-        if (c ? !ahip::dist_all_ok(c, det) : !det) {
-            csr_full_storage(A);
-            return 1;
-        }
+    // whether the fixed-point form (k_csr_ssell_det) serves every rank (a
+    // second agreement, made in either mode, so that deterministic mode turned
+    // on later finds it agreed); in deterministic mode without it the
+    // fixed-order full-storage SpMV stays, reported as kept (1) on every rank
+    const bool det = A->A.ss_det != 0;
+    A->A.ss_det_all = (c ? ahip::dist_all_ok(c, det) : det) ? 1 : 0;
+    if (ahip::deterministic() && !A->A.ss_det_all) {
+        csr_full_storage(A);
+        return 1;
     }
     A->A.kernel = ahip::dev::kCsrSymSell;
     // a distributed block: the spill-free exchange when every rank's lower ghost
@@ -467,24 +470,29 @@ double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, 
 }
 
 static int gen_lap(arpack_hip_csr** out, int64_t m, int dim, double scale, double disorder = 0.0,
-                   uint32_t seed = 0) {
+                   uint32_t seed = 0, int64_t r0 = 0, int64_t r1 = -1) {
     const int64_t n = dim == 2 ? m * m : m * m * m;
+    if (r1 < 0) r1 = n;
+    if (m < 1 || r0 < 0 || r1 <= r0 || r1 > n) return -1;
+    const int64_t rows = r1 - r0;
     int64_t *rp = nullptr, nnz = 0;
     int32_t* col = nullptr;
     double* val = nullptr;
     const int rc = build_generated(
-        n,
+        rows,
         [&](int64_t* cnt) {
-            hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim,
-                               cnt);
+            hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(rows)), dim3(256), 0, nullptr, m, dim,
+                               r0, rows, cnt);
         },
         [&](int64_t* rp_, int32_t* col_, double* val_) {
-            hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dim,
-                               scale, disorder, seed, rp_, col_, val_);
+            hipLaunchKernelGGL(ahip::gen::k_lap_fill, dim3(grid_of(rows)), dim3(256), 0, nullptr, m, dim,
+                               r0, rows, scale, disorder, seed, rp_, col_, val_);
         },
         &rp, &col, &val, &nnz);
     if (rc != 0) return rc;
-    return finish(out, n, n, nnz, rp, col, val);
+    if (finish(out, rows, n, nnz, rp, col, val) != 0) return -2;
+    (*out)->row_begin = r0;
+    return 0;
 }
 
 int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 2, scale); }
@@ -502,7 +510,7 @@ int arpack_hip_gen_convdiff2d(arpack_hip_csr** out, int64_t m, double rho) {
         n,
         [&](int64_t* cnt) {
             hipLaunchKernelGGL(ahip::gen::k_lap_count, dim3(grid_of(n)), dim3(256), 0, nullptr, m, 2,
-                               cnt);
+                               (int64_t)0, n, cnt);
         },
         [&](int64_t* rp_, int32_t* col_, double* val_) {
             hipLaunchKernelGGL(ahip::gen::k_cd_fill, dim3(grid_of(n)), dim3(256), 0, nullptr, m, dd, dl,
@@ -513,6 +521,9 @@ int arpack_hip_gen_convdiff2d(arpack_hip_csr** out, int64_t m, double rho) {
     return finish(out, n, n, nnz, rp, col, val);
 }
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale) { return gen_lap(A, m, 3, scale); }
+int arpack_hip_gen_laplace3d_rows(arpack_hip_csr** A, int64_t m, int64_t r0, int64_t r1, double scale) {
+    return gen_lap(A, m, 3, scale, 0.0, 0, r0, r1);
+}
 int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed) {
     return gen_lap(A, m, dim, 1.0, disorder, seed);
 }

@@ -336,6 +336,11 @@ struct Csr {
     double ss_amax = 0.0;
     int ss_bits = 0;
     int ss_det = 0;
+    // ss_det on every rank of a distributed operator (agreed when the storage
+    // was chosen; = ss_det on one GPU): deterministic mode switched on AFTER
+    // the operator was declared symmetric runs the full-storage (fixed-order)
+    // SpMV on every rank when this is 0 (csr_sym_det_fallback)
+    int ss_det_all = 0;
     int ss_detq = 0;  // most slices one wave walks in a superblock
 };
 enum CsrKernel : int {
@@ -394,8 +399,13 @@ void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue*
 // the first superblock / chain lighter (its workgroup carries the deferred
 // finalize); false under AHIP_LIGHT_SB=0
 bool light_first_sb();
+// AHIP_LIGHT_SB=2: the light superblock 0 shortened by 8% of a chain (A/B)
+bool light_sb_chain();
 // algorithmic HBM bytes of one SpMV: 12*nnz + 8*(n+1) (int64 rowptr) + 8n (x) + 8n (y)
 double csr_bytes(const Csr& A);
+// deterministic mode on a symmetric-storage operator whose fixed-point form is
+// not available (on some rank): the SpMV runs the full-storage kernel instead
+bool csr_sym_det_fallback(const Csr& A);
 
 // ------------------------------------------------------- per-kernel profiler --
 // hipEvent pairs around launches (enabled by arpack_hip_profile(1)); gives the
@@ -409,6 +419,8 @@ enum ProfClass : int {
     kProfPlace,
     kProfFinalize,
     kProfOther,     // rarely-open gated kernels (2nd refinement, zeroing), copies
+    kProfAllreduce, // row-distributed engine: each data-path RCCL allreduce (marker span)
+    kProfHalo,      // row-distributed SpMV: each halo / spill / ghost exchange group
     kProfClasses
 };
 struct ProfStat {

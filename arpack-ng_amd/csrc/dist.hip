@@ -34,7 +34,9 @@ static void exchange_general(const DistOp& D, hipStream_t s, bool p2p) {
     if (D.mode == DistOp::kGhostLists && D.nsend > 0)
         hipLaunchKernelGGL(k_pack, dim3(grid_for_rows(D.nsend)), dim3(256), 0, s, D.nsend, D.send_idx,
                            D.x_mid(), D.send_buf);
+    dev::prof_begin(dev::kProfHalo, s);
     comm_ghosts(D.comm, D, s, p2p);
+    dev::prof_end(dev::kProfHalo, s, 0.0);
 }
 
 void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool p2p, dev::FinQueue* q) {
@@ -45,16 +47,26 @@ void dist_spmv(const DistOp& D, hipStream_t s, const double* x, double* y, bool 
         return;
     }
     const dev::Csr& A = *D.A;
-    const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val;
+    // (deterministic mode without the fixed-point form on every rank: every
+    // rank takes the full-storage exchange and SpMV, csr_spmv's fallback)
+    const bool sym = A.kernel == dev::kCsrSymSell && A.ss_val && !dev::csr_sym_det_fallback(A);
     // spill-free symmetric form (A.ss_lg, agreed by every rank): one two-sided
     // halo, and the leading rows' lower ghost terms from the rank's own rows
+    // the halo group is a marker span of its own (profiler class halo; empty
+    // at one rank), inside the SpMV's span
+    dev::prof_begin(dev::kProfHalo, s);
     comm_halo(D.comm, D, s, sym && !A.ss_lg, p2p);
+    dev::prof_end(dev::kProfHalo, s, 0.0);
     if (sym) {
         dev::csr_spmv_sym_main(s, A, D.x_ext, y);
         // otherwise my rows' upper entries reach the next rank's first rows --
         // those transposed terms (the spill) travel forward and are combined
         // into the receiver's leading rows (a reverse halo)
-        if (!A.ss_lg) comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
+        if (!A.ss_lg) {
+            dev::prof_begin(dev::kProfHalo, s);
+            comm_spill(D.comm, A.ss_lo + A.ss_ncomb, A.ss_spill_out, A.ss_lo, D.send_lo, s, p2p);
+            dev::prof_end(dev::kProfHalo, s, 0.0);
+        }
         dev::csr_spmv_sym_combine(s, A, y, D.x_ext, q);
         return;
     }
@@ -67,7 +79,7 @@ int dist_all_ok(const Comm* c, int ok_local) {
     // one rank only, so every rank always joins the collective
     double h = ok_local ? 0.0 : 1.0, *d = comm_flag(c);  // SUM of failures
     bool ok = hipMemcpy(d, &h, sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
-    if (comm_allreduce_sum(c, d, 1, nullptr) != 0) ok = false;
+    if (comm_allreduce_sum(c, d, 1, nullptr, false) != 0) ok = false;
     ok = ok && hipMemcpy(&h, d, sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
     return ok && h == 0.0;
 }
@@ -134,7 +146,7 @@ bool host_allreduce(const Comm* c, std::vector<double>& h) {
         return false;
     }
     ok = h.empty() || hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
-    if (!h.empty() && comm_allreduce_sum(c, d, (int)h.size(), nullptr) != 0) ok = false;
+    if (!h.empty() && comm_allreduce_sum(c, d, (int)h.size(), nullptr, false) != 0) ok = false;
     ok = ok && (h.empty() || hipMemcpy(h.data(), d, bytes, hipMemcpyDeviceToHost) == hipSuccess);
     (void)hipFree(d);
     return dist_all_ok(c, ok);
@@ -270,7 +282,7 @@ int arpack_hip_dist_create(arpack_hip_dist** out, arpack_hip_csr* A, int64_t n_g
         return -1;
     }
     ok_tab = hipMemcpy(d, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice) == hipSuccess;
-    if (comm_allreduce_sum(c, d, (int)tab.size(), nullptr) != 0) ok_tab = 0;
+    if (comm_allreduce_sum(c, d, (int)tab.size(), nullptr, false) != 0) ok_tab = 0;
     if (hipMemcpy(tab.data(), d, sizeof(double) * tab.size(), hipMemcpyDeviceToHost) != hipSuccess)
         ok_tab = 0;
     (void)hipFree(d);
@@ -440,7 +452,8 @@ int arpack_hip_dist_info(const arpack_hip_dist* D, int64_t* halo_lo, int64_t* ha
 int arpack_hip_dist_spill(const arpack_hip_dist* D) {
     if (!D || !D->csr || !D->D.A) return -1;
     const ahip::dev::Csr& A = *D->D.A;
-    const bool sym = D->D.mode == ahip::DistOp::kHaloNeighbour && A.kernel == ahip::dev::kCsrSymSell && A.ss_val;
+    const bool sym = D->D.mode == ahip::DistOp::kHaloNeighbour && A.kernel == ahip::dev::kCsrSymSell &&
+                     A.ss_val && !ahip::dev::csr_sym_det_fallback(A);
     return sym && !A.ss_lg ? 1 : 0;
 }
 

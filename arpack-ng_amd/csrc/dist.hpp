@@ -22,8 +22,11 @@ Comm* comm_get();
 int comm_rank(const Comm*);
 int comm_size(const Comm*);
 // in-place SUM allreduce of `count` doubles on `stream`; 0, or -1 after an
-// RCCL / HIP / transport error (also recorded: comm_failed)
-int comm_allreduce_sum(const Comm*, double* dev, int count, hipStream_t stream);
+// RCCL / HIP / transport error (also recorded: comm_failed).  timed: the
+// collective is a marker span of the profiler's allreduce class (the engine's
+// data path: the Gram-Schmidt sums); the control plane's flag agreements and
+// plan tables pass false
+int comm_allreduce_sum(const Comm*, double* dev, int count, hipStream_t stream, bool timed = true);
 // nonzero once a collective of c failed (sticky; also polls RCCL's async error)
 int comm_failed(const Comm* c);
 // generation of a communicator and whether (c, gen) is still the live one

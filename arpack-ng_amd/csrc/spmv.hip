@@ -720,6 +720,13 @@ bool light_first_sb() {
     }();
     return on;
 }
+bool light_sb_chain() {
+    static const bool on = [] {
+        const char* e = getenv("AHIP_LIGHT_SB");
+        return e && e[0] == '2';
+    }();
+    return on;
+}
 
 int csr_analyse_ranges(Csr& A, int64_t ncols, void** owned) {
     const int64_t n = A.n;
@@ -1047,6 +1054,11 @@ int csr_analyse(Csr& A, int tile, int64_t** rblk_dev) {
 double csr_bytes(const Csr& A) {
     // bytes the selected kernel must move: val + column index (+ rowptr, x, y);
     // SELL: 10 B per stored nonzero + the 4-B row map (padding not counted)
+    if (csr_sym_det_fallback(A)) {  // the full-storage kernel csr_spmv runs instead
+        Csr F = A;
+        F.kernel = A.s_val ? kCsrSell : (A.rblk ? kCsrStream : kCsrVector);
+        return csr_bytes(F);
+    }
     if (A.kernel == kCsrSell && A.s_val)
         return 10.0 * (double)A.nnz + 4.0 * (double)A.n + 16.0 * (double)A.n;
     // symmetric storage: 10 B per stored upper-triangle entry + row map + x + y
@@ -1091,7 +1103,19 @@ static bool sell_fin() {
     return on;
 }
 
+bool csr_sym_det_fallback(const Csr& A) {
+    return A.kernel == kCsrSymSell && A.ss_val && !A.ss_det_all && deterministic();
+}
+
 void csr_spmv(hipStream_t s, const Csr& A, const double* x, double* y, FinQueue* q) {
+    if (csr_sym_det_fallback(A)) {
+        // the full CSR arrays stay resident under symmetric storage: the
+        // fixed-order full-storage form the operator had before
+        Csr F = A;
+        F.kernel = A.s_val ? kCsrSell : (A.rblk ? kCsrStream : kCsrVector);
+        csr_spmv(s, F, x, y, q);
+        return;
+    }
     if (A.kernel == kCsrSymSell && A.ss_val) {  // (carries a deferred finalize itself)
         csr_spmv_sym(s, A, x, y, q);
         return;

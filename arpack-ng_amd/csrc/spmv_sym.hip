@@ -51,46 +51,38 @@ namespace {
 constexpr int kSymThreads = 1024;
 constexpr int kSymWin = 10240;  // doubles per LDS window (x and y: 2 x 80 KB = all 160 KB)
 
-// per row: number of upper entries (col >= row) and their largest column
-// (at least the row itself, so every row's y slot is inside its window)
-// (columns relative to the diagonal's: j - coff, coff = halo_lo for a rank's
-// block of a row-distributed operator whose x is [halo_lo | local | halo_hi])
-// Also the deterministic form's scale inputs (k_csr_ssell_det): the largest
-// |a_ij| above the diagonal (as the bits of a non-negative double, which order
-// like the unsigned integers) and the most entries left of the diagonal in a
-// row (= the transposed terms that row receives).
+// Per row: the count of upper entries (diagonal included; bit 30 flags a
+// column left of the block) and the largest column; over the matrix: the
+// largest |a_ij| above the diagonal (as the bits of a non-negative double,
+// which order like the unsigned integers).  Per column j (local, spill columns
+// [n, n + spill_out) included): the strictly-upper entries (i < j) whose
+// transposed terms the fixed-point form sums into word j -- its overflow
+// headroom is the largest of these counts, whatever the pattern's symmetry.
 __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict__ rp,
                               const int32_t* __restrict__ col, const double* __restrict__ val,
                               int32_t* __restrict__ cnt, int32_t* __restrict__ cmax,
-                              unsigned long long* __restrict__ amax, int* __restrict__ lmax) {
+                              unsigned long long* __restrict__ amax, int32_t* __restrict__ ccol) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     double am = 0.0;
-    int lm = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        int32_t c = 0, m = (int32_t)i, low = 0, lower = 0;
+        int32_t c = 0, m = (int32_t)i, low = 0;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
             const int32_t j = (int32_t)(col[k] - coff);
             if (j >= i) {
                 ++c;
                 m = max(m, j);
-                if (j > i) am = fmax(am, fabs(val[k]));
-            } else {
-                ++lower;
+                if (j > i) {
+                    am = fmax(am, fabs(val[k]));
+                    atomicAdd(&ccol[j], 1);
+                }
             }
             low |= j < 0;  // a column of the previous rank's block (halo_lo)
         }
         cnt[i] = c | (low << 30);
         cmax[i] = m;
-        lm = max(lm, lower);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        am = fmax(am, __shfl_xor(am, o, 64));
-        lm = max(lm, __shfl_xor(lm, o, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(amax, (unsigned long long)__double_as_longlong(am));
-        atomicMax(lmax, lm);
-    }
+    for (int o = 32; o > 0; o >>= 1) am = fmax(am, __shfl_xor(am, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, (unsigned long long)__double_as_longlong(am));
 }
 
 // one 64-thread block per slice, lane = row: the row's upper entries in CSR
@@ -810,15 +802,17 @@ int symsell_plan(int64_t n, const int32_t* cmax, int win, std::vector<int64_t>& 
         return plan_check(n, cmax, win, r0s, spans, pre, off, spill_in, spill_out);
     };
     // k blocks with the first one lighter: workgroup 0 walks chain 0 and then
-    // runs the step's deferred finalize (k_csr_ssell FUSE), so chain 0 gets
-    // ~8% of one chain's rows fewer (~5 us at a 1.25e6-row share, ~3 us at
-    // n = 1e7; the finalize takes 3-6 us) and the finalize overlaps the other
-    // chains instead of trailing them.  Inside a chain the window shift needs
-    // span <= 2R, so the first superblock keeps at least the reach m.
+    // runs the step's deferred finalize (k_csr_ssell FUSE), so the finalize
+    // overlaps the other chains instead of trailing them.  Superblock 0 (of R
+    // rows) is shortened by d = 8% of R / chain -- at n = 1e7 (chain 4) 2% of R,
+    // ~0.5% of chain 0's rows, about 1 us of its walk; AHIP_LIGHT_SB=2 takes
+    // the larger d = 8% of the chain's rows (2 R chain / 25) for the
+    // A/B.  Inside a chain the window shift needs span <= 2R, so the first
+    // superblock keeps at least the reach m.
     auto light_first = [&](int64_t k) {
         if (!light_first_sb() || kQuantum <= 0 || k % kQuantum != 0 || k < 2) return false;
         const int64_t chain = k / kQuantum, R = n / k;
-        int64_t d = (R * 2) / (25 * chain);  // 8% of a chain
+        int64_t d = light_sb_chain() ? (R * 2 * chain) / 25 : (R * 2) / (25 * chain);
         if (chain > 1 && R - d < m + 1) d = R - (m + 1);
         if (d <= 0) return false;
         r0s.resize(k + 1);
@@ -861,34 +855,42 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
                       void** owned) {
     const int64_t n = A.n;
     if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
-    int32_t *dcnt = nullptr, *dcm = nullptr;
-    unsigned long long* dst = nullptr;  // [0]: amax bits, [1]: lower-count max
-    if (fault_filter(hipMalloc(&dcnt, sizeof(int32_t) * n)) != hipSuccess) return -2;
-    if (fault_filter(hipMalloc(&dcm, sizeof(int32_t) * n)) != hipSuccess) {
-        (void)hipFree(dcnt);
-        return -2;
-    }
-    if (fault_filter(hipMalloc(&dst, 2 * sizeof(unsigned long long))) != hipSuccess) {
+    const int64_t nc = n + spill_out;  // columns that receive transposed terms
+    int32_t *dcnt = nullptr, *dcm = nullptr, *dcc = nullptr;
+    unsigned long long* dst = nullptr;  // amax bits
+    auto free_all = [&]() {
         (void)hipFree(dcnt);
         (void)hipFree(dcm);
+        (void)hipFree(dcc);
+        (void)hipFree(dst);
+    };
+    if (fault_filter(hipMalloc(&dcnt, sizeof(int32_t) * n)) != hipSuccess ||
+        fault_filter(hipMalloc(&dcm, sizeof(int32_t) * n)) != hipSuccess ||
+        fault_filter(hipMalloc(&dcc, sizeof(int32_t) * nc)) != hipSuccess ||
+        fault_filter(hipMalloc(&dst, sizeof(unsigned long long))) != hipSuccess) {
+        free_all();
         return -2;
     }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    bool got = fault_filter(hipMemset(dst, 0, 2 * sizeof(unsigned long long))) == hipSuccess;
+    bool got = fault_filter(hipMemset(dst, 0, sizeof(unsigned long long))) == hipSuccess &&
+               fault_filter(hipMemset(dcc, 0, sizeof(int32_t) * nc)) == hipSuccess;
     if (got)
         AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
-                    A.val, dcnt, dcm, dst, reinterpret_cast<int*>(dst + 1));
-    std::vector<int32_t> cnt(n), cm(n);
+                    A.val, dcnt, dcm, dst, dcc);
+    std::vector<int32_t> cnt(n), cm(n), ccol(nc);
     unsigned long long hst[2] = {0, 0};
     got = got &&
           fault_filter(hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
           fault_filter(hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
-          fault_filter(hipMemcpy(hst, dst, sizeof(hst), hipMemcpyDeviceToHost)) == hipSuccess;
-    (void)hipFree(dcnt);
-    (void)hipFree(dcm);
-    (void)hipFree(dst);
+          fault_filter(hipMemcpy(ccol.data(), dcc, sizeof(int32_t) * nc, hipMemcpyDeviceToHost)) == hipSuccess &&
+          fault_filter(hipMemcpy(hst, dst, sizeof(unsigned long long), hipMemcpyDeviceToHost)) == hipSuccess;
+    free_all();
     if (!got) return -2;
+    // the most transposed terms one word sums (per column, not the
+    // row's lower count, which equals it only for a structurally symmetric
+    // pattern and never sees the spill columns)
+    for (int64_t j = 0; j < nc; ++j) hst[1] = std::max<unsigned long long>(hst[1], (unsigned long long)ccol[j]);
     // rows with columns before the block (a distributed block's low halo): the
     // spill-free exchange computes their lower ghost terms locally
     int64_t lg_rows = 0;

@@ -556,6 +556,8 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
         return;
     }
     if (A.tile && A.t_det) {  // deterministic: the fixed-point tile form (else the CSR split, kept)
+        // (t_xmax, like s_y, is the operator's scratch: one stream per ZCsr,
+        // include/arpack_hip.h -- ADVICE r05)
         hipLaunchKernelGGL(k_zabsmax, dim3(kZMaxBlocks), dim3(256), 0, s, 2 * A.n,
                            reinterpret_cast<const double*>(x2), A.t_xmax, gate);
         hipLaunchKernelGGL(k_ztile_det<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w,

@@ -135,21 +135,40 @@ def launch_ranks(args, argv) -> int:
     return rc
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch of `kernel_substr` from the committed rocprofv3 PMC
+def kernel_family(name: str):
+    """`k_csr_ssell` of 'void ahip::dev::(anonymous namespace)::k_csr_ssell<8, ...>(...)'."""
+    import re
+    m = re.search(r"(k_[A-Za-z0-9_]+)\s*[<(]", name)
+    return m.group(1) if m else name
+
+
+# the keys a PMC summary's workload block must share with the line it serves
+PMC_KEYS = ("workload", "n", "nnz", "storage", "deterministic")
+
+
+def pmc_traffic(families, workload, profiles_dir=None):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC
     summary (profiles/r*_pmc.json, written by tools/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes of this same command, gfx950-corrected)."""
+    FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected) OF THIS WORKLOAD: only a
+    summary whose "workload" block equals `workload` on PMC_KEYS counts (the
+    newest such file); the launch-weighted mean over the kernels whose family
+    (template name) is in `families`.  Returns (bytes, file, None), or
+    (None, None, reason)."""
     import glob
-    # the newest profile set that measured this kernel (other configs' PMC
-    # summaries, e.g. the complex kernels', live beside it)
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+    d = profiles_dir or os.path.join(ROOT, "profiles")
+    for f in sorted(glob.glob(os.path.join(d, "r*_pmc.json")), reverse=True):
         with open(f) as fh:
-            ks = json.load(fh).get("kernels", {})
-        hits = [v for k, v in ks.items() if kernel_substr in k]
-        if hits:
-            v = max(hits, key=lambda e: e["launches"])
-            return v["traffic_bytes"], os.path.basename(f)
-    return None, None
+            doc = json.load(fh)
+        w = doc.get("workload")
+        if not isinstance(w, dict) or any(w.get(k) != workload.get(k) for k in PMC_KEYS):
+            continue
+        hits = [v for k, v in doc.get("kernels", {}).items() if kernel_family(k) in families]
+        n = sum(v["launches"] for v in hits)
+        if n:
+            return sum(v["traffic_bytes"] * v["launches"] for v in hits) / n, os.path.basename(f), None
+    return None, None, ("no committed PMC summary of this workload (%s) holds %s" %
+                        (", ".join("%s=%s" % (k, workload.get(k)) for k in PMC_KEYS),
+                         "/".join(sorted(families))))
 
 
 def cpu_share():
@@ -190,6 +209,8 @@ def cpu_baseline(args, cycles):
     cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--seed",
            str(args.seed), "--bandwidth", str(args.bandwidth), "--per-row", str(args.per_row),
            "--threads", str(threads), "--cycles", str(cycles)]
+    if args.workload == "lap3d":
+        cmd += ["--lap3d", str(args.m)]
     if not args.no_cpu_ttc:
         cmd.append("--ttc")
     try:
@@ -230,11 +251,51 @@ def ref_model_bytes(n, nnz, kev, kplusp):
     return spmv, steps + apps
 
 
+def comm_report(prof, D, dist, rank, ms_per_step):
+    """The row-distributed engine's collectives in the profiled cycles: per rank
+    and max over ranks, the device time per Lanczos step of the data-path RCCL
+    allreduces (profiler class "allreduce": the Gram-Schmidt sums,
+    PARPACK/SRC/MPI/pdsaitr.f:575-776) and of the SpMV's halo groups ("halo"),
+    their counts per step, the kernels' time per step beside them, and
+    comm_share = (allreduce + halo) per restart cycle / ms_per_step.  None on
+    the single-GPU engine (no communicator)."""
+    if D is None or not prof["spmv"][2]:
+        return None
+    steps = prof["spmv"][2]            # one SpMV (one halo group) per Lanczos step
+    cyc = max(prof["vq"][2], 1)        # one V*Q per restart cycle
+    ar_ms, _, ar_n = prof["allreduce"]
+    h_ms, _, h_n = prof["halo"]
+    kern_ms = sum(v[0] for k, v in prof.items() if k not in ("allreduce", "halo")) - h_ms
+    mine = dict(rank=rank, lanczos_steps=steps, cycles=cyc,
+                allreduce_us_per_step=1e3 * ar_ms / steps, allreduce_per_step=ar_n / steps,
+                halo_us_per_step=1e3 * h_ms / steps, halo_per_step=h_n / steps,
+                kernels_us_per_step=1e3 * kern_ms / steps,
+                comm_ms_per_cycle=(ar_ms + h_ms) / cyc)
+    ranks = [mine]
+    if dist:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, mine)
+    keys = ("allreduce_us_per_step", "halo_us_per_step", "kernels_us_per_step", "comm_ms_per_cycle")
+    mx = {k: max(r[k] for r in ranks) for k in keys}
+    return dict(per_rank=ranks, max_over_ranks=mx,
+                comm_share=mx["comm_ms_per_cycle"] / ms_per_step if ms_per_step > 0 else None,
+                measured_on="hipEvent marker spans on the engine's stream around each data-path "
+                            "allreduce and each halo group, in the profiled cycles (not the timed "
+                            "ones); the SpMV span holds its halo group, reported apart here",
+                counts_note="allreduce_per_step and halo_per_step are launches per Lanczos step "
+                            "(restart-cycle collectives included in the average)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=("ns", "lap3d"), default="ns",
+                    help="ns: the north-star banded symmetric CSR (n = --rows); lap3d: BASELINE "
+                         "config 4, the 3-D 7-pt Laplacian m^3 (m = --m), row-block / z-slab "
+                         "sharded over the ranks (PARPACK/EXAMPLES/MPI/pdsdrv1.f)")
+    ap.add_argument("--m", type=int, default=215, help="lap3d grid edge (n = m^3; 215: 9.94e6)")
     ap.add_argument("--rows", "--n", dest="n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=25)
     ap.add_argument("--bandwidth", type=int, default=4096)
@@ -266,6 +327,12 @@ def main():
                          "SpMV forms (--storage sym: the fixed-point symmetric kernel "
                          "k_csr_ssell_det), so every solve is bitwise reproducible")
     args = ap.parse_args()
+    if args.workload == "lap3d":
+        args.n = args.m ** 3
+        # the 7-pt Laplacian's top eigenvalues are clustered (multiplicities 3
+        # and 6, gaps ~ 1/m^2): the tol = 1e-6 solve runs hundreds of cycles on
+        # either side, so config 4's line is the restart-cycle rate only
+        args.no_ttc = args.no_cpu_ttc = True
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         sys.exit(2)
@@ -328,7 +395,10 @@ def main():
         dist.all_gather_object(allr, devices[0])
         devices = allr
     t = time.time()
-    A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row, r0, r1)
+    if args.workload == "lap3d":  # this rank's z-slab rows, global columns
+        A = pkg.CSR.laplace3d(args.m, 1.0, r0, r1)
+    else:
+        A = pkg.CSR.banded_sym(n, args.seed, args.bandwidth, args.per_row, r0, r1)
     if world > 1 or args.force_dist:
         D = pkg.DistOp(A, n, r0)
     storage = "full"
@@ -521,9 +591,12 @@ def main():
     del v0
 
     if prof is None:
-        prof = {k: (0.0, 0.0, 0) for k in ("spmv", "cgs_dots", "update", "vq", "place",
-                                           "finalize", "other")}
+        prof = {k: (0.0, 0.0, 0) for k in pkg.PROF_CLASSES}
     ms, by, cnt = prof["spmv"]
+    if D is not None:
+        # a row-distributed SpMV is a marker span holding its halo group: the
+        # kernel's own time is the span less the halo's
+        ms = max(ms - prof["halo"][0], 0.0)
     spmv_avg_ms = ms / max(cnt, 1)
     spmv_bytes = by / max(cnt, 1)
     achieved = spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9 if cnt else None
@@ -535,10 +608,24 @@ def main():
     step_ms = ms + orth_ms
     step_gbs = (by + orth_bytes) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
 
-    # PMC traffic is collected on the default single-GPU workload only
-    spmv_kernel = "k_csr_ssell" if storage == "sym" else "k_csr_sell"
-    traffic, traffic_src = (pmc_traffic(spmv_kernel) if world == 1 and n == 10_000_000
-                            else (None, None))
+    # counter traffic from a committed PMC summary of THIS workload (same
+    # operator, size, storage and mode), single GPU only
+    families = ({"k_csr_ssell_det"} if args.deterministic else {"k_csr_ssell"}) if storage == "sym" \
+        else {"k_csr_sell", "k_csr_sell_fin"}
+    wl = dict(workload=args.workload, n=n, nnz=nnz, storage=storage,
+              deterministic=bool(args.deterministic))
+    if world == 1 and D is None:
+        traffic, traffic_src, traffic_note = pmc_traffic(families, wl)
+    else:
+        traffic, traffic_src, traffic_note = None, None, "PMC summaries are single-GPU runs"
+    comm_prof = comm_report(prof, D, dist, rank, 1e3 * elapsed / args.steps)
+    if args.workload == "lap3d":
+        wl_name = ("dsaupd LA on the 3-D 7-pt Laplacian m=%d, n=%d (BASELINE config 4, "
+                   "pdsaupd-equivalent row-block / z-slab sharding)" % (args.m, n))
+        data = "synthetic (3-D 7-pt Laplacian generated in HBM, each rank its own z-slab rows)"
+    else:
+        wl_name = "dsaupd LA on NS symmetric CSR (BASELINE north star)"
+        data = "synthetic (NS operator generated in HBM from a counter hash; no files)"
     out = {
         "metric": "Arnoldi iters/sec + time-to-converge (nev=10), n=10M CSR; %HBM roofline",
         "value": iters_per_s,
@@ -551,8 +638,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (NS operator generated in HBM from a counter hash; no files)",
-        "config": {"workload": "dsaupd LA on NS symmetric CSR (BASELINE north star)",
+        "data": data,
+        "config": {"workload": wl_name, "workload_key": args.workload,
                    "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
                    "which": "LA", "tol": "eps (a solve that converges inside the timed window is followed by a fresh one)",
                    "spmv_storage": "symmetric (upper triangle)" if storage == "sym" else "full CSR",
@@ -572,7 +659,8 @@ def main():
         "time_to_converge": ttc,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                     "traffic_source": traffic_src,
+                     "traffic_source": traffic_src, "traffic_note": traffic_note,
+                     "traffic_ratio": (traffic / spmv_bytes) if traffic and spmv_bytes else None,
                      "kernel": ("csr_spmv symmetric storage (k_csr_ssell: upper-triangle SELL-64 "
                                 "slices over LDS x/y windows, LDS atomic transposed terms, 16-bit "
                                 "window-relative cols; on one GPU the chain-head combine and the "
@@ -610,6 +698,7 @@ def main():
                      "spmv_plus_orth_gbs": step_gbs,
                      "spmv_plus_orth_frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None},
         "kernels": kernels,
+        "comm_profile": comm_prof,
         "gen_s": gen_s,
         "storage": storage,
         "full_storage": full_storage,

@@ -278,7 +278,11 @@ void arpack_hip_dnaupd_csr_cycles(const arpack_hip_csr* A, int max_cycles, int* 
 /* Complex CSR operator (rowptr int64[n+1], col int32[nnz], val complex128[nnz]
  * interleaved) and the complex random operator of BASELINE config 5 (SURVEY.md
  * §8d S5: per_row hashed columns, U(-1,1)+iU(-1,1) on a 2^-10 grid, duplicate
- * columns summed, diagonal += dshift). */
+ * columns summed, diagonal += dshift).  The product's scratch (the column
+ * slices' partial sums and, in deterministic mode, the block maxima of |x| that
+ * set the fixed-point scale) belongs to the operator: products of one
+ * arpack_hip_zcsr must be ordered on one stream (two solves sharing it run one
+ * after the other, or each holds its own operator). */
 typedef struct arpack_hip_zcsr arpack_hip_zcsr;
 int arpack_hip_zcsr_create(arpack_hip_zcsr** A, int64_t n, int64_t nnz, const int64_t* rowptr,
                            const int32_t* col, const double* val);
@@ -598,7 +602,9 @@ int arpack_hip_test_symspmv_handoff(const arpack_hip_csr* A, const double* x, do
  * (bitwise SciPy's csr_matvec) and returns 1 for an operator outside that
  * form; the complex operator's column-sorted tiles take their fixed-point
  * form (else the column-split kernel).  Products of operators already
- * declared symmetric follow the switch when they run.  Off by default
+ * declared symmetric follow the switch when they run: the fixed-point form
+ * where it serves the operator (on every rank of a distributed one), else the
+ * full-storage kernel over the still-resident full CSR.  Off by default
  * (ARPACK_HIP_DETERMINISTIC=1 in the environment: on, read at first use). */
 void arpack_hip_set_deterministic(int on);
 int arpack_hip_deterministic(void);
@@ -612,6 +618,12 @@ int arpack_hip_gen_laplace2d(arpack_hip_csr** A, int64_t m, double scale);
  * (EXAMPLES/NONSYM/dndrv1.f:397-475; complex spectrum once rho*h/2 > 1). */
 int arpack_hip_gen_convdiff2d(arpack_hip_csr** A, int64_t m, double rho);
 int arpack_hip_gen_laplace3d(arpack_hip_csr** A, int64_t m, double scale);
+/* Rows [row_begin, row_end) of the m^3 7-pt Laplacian with global columns: one
+ * rank's z-slab block of BASELINE config 4 (the row-block decomposition of
+ * PARPACK/EXAMPLES/MPI/pdsdrv1.f:429-480), bit-identical to those rows of
+ * arpack_hip_gen_laplace3d; -1 on an empty or out-of-range block. */
+int arpack_hip_gen_laplace3d_rows(arpack_hip_csr** A, int64_t m, int64_t row_begin, int64_t row_end,
+                                  double scale);
 int arpack_hip_gen_anderson(arpack_hip_csr** A, int64_t m, int dim, double disorder, uint32_t seed);
 int arpack_hip_gen_banded_sym(arpack_hip_csr** A, int64_t n, int64_t row_begin,
                               int64_t row_end, uint32_t seed, int bandwidth, int per_row);

@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--bandwidth", type=int, default=4096)
     ap.add_argument("--per-row", type=int, default=25)
+    ap.add_argument("--lap3d", type=int, default=0,
+                    help="m > 0: the bench's lap3d workload (BASELINE config 4, the m^3 7-pt "
+                         "Laplacian) in place of the banded operator; --n is m^3")
     ap.add_argument("--nev", type=int, default=10)
     ap.add_argument("--ncv", type=int, default=30)
     ap.add_argument("--threads", type=int, default=16)
@@ -84,7 +87,11 @@ def main():
     pkg = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(pkg)
     t = time.time()
-    A = pkg.CSR.banded_sym(args.n, args.seed, args.bandwidth, args.per_row)
+    if args.lap3d > 0:
+        args.n = args.lap3d ** 3
+        A = pkg.CSR.laplace3d(args.lap3d)
+    else:
+        A = pkg.CSR.banded_sym(args.n, args.seed, args.bandwidth, args.per_row)
     rowptr, col, val = A.download()
     del A
     t_gen = time.time() - t
@@ -132,7 +139,7 @@ def main():
         setup_s=stamps[opens[0]] - t_start, gen_download_s=t_gen, nnz=int(len(col)), n=n,
         kind="reference",
         sample=f"restart cycles 1..{args.cycles} (np={np_} Lanczos steps + dsapps each) of the "
-               f"bench workload's tol=eps solve from dlarnv(1,3,5,7), reference Fortran dsaupd_ "
+               f"bench workload's ({'lap3d m=%d' % args.lap3d if args.lap3d else 'NS'}) tol=eps solve from dlarnv(1,3,5,7), reference Fortran dsaupd_ "
                f"+ OpenBLAS, OpenMP CSR OP, {args.threads} threads")
     del v, workd, workl
     if args.ttc:

@@ -198,13 +198,18 @@ def lap3d(pkg, out, rank, world, m, cap):
     n = len(rp) - 1
     r0, r1 = pkg.partition_rows(n, world, rank)
     nloc = r1 - r0
-    A = pkg.CSR.from_arrays(rp[r0:r1 + 1] - rp[r0], col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]])
+    # the device generator's row-block form (bench.py --workload lap3d builds
+    # each rank's slab this way) == rows r0:r1 of the global operator
+    A = pkg.CSR.laplace3d(m, 1.0, r0, r1)
+    lrp, lcol, lval = A.download()
+    gen_ok = (np.array_equal(lrp, rp[r0:r1 + 1] - rp[r0]) and
+              np.array_equal(lcol, col[rp[r0]:rp[r1]]) and np.array_equal(lval, val[rp[r0]:rp[r1]]))
     D = pkg.DistOp(A, n, r0)
     s = pkg.SymRci(nloc, 10, 30, "LA", 1e-10, mxiter=cap, v0=dlarnv_fast(n)[r0:r1], device=True)
     assert pkg.pdsaupd_cycles(s, D, -1) == 99
     np.savez(os.path.join(out, "rank%d.npz" % rank), iparam=s.iparam.copy(), info=s.info.copy(),
              ritz=np.asarray(s.ritz), halo=np.array(list(D.info().values())),
-             failed=np.array([pkg.comm_failed()]))
+             failed=np.array([pkg.comm_failed()]), gen_ok=np.array([gen_ok]))
     del D
 
 

@@ -186,6 +186,54 @@ def test_full_window_keeps_full_storage(pkg, det):
     pkg.set_deterministic(True)
 
 
+def test_declared_first_then_deterministic_runs_full_storage(pkg):
+    """an operator declared symmetric while deterministic
+    mode is off, whose fixed-point form is NOT available (the full-window
+    operator above: ss_det = 0), keeps the LDS-atomic kernel -- until the mode
+    is switched on: its products then run the full-storage fixed-order kernel
+    (the full CSR stays resident), so they repeat bitwise and equal the
+    full-storage product bit for bit; switching the mode off restores the
+    symmetric kernel."""
+    import scipy.sparse as sp
+    n = 20_000
+    i = np.arange(n)
+    rows = np.concatenate([i, i[1:], i[:-1], [0, 10_239]])
+    cols = np.concatenate([i, i[:-1], i[1:], [10_239, 0]])
+    vals = np.concatenate([np.full(n, 2.0), np.full(2 * (n - 1), -1.0), [0.5, 0.5]])
+    S = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    S.sort_indices()
+    x = np.random.default_rng(4).standard_normal(n) * 10.0 ** np.random.default_rng(5).uniform(-6, 0, n)
+    xd, yd = pkg.DeviceBuffer.from_numpy(x), pkg.DeviceBuffer(n)
+    F = pkg.CSR.from_arrays(S.indptr, S.indices, S.data)  # full storage throughout
+    F.matvec_device(xd, yd)
+    y_full = yd.numpy().copy()
+    pkg.set_deterministic(False)
+    A = pkg.CSR.from_arrays(S.indptr, S.indices, S.data)
+    A.set_symmetric(True)
+    assert A.last_rc == 0 and A.symmetric
+    try:
+        pkg.set_deterministic(True)
+        ys = []
+        for _ in range(4):
+            pkg.lib().arpack_hip_memset(yd.ptr, 0xFF, 8 * n)
+            A.matvec_device(xd, yd)
+            ys.append(yd.numpy().copy())
+        for y in ys:
+            np.testing.assert_array_equal(y.view(np.int64), y_full.view(np.int64))
+        # and a solve through it is bitwise repeatable
+        v0 = M.dlarnv_uniform(n)[0]
+        runs = []
+        for _ in range(2):
+            s = pkg.SymRci(n, 4, 20, "LA", 1e-10, mxiter=300, device=True, v0=v0)
+            assert s.aupd_csr(A) == 99 and int(s.info[0]) == 0
+            runs.append(s.eupd(rvec=False)[0].copy())
+        np.testing.assert_array_equal(runs[0], runs[1])
+    finally:
+        pkg.set_deterministic(False)
+    A.matvec_device(xd, yd)  # the symmetric kernel again: SciPy's product to rounding
+    np.testing.assert_allclose(yd.numpy(), S @ x, rtol=0, atol=1e-12 * np.abs(x).max() * 4)
+
+
 def test_deterministic_off_restores_symmetric(pkg):
     pkg.set_deterministic(False)
     A = pkg.CSR.banded_sym(200_000, 1234, 4096, 25)

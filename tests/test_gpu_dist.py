@@ -216,10 +216,13 @@ def _lap3d_reference(m, cap):
     return _LAP[(m, cap)]
 
 
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_lap3d_config4_family_ranks(tmp_path, P):
     """BASELINE config 4's operator family (3-D 7-pt Laplacian, row-block /
-    z-slab sharding) at m = 60 (n = 216,000) over P host-transport ranks,
+    z-slab sharding) at m = 60 (n = 216,000) over P host-transport ranks
+    (P = 8: the 8-way plan of config 4 as stated, 27,000 rows a rank), each
+    rank's block from the device generator's row-block form,
     capped at 6 restart cycles: every rank reports the reference's info,
     cycles and OP*x, and the ncv Ritz values in workl agree with the
     reference's to 1e-10 relative; each interior rank exchanges one m x m plane
@@ -229,6 +232,7 @@ def test_lap3d_config4_family_ranks(tmp_path, P):
     ranks = _run(tmp_path, "lap3d", "m%d_cap%d" % (m, cap), P)
     for r in ranks:
         assert not bool(r["failed"][0])
+        assert bool(r["gen_ok"][0])
         assert int(r["info"][0]) == ref["info"]
         for k in (2, 4, 8):
             assert int(r["iparam"][k]) == int(ref["iparam"][k]), (P, k)
@@ -236,6 +240,8 @@ def test_lap3d_config4_family_ranks(tmp_path, P):
         assert np.all(np.abs(got - want) <= 1e-10 * np.maximum(1.0, np.abs(want)))
     h = ranks[1]["halo"]  # {halo_lo, halo_hi, send_lo, send_hi}
     assert h[0] == m * m and (P == 2 or h[1] == m * m)
+    # the end ranks exchange one plane on their inner side only
+    assert ranks[0]["halo"][0] == 0 and ranks[-1]["halo"][1] == 0
 
 
 @pytest.mark.timeout(600)

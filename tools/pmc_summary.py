@@ -1,6 +1,6 @@
 """Per-kernel HBM traffic from rocprofv3 PMC passes (MI355X_MICROARCH.md, HBM section).
 
-    python tools/pmc_summary.py FETCH_DIR WRITE_DIR [TRACE_DIR] > profiles/rNN_pmc.json
+    python tools/pmc_summary.py [--workload JSON] FETCH_DIR WRITE_DIR [TRACE_DIR] > profiles/rNN_pmc.json
     python tools/pmc_summary.py --stats TRACE_DIR > profiles/rNN_kernel_stats.csv
 
 Reads rocprofv3 CSV output or its rocpd SQLite database (the default format).
@@ -10,6 +10,11 @@ not fit one TCC pass).  Both are reported in KiB.  On gfx950 FETCH_SIZE counts
 128-B memory-side read requests as 64 B, so the corrected read bytes are
 2 x FETCH_SIZE; WRITE_SIZE is exact for streaming stores.  Output: per kernel
 name, launches, mean raw FETCH/WRITE (bytes) and the corrected traffic per launch.
+
+--workload JSON: the profiled command's workload ({"workload", "n", "nnz",
+"storage", "deterministic", "command"}, as bench.py's config names it), stored
+in the summary; bench.py takes a summary's traffic only for a line of that
+same workload (bench.pmc_traffic).
 """
 import csv
 import glob
@@ -60,6 +65,10 @@ def stats_csv(d):
 
 
 def main():
+    workload = None
+    if len(sys.argv) > 2 and sys.argv[1] == "--workload":
+        workload = json.loads(sys.argv[2])
+        del sys.argv[1:3]
     if sys.argv[1] == "--stats":
         return stats_csv(sys.argv[2])
     fetch = load(sys.argv[1], "FETCH_SIZE")
@@ -77,8 +86,11 @@ def main():
             e["avg_ns"] = dur[k]["avg_ns"]
             e["traffic_gbs"] = e["traffic_bytes"] / dur[k]["avg_ns"]
         res[k] = e
-    json.dump(dict(correction="traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
-                   kernels=res), sys.stdout, indent=1)
+    doc = dict(correction="traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
+               kernels=res)
+    if workload is not None:
+        doc["workload"] = workload
+    json.dump(doc, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
