@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <type_traits>
 #include <cstring>
 #include <cstdint>
 #include <vector>
@@ -130,17 +131,62 @@ __device__ __forceinline__ T ldg(const T* p) {
 // with another workgroup's (or rank's) spill through the slots, and only its
 // last superblock's spill leaves through a slot.  Each wave streams its slices
 // with the next slice's first chunk in flight, across superblock boundaries.
+//
+// ONE walk, two accumulators (DET):
+//  * DET = false (default): the transposed terms a_ij x_i meet as LDS fp64
+//    atomic adds in the y window, in wave-schedule order -- not bitwise
+//    reproducible run to run (~1 ulp of the row's terms);
+//  * DET = true (deterministic mode, arpack_hip_set_deterministic): they become
+//    64-bit FIXED-POINT integers, and integer addition is exact, so their sum
+//    is the same in any order:
+//      q = rint(a_ij x_i 2^(B-E))      (one fma onto 1.5 * 2^52: the low mantissa
+//                                       bits of the result are q, |q| < 2^B <= 2^51)
+//      y_j = (row sum) + (double)(sum of the q) * 2^(E-B)
+//    with 2^E >= amax * (largest |x| the chain has staged so far): a running
+//    maximum, so E only grows, and a partial sum carried into the next window
+//    is rescaled by an arithmetic shift when it does; B = min(51, 62 - bits(L))
+//    for columns that receive at most L transposed terms, so no sum can
+//    overflow.  Each term is rounded to 2^(E-B) -- at most 2^-51 of the
+//    window's largest product.  The row sums (one lane's sequential sum, as in
+//    the default) wait in registers (at most MAXQ slices a wave) until the
+//    window's x is spent, then meet the integer sums in the x window.  One LDS
+//    word past every window (span <= kSymWin - 1) holds the running maximum.
+// Everything else -- chunk pipeline, window carry, slots, the chain-head
+// hand-off and the carried finalize -- is the same code for both.
+//
 // FUSE (one GPU; AHIP_SPMV_FUSE=0 turns it off): the chain-head combine
 // y = lo + hi happens here instead of in k_ssell_combine.  Each chain's head
 // rows pair two workgroups (the previous chain's, whose last spill is lo, and
-// this chain's, whose first superblock's head rows are hi); both store their
-// part with sc1 stores, wait for them, and add to the pair's counter; the one
-// whose add returns 1 arrived second and combines, reading both parts with sc1
-// loads -- MI355X_MICROARCH.md's hand-off row for one workgroup a CU (this
-// kernel's occupancy): no fence, no waiting, so no workgroup ever blocks on
-// another.  The deferred finalize of the step (fa, kernels.hip) then runs in
-// workgroup 0 over its spent x window.
-template <int U, bool NT, bool YNT = false, bool FUSE = false>
+// this chain's, whose first superblock's head rows are hi); both publish their
+// part and add to the pair's counter; the one whose add returns 1 arrived
+// second and combines.  No workgroup ever waits on another.  Two orderings
+// (handoff_store / handoff_arrive / handoff_load below):
+//  * FUSE = 1 (measured form, MI355X_MICROARCH.md's hand-off row for one
+//    workgroup a CU): agent-scope (sc1) slot stores drained by a vmcnt(0)
+//    wait, a relaxed counter add, agent-scope (sc1) slot loads;
+//  * FUSE = 2 (the memory model's form): plain slot stores, the workgroup
+//    barrier, ONE acq_rel agent-scope counter add (release: the barrier-ordered
+//    stores of every wave; acquire: the partner's), the barrier, plain loads --
+//    the idiom of a grid barrier.  AHIP_HANDOFF=2 selects it (A/B).
+// The deferred finalize of the step (fa, kernels.hip) then runs in workgroup 0
+// over its spent x window.
+template <int FUSE>
+__device__ __forceinline__ void handoff_store(double* p, double v) {
+    if constexpr (FUSE == 1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <int FUSE>
+__device__ __forceinline__ double handoff_load(const double* p) {
+    if constexpr (FUSE == 1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <int FUSE>
+__device__ __forceinline__ int handoff_arrive(int* p) {
+    if constexpr (FUSE == 1) return __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_fetch_add(p, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int U, bool NT, bool YNT = false, int FUSE = 0, bool DET = false, int MAXQ = 1>
 __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
     const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
@@ -148,10 +194,13 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
     const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
     const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
     double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff, int chain,
-    int64_t nsb, int* __restrict__ pair, FinArgs fa) {
+    int64_t nsb, int* __restrict__ pair, FinArgs fa, double amax, int bits) {
+    // the y window: fp64 sums, or (DET) two's-complement fixed-point sums
+    using Word = std::conditional_t<DET, unsigned long long, double>;
     __shared__ double xw[kSymWin];
-    __shared__ double yw[kSymWin];
+    __shared__ Word yw[kSymWin];
     constexpr int NW = kSymThreads / 64;
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
     const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
@@ -183,6 +232,16 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
             cur_s = s;
         }
     }
+    // DET: the fixed-point scale 2^(B-E) (inv) and its inverse (sc)
+    [[maybe_unused]] unsigned long long* xmax = nullptr;  // bits of the running max |x|
+    [[maybe_unused]] int ea = 0, E = INT_MIN;
+    [[maybe_unused]] double inv = 1.0, sc = 0.0;
+    if constexpr (DET) {
+        xmax = reinterpret_cast<unsigned long long*>(&yw[kSymWin - 1]);
+        (void)frexp(amax, &ea);  // amax < 2^ea
+        if (t == 0) *xmax = 0ull;
+        __syncthreads();  // before any wave's first atomicMax (LDS holds the last launch's words)
+    }
     int R_prev = 0, span_prev = 0;
     for (int64_t b = b0; b < b1; ++b) {
         const int64_t r0 = sb_r0[b];
@@ -200,19 +259,55 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
             }
             __syncthreads();  // the staging below overwrites the shift's source range
         }
-        for (int i = carry + t; i < span; i += kSymThreads) {
-            xw[i] = x[coff + r0 + i];
-            yw[i] = 0.0;
+        if constexpr (!DET) {
+            for (int i = carry + t; i < span; i += kSymThreads) {
+                xw[i] = x[coff + r0 + i];
+                yw[i] = 0.0;
+            }
+            __syncthreads();
+        } else {
+            // stage the new columns; the max over their |x| (as bit patterns, so a
+            // NaN wins and reaches every output of the chain) joins the running max
+            unsigned long long mb = 0;
+            for (int i = carry + t; i < span; i += kSymThreads) {
+                const double v = x[coff + r0 + i];
+                xw[i] = v;
+                yw[i] = 0;
+                mb = max(mb, (unsigned long long)__double_as_longlong(fabs(v)));
+            }
+            for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned long long)__shfl_xor(mb, o, 64));
+            if (lane == 0) atomicMax(xmax, mb);
+            __syncthreads();
+            const double X = __longlong_as_double((long long)*xmax);
+            int ex = 0;
+            (void)frexp(X, &ex);  // X < 2^ex
+            // (floor: 2^(B-E) <= 2^1000; with 2^-900 <= amax <= 2^900, the
+            // plan's condition, x_i 2^(B-E) then stays finite and every |q| < 2^B)
+            const int En = max(ea + ex, bits - 1000);
+            if (En > E) {  // uniform: X came from LDS after the barrier
+                if (carry > 0) {  // the carried sums were scaled by 2^(B-E): rescale
+                    const int d = min(En - E, 63);
+                    for (int i = t; i < carry; i += kSymThreads)
+                        yw[i] = (unsigned long long)((long long)yw[i] >> d);
+                    __syncthreads();
+                }
+                E = En;
+                inv = ldexp(1.0, bits - E);
+                sc = ldexp(1.0, E - bits);
+            }
+            if (!(X <= DBL_MAX)) sc = __longlong_as_double(0x7ff8000000000000ll);  // NaN / inf in x
         }
-        __syncthreads();
-        for (int64_t s = sb_slice0[b] + wave; s < s1; s += NW) {
+        [[maybe_unused]] double accq[MAXQ];
+        [[maybe_unused]] uint32_t rlq[(MAXQ + 1) / 2];  // window rows, two 16-bit halves (0xffff: padding)
+        int nq = 0;
+        for (int64_t s = sb_slice0[b] + wave; s < s1; s += NW, ++nq) {
             int64_t base;
             int w;
             geom(s, base, w);
             if (cur_s != s) load(cur, base, w, 0);
             const int row = srow[s * 64 + lane];
             const int rl = row >= 0 ? row - (int)r0 : 0;
-            const double xi = xw[rl];
+            const double xi = DET ? xw[rl] * inv : xw[rl];  // (DET: exact, a power-of-two scale)
             // this wave's next slice: in this superblock, else its first in the next one
             int64_t sn = s + NW;
             if (sn >= s1) sn = b + 1 < b1 ? sb_slice0[b + 1] + wave : -1;
@@ -230,25 +325,59 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
                     const int c = cur.c[u];
                     if (c >= 0) {
                         acc += cur.v[u] * xw[c];
-                        if (c != rl) atomicAdd(&yw[c], cur.v[u] * xi);
+                        if (c != rl) {
+                            if constexpr (DET) {
+                                const double f = fma(cur.v[u], xi, kMagic);
+                                atomicAdd(&yw[c], (unsigned long long)__double_as_longlong(f) -
+                                                      (unsigned long long)__double_as_longlong(kMagic));
+                            } else {
+                                atomicAdd(&yw[c], cur.v[u] * xi);
+                            }
+                        }
                     }
                 }
                 cur = nxt;
                 k += U;
             } while (k < w);
             cur_s = sn;
-            if (row >= 0) atomicAdd(&yw[rl], acc);
+            if constexpr (DET) {
+                const uint32_t h = row >= 0 ? (uint32_t)rl : 0xffffu;
+#pragma unroll
+                for (int u = 0; u < MAXQ; ++u)
+                    if (u == nq) {
+                        accq[u] = acc;
+                        if (u & 1) rlq[u >> 1] = (rlq[u >> 1] & 0xffffu) | (h << 16);
+                        else rlq[u >> 1] = h;
+                    }
+            } else {
+                if (row >= 0) atomicAdd(&yw[rl], acc);
+            }
         }
-        __syncthreads();
+        __syncthreads();  // (DET: x of the window spent, every integer sum complete)
+        if constexpr (DET) {
+#pragma unroll
+            for (int u = 0; u < MAXQ; ++u) {
+                const uint32_t h = (u & 1) ? rlq[u >> 1] >> 16 : rlq[u >> 1] & 0xffffu;
+                if (u < nq && h != 0xffffu) xw[h] = accq[u];
+            }
+            __syncthreads();
+        }
+        // the window's word i as y: the row sum (+ the transposed terms)
+        auto yrow = [&](int i) {
+            if constexpr (DET) return xw[i] + (double)(long long)yw[i] * sc;
+            else return yw[i];
+        };
+        auto yspill = [&](int i) {
+            if constexpr (DET) return (double)(long long)yw[i] * sc;
+            else return yw[i];
+        };
         // head rows meet another chain's spill through the slots; the rest are final
         const int head = b == b0 ? sb_pre[b] : 0;
         const int64_t off = sb_off[b];
         for (int i = t; i < R; i += kSymThreads) {
-            const double v = yw[i];
+            const double v = yrow(i);
             if (i < head) {
-                if constexpr (FUSE) __hip_atomic_store(slot_hi + off + i, v, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                else slot_hi[off + i] = v;
+                handoff_store<FUSE>(slot_hi + off + i, v);
             } else if constexpr (YNT) {
                 __builtin_nontemporal_store(v, y + r0 + i);
             } else {
@@ -257,35 +386,30 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
         }
         if (b == b1 - 1) {  // the chain's last spill leaves through a slot
             const int64_t offn = sb_off[b + 1];
-            for (int i = R + t; i < span; i += kSymThreads) {
-                if constexpr (FUSE) __hip_atomic_store(slot_lo + offn + (i - R), yw[i], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                else slot_lo[offn + (i - R)] = yw[i];
-            }
+            for (int i = R + t; i < span; i += kSymThreads)
+                handoff_store<FUSE>(slot_lo + offn + (i - R), yspill(i));
         }
         R_prev = R;
         span_prev = span;
     }
-    if constexpr (FUSE) {
+    if constexpr (FUSE != 0) {
         const int64_t nch = gridDim.x;
         int* flag = reinterpret_cast<int*>(xw);  // the x window is spent
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slot stores
+        if constexpr (FUSE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slot stores
         __syncthreads();
         if (t == 0) {
-            flag[0] = ch > 0 ? __hip_atomic_fetch_add(pair + ch, 1, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) : 0;
-            flag[1] = ch + 1 < nch ? __hip_atomic_fetch_add(pair + ch + 1, 1, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT) : 0;
+            flag[0] = ch > 0 ? handoff_arrive<FUSE>(pair + ch) : 0;
+            flag[1] = ch + 1 < nch ? handoff_arrive<FUSE>(pair + ch + 1) : 0;
         }
-        // Ordering (MI355X_MICROARCH.md, the measured sc1 hand-off row for one
-        // workgroup per CU, this kernel's occupancy): every slot store above is
-        // an agent-scope (sc1) store drained by the vmcnt(0) wait before the
-        // barrier, ONE lane adds to the pair's unsharded counter, and the
-        // second arriver -- told by the value its add returned -- reads both
-        // slots with agent-scope (sc1) loads after the barrier below.  The
-        // barriers also keep the compiler from moving the slot accesses across
-        // the counter (they are workgroup fences); the word-by-word check under
-        // uneven load is tests/test_gpu_symspmv_handoff.py.
+        // FUSE = 1 (the measured sc1 hand-off for one workgroup per CU, this
+        // kernel's occupancy): every slot store above is an agent-scope (sc1)
+        // store drained by the vmcnt(0) wait before the barrier, ONE lane adds
+        // to the pair's unsharded counter, and the second arriver -- told by the
+        // value its add returned -- reads both slots with agent-scope (sc1)
+        // loads after the barrier below.  The barriers also keep the compiler
+        // from moving the slot accesses across the counter (they are workgroup
+        // fences).  FUSE = 2: the counter add is acq_rel at agent scope.  The
+        // word-by-word check under uneven load is tests/test_gpu_symspmv_handoff.py.
         __syncthreads();
         for (int side = 0; side < 2; ++side) {
             if (flag[side] != 1) continue;  // first of its pair: the partner combines
@@ -294,238 +418,11 @@ __global__ __launch_bounds__(kSymThreads) void k_csr_ssell(
             const int pre = sb_pre[bh];
             const int64_t off = sb_off[bh], rh = sb_r0[bh];
             for (int i = t; i < pre; i += kSymThreads)
-                y[rh + i] = __hip_atomic_load(slot_lo + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                            __hip_atomic_load(slot_hi + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                y[rh + i] = handoff_load<FUSE>(slot_lo + off + i) + handoff_load<FUSE>(slot_hi + off + i);
             if (t == 0) pair[c] = 0;  // both parties are done with it (next launch: kernel order)
         }
         if (fa.active && blockIdx.x == 0) {
             __syncthreads();  // flag[] read by every wave before the window is reused
-            finalize_block<false>(fa, reinterpret_cast<FinLds*>(xw), nullptr);
-        }
-    }
-}
-
-// Deterministic mode's symmetric SpMV (arpack_hip_set_deterministic): the walk
-// of k_csr_ssell with every sum in an order no schedule can change.  The row
-// part stays one lane's sequential sum.  The transposed terms -- whose LDS
-// atomic adds meet in wave-schedule order -- become 64-bit FIXED-POINT
-// integers, and integer addition is exact, so their sum is the same in any
-// order:
-//   q = rint(a_ij x_i 2^(B-E))      (one fma onto 1.5 * 2^52: the low mantissa
-//                                    bits of the result are q, |q| < 2^B <= 2^51)
-//   y_j = (row sum) + (double)(sum of the q) * 2^(E-B)
-// with 2^E >= amax * (largest |x| the chain has staged so far): a running
-// maximum, so E only grows, and a partial sum carried into the next window is
-// rescaled by an arithmetic shift when it does; B = min(51, 62 - bits(L)) for
-// rows that receive at most L transposed terms, so no sum can overflow.  Each
-// term is rounded to 2^(E-B) -- at most 2^-51 of the window's largest product
-// (a double partial sum of such terms rounds each add to 2^-53 of its value).
-// The row sums wait in registers (at most MAXQ slices a wave) until the
-// window's x is spent, then meet the integer sums in the x window.  One LDS
-// word past every window (span <= kSymWin - 1) holds the running maximum.  The
-// chain-head combine, the slots and the deferred finalize are k_csr_ssell's.
-template <int U, bool NT, bool FUSE, int MAXQ>
-__global__ __launch_bounds__(kSymThreads) void k_csr_ssell_det(
-    const int64_t* __restrict__ sb_r0, const int32_t* __restrict__ sb_span,
-    const int32_t* __restrict__ sb_pre, const int64_t* __restrict__ sb_off,
-    const int64_t* __restrict__ sb_slice0, const int64_t* __restrict__ sptr,
-    const int32_t* __restrict__ srow, const uint16_t* __restrict__ scolw,
-    const double* __restrict__ sval, const double* __restrict__ x, double* __restrict__ y,
-    double* __restrict__ slot_lo, double* __restrict__ slot_hi, int64_t coff, int chain,
-    int64_t nsb, double amax, int bits, int* __restrict__ pair, FinArgs fa) {
-    __shared__ double xw[kSymWin];
-    __shared__ unsigned long long tw[kSymWin];  // two's-complement fixed-point sums
-    constexpr int NW = kSymThreads / 64;
-    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
-    const unsigned long long kMagicBits = (unsigned long long)__double_as_longlong(kMagic);
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t ch = xcd_block(blockIdx.x, gridDim.x);
-    const int64_t b0 = ch * chain, b1 = min(b0 + (int64_t)chain, nsb);
-    unsigned long long* xmax = &tw[kSymWin - 1];  // bits of the running max |x|
-    int ea = 0;
-    (void)frexp(amax, &ea);  // amax < 2^ea
-    struct Chunk {
-        double v[U];
-        int c[U];
-    };
-    auto load = [&](Chunk& c, int64_t base, int w, int k0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool in = k0 + u < w;
-            c.v[u] = in ? ldg<double, NT>(sval + base + (int64_t)(k0 + u) * 64 + lane) : 0.0;
-            c.c[u] = in ? (int)ldg<uint16_t, NT>(scolw + base + (int64_t)(k0 + u) * 64 + lane) : -1;
-        }
-    };
-    auto geom = [&](int64_t sl, int64_t& base, int& w) {
-        base = sptr[sl];
-        w = (int)((sptr[sl + 1] - base) >> 6);
-    };
-    Chunk cur, nxt;
-    int64_t cur_s = -1;
-    {
-        const int64_t s = sb_slice0[b0] + wave;
-        if (s < sb_slice0[b0 + 1]) {
-            int64_t base;
-            int w;
-            geom(s, base, w);
-            load(cur, base, w, 0);
-            cur_s = s;
-        }
-    }
-    if (t == 0) *xmax = 0ull;
-    __syncthreads();  // before any wave's first atomicMax (LDS holds the last launch's words)
-    int E = INT_MIN;
-    double inv = 0.0, sc = 0.0;
-    int R_prev = 0, span_prev = 0;
-    for (int64_t b = b0; b < b1; ++b) {
-        const int64_t r0 = sb_r0[b];
-        const int R = (int)(sb_r0[b + 1] - r0);
-        const int span = sb_span[b];
-        const int64_t s1 = sb_slice0[b + 1];
-        int carry = 0;
-        if (b > b0) {
-            carry = span_prev - R_prev;
-            __syncthreads();
-            for (int i = t; i < carry; i += kSymThreads) {
-                xw[i] = xw[R_prev + i];
-                tw[i] = tw[R_prev + i];
-            }
-            __syncthreads();
-        }
-        // stage the new columns; the max over their |x| (as bit patterns, so a
-        // NaN wins and reaches every output of the chain) joins the running max
-        unsigned long long mb = 0;
-        for (int i = carry + t; i < span; i += kSymThreads) {
-            const double v = x[coff + r0 + i];
-            xw[i] = v;
-            tw[i] = 0;
-            mb = max(mb, (unsigned long long)__double_as_longlong(fabs(v)));
-        }
-        for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned long long)__shfl_xor(mb, o, 64));
-        if (lane == 0) atomicMax(xmax, mb);
-        __syncthreads();
-        {
-            const double X = __longlong_as_double((long long)*xmax);
-            int ex = 0;
-            (void)frexp(X, &ex);  // X < 2^ex
-            // (floor: 2^(B-E) <= 2^1000; with 2^-900 <= amax <= 2^900, the
-            // plan's condition, x_i 2^(B-E) then stays finite and every |q| < 2^B)
-            const int En = max(ea + ex, bits - 1000);
-            if (En > E) {  // uniform: X came from LDS after the barrier
-                if (carry > 0) {  // the carried sums were scaled by 2^(B-E): rescale
-                    const int d = min(En - E, 63);
-                    for (int i = t; i < carry; i += kSymThreads)
-                        tw[i] = (unsigned long long)((long long)tw[i] >> d);
-                    __syncthreads();
-                }
-                E = En;
-                inv = ldexp(1.0, bits - E);
-                sc = ldexp(1.0, E - bits);
-            }
-            if (!(X <= DBL_MAX)) sc = __longlong_as_double(0x7ff8000000000000ll);  // NaN / inf in x
-        }
-        double accq[MAXQ];
-        uint32_t rlq[(MAXQ + 1) / 2];  // window rows, two 16-bit halves (0xffff: padding lane)
-        int nq = 0;
-        for (int64_t s = sb_slice0[b] + wave; s < s1; s += NW, ++nq) {
-            int64_t base;
-            int w;
-            geom(s, base, w);
-            if (cur_s != s) load(cur, base, w, 0);
-            const int row = srow[s * 64 + lane];
-            const int rl = row >= 0 ? row - (int)r0 : 0;
-            const double xs = xw[rl] * inv;  // exact: a power-of-two scale
-            int64_t sn = s + NW;
-            if (sn >= s1) sn = b + 1 < b1 ? sb_slice0[b + 1] + wave : -1;
-            if (sn >= 0 && b + 1 < b1 && sn >= s1 && sn >= sb_slice0[b + 2]) sn = -1;
-            int64_t nbase = 0;
-            int nw = 0;
-            if (sn >= 0) geom(sn, nbase, nw);
-            double acc = 0.0;
-            int k = 0;
-            do {
-                if (k + U < w) load(nxt, base, w, k + U);
-                else if (sn >= 0) load(nxt, nbase, nw, 0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int c = cur.c[u];
-                    if (c >= 0) {
-                        acc += cur.v[u] * xw[c];
-                        if (c != rl) {
-                            const double f = fma(cur.v[u], xs, kMagic);
-                            atomicAdd(&tw[c], (unsigned long long)__double_as_longlong(f) - kMagicBits);
-                        }
-                    }
-                }
-                cur = nxt;
-                k += U;
-            } while (k < w);
-            cur_s = sn;
-            const uint32_t h = row >= 0 ? (uint32_t)rl : 0xffffu;
-#pragma unroll
-            for (int u = 0; u < MAXQ; ++u)
-                if (u == nq) {
-                    accq[u] = acc;
-                    if (u & 1) rlq[u >> 1] = (rlq[u >> 1] & 0xffffu) | (h << 16);
-                    else rlq[u >> 1] = h;
-                }
-        }
-        __syncthreads();  // x of the window spent, every integer sum complete
-#pragma unroll
-        for (int u = 0; u < MAXQ; ++u) {
-            const uint32_t h = (u & 1) ? rlq[u >> 1] >> 16 : rlq[u >> 1] & 0xffffu;
-            if (u < nq && h != 0xffffu) xw[h] = accq[u];
-        }
-        __syncthreads();
-        const int head = b == b0 ? sb_pre[b] : 0;
-        const int64_t off = sb_off[b];
-        for (int i = t; i < R; i += kSymThreads) {
-            const double v = xw[i] + (double)(long long)tw[i] * sc;
-            if (i < head) {
-                if constexpr (FUSE) __hip_atomic_store(slot_hi + off + i, v, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                else slot_hi[off + i] = v;
-            } else {
-                y[r0 + i] = v;
-            }
-        }
-        if (b == b1 - 1) {
-            const int64_t offn = sb_off[b + 1];
-            for (int i = R + t; i < span; i += kSymThreads) {
-                const double v = (double)(long long)tw[i] * sc;
-                if constexpr (FUSE) __hip_atomic_store(slot_lo + offn + (i - R), v, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                else slot_lo[offn + (i - R)] = v;
-            }
-        }
-        R_prev = R;
-        span_prev = span;
-    }
-    if constexpr (FUSE) {  // k_csr_ssell's hand-off, verbatim in its ordering
-        const int64_t nch = gridDim.x;
-        int* flag = reinterpret_cast<int*>(xw);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) {
-            flag[0] = ch > 0 ? __hip_atomic_fetch_add(pair + ch, 1, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) : 0;
-            flag[1] = ch + 1 < nch ? __hip_atomic_fetch_add(pair + ch + 1, 1, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT) : 0;
-        }
-        __syncthreads();
-        for (int side = 0; side < 2; ++side) {
-            if (flag[side] != 1) continue;
-            const int64_t c = ch + side;
-            const int64_t bh = c * chain;
-            const int pre = sb_pre[bh];
-            const int64_t off = sb_off[bh], rh = sb_r0[bh];
-            for (int i = t; i < pre; i += kSymThreads)
-                y[rh + i] = __hip_atomic_load(slot_lo + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                            __hip_atomic_load(slot_hi + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (t == 0) pair[c] = 0;
-        }
-        if (fa.active && blockIdx.x == 0) {
-            __syncthreads();
             finalize_block<false>(fa, reinterpret_cast<FinLds*>(xw), nullptr);
         }
     }
@@ -1071,23 +968,33 @@ static bool spmv_ynt() {
 
 // deterministic mode takes the fixed-point form where the plan allows it
 static bool sym_det(const Csr& A) { return A.ss_det && deterministic(); }
+// AHIP_HANDOFF=2: the fused chain-head hand-off in the memory model's acq_rel
+// form instead of the measured sc1 form (k_csr_ssell FUSE = 2 vs 1, A/B)
+static int handoff_form() {
+    static const int f = [] {
+        const char* e = getenv("AHIP_HANDOFF");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    return f;
+}
 // MAXQ: slices a wave walks in one superblock -- at most 10 (rows <= span <=
 // kSymWin - 1); 6 (superblocks of <= 96 slices, the NS operator's 88) keeps
 // the kernel inside 128 VGPRs without spilling
-template <bool FUSE>
+template <int FUSE>
 static void launch_det(hipStream_t s, const Csr& A, const double* x, double* y, int* pair,
                        const FinArgs& fa) {
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
-    auto* kern = A.ss_detq <= 6 ? &k_csr_ssell_det<8, true, FUSE, 6> : &k_csr_ssell_det<8, true, FUSE, 10>;
+    auto* kern = A.ss_detq <= 6 ? &k_csr_ssell<8, true, false, FUSE, true, 6>
+                                : &k_csr_ssell<8, true, false, FUSE, true, 10>;
     AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0, A.ss_sb_span, A.ss_sb_pre,
                 A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row, A.ss_colw, A.ss_val, x, y, A.ss_lo,
-                A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_amax, A.ss_bits, pair, fa);
+                A.ss_hi, A.ss_coff, chain, A.ss_nsb, pair, fa, A.ss_amax, A.ss_bits);
 }
 
 void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) {
     if (sym_det(A)) {
-        launch_det<false>(s, A, x, y, nullptr, FinArgs{});
+        launch_det<0>(s, A, x, y, nullptr, FinArgs{});
         return;
     }
     auto go = [&](auto kern) {
@@ -1096,7 +1003,7 @@ void csr_spmv_sym_main(hipStream_t s, const Csr& A, const double* x, double* y) 
         AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0,
                            A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
                            A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb,
-                           (int*)nullptr, FinArgs{});
+                           (int*)nullptr, FinArgs{}, 0.0, 0);
     };
     // measured on the NS operator (tools/spmv_sym_time.py, one process, before
     // chaining): U = 8 with non-temporal val/col loads 0.594 ms incl. the
@@ -1202,13 +1109,17 @@ void csr_spmv_sym_as(hipStream_t s, const Csr& A, const double* x, double* y, bo
     const int chain = sym_chain(A);
     const int64_t nch = (A.ss_nsb + chain - 1) / chain;
     if (sym_det(A)) {
-        launch_det<true>(s, A, x, y, A.ss_pair, fa);
+        if (handoff_form() == 2) launch_det<2>(s, A, x, y, A.ss_pair, fa);
+        else launch_det<1>(s, A, x, y, A.ss_pair, fa);
         return;
     }
-    AHIP_LAUNCH((k_csr_ssell<8, true, false, true>), dim3((unsigned)nch), dim3(kSymThreads), 0, s,
-                A.ss_sb_r0, A.ss_sb_span, A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row,
-                A.ss_colw, A.ss_val, x, y, A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_pair,
-                fa);
+    auto go = [&](auto kern) {
+        AHIP_LAUNCH(kern, dim3((unsigned)nch), dim3(kSymThreads), 0, s, A.ss_sb_r0, A.ss_sb_span,
+                    A.ss_sb_pre, A.ss_sb_off, A.ss_slice0, A.ss_ptr, A.ss_row, A.ss_colw, A.ss_val, x, y,
+                    A.ss_lo, A.ss_hi, A.ss_coff, chain, A.ss_nsb, A.ss_pair, fa, 0.0, 0);
+    };
+    if (handoff_form() == 2) go(k_csr_ssell<8, true, false, 2>);
+    else go(k_csr_ssell<8, true, false, 1>);
 }
 
 }  // namespace ahip::dev

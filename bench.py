@@ -283,7 +283,11 @@ def comm_report(prof, D, dist, rank, ms_per_step):
                             "allreduce and each halo group, in the profiled cycles (not the timed "
                             "ones); the SpMV span holds its halo group, reported apart here",
                 counts_note="allreduce_per_step and halo_per_step are launches per Lanczos step "
-                            "(restart-cycle collectives included in the average)")
+                            "(restart-cycle collectives included in the average)",
+                baseline_note="a span's time includes its two marker packets (a 1-rank line's "
+                              "halo group moves nothing and reads ~5 us a step: "
+                              "profiles/r06a_force_dist.json) -- subtract that floor when "
+                              "reading an N-rank line")
 
 
 def main():
@@ -293,9 +297,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=("ns", "lap3d"), default="ns",
                     help="ns: the north-star banded symmetric CSR (n = --rows); lap3d: BASELINE "
-                         "config 4, the 3-D 7-pt Laplacian m^3 (m = --m), row-block / z-slab "
+                         "config 4, the 3-D 7-pt Laplacian m^3 (m = --lap-m), row-block / z-slab "
                          "sharded over the ranks (PARPACK/EXAMPLES/MPI/pdsdrv1.f)")
-    ap.add_argument("--m", type=int, default=215, help="lap3d grid edge (n = m^3; 215: 9.94e6)")
+    ap.add_argument("--lap-m", dest="m", type=int, default=215,
+                    help="lap3d grid edge (n = m^3; 215: 9.94e6); not --m, which torch.distributed.run "
+                         "would take as an abbreviation of its own options")
     ap.add_argument("--rows", "--n", dest="n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=25)
     ap.add_argument("--bandwidth", type=int, default=4096)
@@ -325,7 +331,7 @@ def main():
     ap.add_argument("--deterministic", action="store_true",
                     help="deterministic mode (arpack_hip_set_deterministic): only fixed-order "
                          "SpMV forms (--storage sym: the fixed-point symmetric kernel "
-                         "k_csr_ssell_det), so every solve is bitwise reproducible")
+                         "k_csr_ssell<..., DET = true>), so every solve is bitwise reproducible")
     args = ap.parse_args()
     if args.workload == "lap3d":
         args.n = args.m ** 3
@@ -486,14 +492,14 @@ def main():
     det_mode = None
     if storage == "sym" and world == 1 and not args.no_full_storage and not args.deterministic:
         # the same K cycles in deterministic mode (the fixed-point symmetric
-        # kernel k_csr_ssell_det: bitwise reproducible solves), reported beside
+        # form of k_csr_ssell: bitwise reproducible solves), reported beside
         pkg.set_deterministic(True)
         A.set_symmetric(True)  # 0: the fixed-point form serves this operator
         if A.last_rc == 0 and A.symmetric:
             s_d, ido_d, el_d, nopx_d, _ = timed_run()
             det_mode = dict(value=args.steps / el_d, ms_per_step=1e3 * el_d / args.steps,
                             lanczos_steps_per_s=nopx_d / el_d, bitwise_reproducible=True,
-                            kernel="k_csr_ssell_det (64-bit fixed-point transposed terms)")
+                            kernel="k_csr_ssell, DET form (64-bit fixed-point transposed terms)")
             del s_d
         else:
             det_mode = dict(value=None, note="operator outside the fixed-point form "
@@ -610,7 +616,10 @@ def main():
 
     # counter traffic from a committed PMC summary of THIS workload (same
     # operator, size, storage and mode), single GPU only
-    families = ({"k_csr_ssell_det"} if args.deterministic else {"k_csr_ssell"}) if storage == "sym" \
+    # (one symmetric kernel, k_csr_ssell<..., DET, ...>, since round 6; the
+    # deterministic form's former name is kept for older summaries -- the
+    # workload's "deterministic" key tells the two modes apart)
+    families = {"k_csr_ssell", "k_csr_ssell_det"} if storage == "sym" \
         else {"k_csr_sell", "k_csr_sell_fin"}
     wl = dict(workload=args.workload, n=n, nnz=nnz, storage=storage,
               deterministic=bool(args.deterministic))
@@ -665,7 +674,7 @@ def main():
                                 "slices over LDS x/y windows, LDS atomic transposed terms, 16-bit "
                                 "window-relative cols; on one GPU the chain-head combine and the "
                                 "step's deferred finalize run inside it, else k_ssell_combine "
-                                "follows)" + ("; deterministic mode: k_csr_ssell_det, the "
+                                "follows)" + ("; deterministic mode: the same walk with the "
                                               "transposed terms as 64-bit fixed-point LDS sums"
                                               if args.deterministic else "")) if storage == "sym"
                                else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "

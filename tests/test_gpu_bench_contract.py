@@ -66,7 +66,7 @@ def test_two_ranks_one_json_line():
     _comm_profile_ok(d, 2)
 
 
-LAP = ["--workload", "lap3d", "--m", "100", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+LAP = ["--workload", "lap3d", "--lap-m", "100", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
 
 
 def test_lap3d_workload_line():
