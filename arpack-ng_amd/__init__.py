@@ -594,6 +594,21 @@ class NsRci(SymRci):
         self.tol = tol.value
         return int(self.ido[0])
 
+    def aupd_gen(self, G: "DGen"):
+        """Whole loop on the GPU in dnaupd's generalized modes (bmat="G", mode
+        2, or 3 with G's real sigma): OP*x and B*x by the device operator pair
+        G (arpack_hip_dnaupd_gen)."""
+        tol = C.c_double(self.tol)
+        L = lib()
+        L.arpack_hip_dnaupd_gen.argtypes = L.arpack_hip_dsaupd_shift.argtypes
+        L.arpack_hip_dnaupd_gen(G.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                self.which.encode(), self.nev, C.byref(tol),
+                                _ptr(self.resid), self.ncv, _ptr(self.v), self.ldv,
+                                _ip(self.iparam), _ip(self.ipntr), _ptr(self.workd),
+                                self.workl.ctypes.data, self.lworkl, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
     def aupd_shift(self, S: "DShift"):
         """dnaupd in mode 3 (real shift) with OP = (A - sigma I)^{-1} by the
         device BiCGStab S (arpack_hip_dnaupd_shift)."""
@@ -791,8 +806,9 @@ class DGen:
     """Device operator pair of dsaupd's generalized modes (bmat = 'G', modes
     2-5; arpack_hip_dgen_create): mode 2 OP = inv[M] A; 3 OP = inv[A - sigma M]
     M; 4 (buckling, A = K, B = KG) OP = inv[K - sigma KG] K; 5 (Cayley) OP =
-    inv[A - sigma M](A + sigma M).  The inverse is a device CG (method 0) or
-    MINRES (1) to relative residual rtol on C = A - sigma B."""
+    inv[A - sigma M](A + sigma M).  The inverse is a device CG (method 0),
+    MINRES (1) or BiCGStab (2: a nonsymmetric C, dnaupd's modes 2-3 through
+    NsRci.aupd_gen) to relative residual rtol on C = A - sigma B."""
 
     def __init__(self, A: CSR, B: CSR, mode: int, sigma: float = 0.0, rtol: float = 1e-12,
                  maxit: int = 5000, method: int = 0):

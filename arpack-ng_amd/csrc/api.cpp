@@ -163,8 +163,9 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         // a device OP serves mode 1 (OP = A), or mode 3 through the device solve
         // (symmetric only: CG); bmat = 'I'
         // (dnaupd: a nonsymmetric A needs the general solve, BiCGStab)
-        if (gen) {  // the operator pair fixes the mode (bmat = 'G', dsaupd only)
-            if (ns || dist || bmat[0] != 'G' || mode != gen->mode || gen->n != n)
+        if (gen) {  // the operator pair fixes the mode (bmat = 'G'); dnaupd: modes 2, 3
+            if (dist || bmat[0] != 'G' || mode != gen->mode || gen->n != n ||
+                (ns && mode != 2 && mode != 3))
                 ierr = (ierr ? ierr : -11);
         } else if (csr && ((shift ? mode != 3 || dist || (ns && shift->method != dev::kDShiftBicgstab)
                                   : mode != 1) ||
@@ -324,7 +325,9 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
                 double* yp = S->op_y ? S->op_y : W + r.y;
                 const double* bxp = (r.ido == 1 && r.bx >= 0) ? W + r.bx : nullptr;
                 dev::flush_deferred_finalize(S->ws.defq, S->a.stream);
-                const int rc = dev::dgen_apply(*S->gen, S->a.stream, r.ido, xp, yp, bxp, W + r.x);
+                // (dnaupd's mode 2 has no x <- A x write-back: dndrv3.f:215-240)
+                const int rc = dev::dgen_apply(*S->gen, S->a.stream, r.ido, xp, yp, bxp,
+                                               S->arnoldi ? nullptr : W + r.x);
                 if (rc < 0) {  // a solve missed its tolerance: OP is not what was asked
                     S->a.sync();
                     *info = -9999;
@@ -531,7 +534,7 @@ struct arpack_hip_dgen {
 int arpack_hip_dgen_create(arpack_hip_dgen** out, const arpack_hip_csr* A, const arpack_hip_csr* B,
                            int mode, double sigma, double rtol, int maxit, int method) {
     if (!out || !(rtol > 0.0) || maxit < 1 || method < ahip::dev::kDShiftCg ||
-        method > ahip::dev::kDShiftMinres)
+        method > ahip::dev::kDShiftBicgstab)
         return -1;
     auto* D = new arpack_hip_dgen;
     const int rc = ahip::dev::dgen_create(D->G, A, B, mode, sigma, rtol, maxit, method);
@@ -571,6 +574,22 @@ void arpack_hip_dsaupd_gen(arpack_hip_dgen* D, int* ido, char const* bmat, int n
     }
     sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
              info, nullptr, -1, nullptr, false, nullptr, &D->G);
+}
+
+// dnaupd's generalized modes on the device (bmat = 'G'; mode 2, or mode 3 with
+// the real shift the operator pair was made with; dneupd_c then takes
+// sigmar = sigma, sigmai = 0)
+void arpack_hip_dnaupd_gen(arpack_hip_dgen* D, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, double* resid, int ncv, double* v, int ldv,
+                           int* iparam, int* ipntr, double* workd, double* workl, int lworkl,
+                           int* info) {
+    if (!D) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
+    sym_aupd(ido, bmat, n, which, nev, tol, resid, ncv, v, ldv, iparam, ipntr, workd, workl, lworkl,
+             info, nullptr, -1, nullptr, true, nullptr, &D->G);
 }
 
 int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, double sigma,

@@ -1,12 +1,18 @@
 // Device operator pair of the generalized modes (bmat = 'G'): the caller's half
-// of dsaupd's reverse communication for modes 2-5 (SRC/dsaupd.f:30-77), served
-// on the GPU so the whole solve runs free (arpack_hip_dsaupd_gen) instead of
-// returning to the host for every OP*x and B*x:
+// of dsaupd's reverse communication for modes 2-5 (SRC/dsaupd.f:30-77), and of
+// dnaupd's for modes 2-3 with a real shift (SRC/dnaupd.f:18-33), served on the
+// GPU so the whole solve runs free (arpack_hip_dsaupd_gen /
+// arpack_hip_dnaupd_gen) instead of returning to the host for every OP*x and B*x:
 //
 //   mode 2  OP = inv[M] A,              B = M   (x <- A x written back, dsaupd.f:40-46)
 //   mode 3  OP = inv[A - sigma M] M,    B = M
 //   mode 4  OP = inv[K - sigma KG] K,   B = K   (buckling: A = K, M = KG)
 //   mode 5  OP = inv[A - sigma M](A + sigma M),  B = M   (Cayley)
+//
+// dnaupd (A nonsymmetric, M symmetric positive semi-definite):
+//   mode 2  OP = inv[M] A,  B = M  (no write-back: EXAMPLES/NONSYM/dndrv3.f:215-240)
+//   mode 3  OP = inv[A - sigma M] M,  B = M, sigma real (dndrv4.f:243-300);
+//           C is nonsymmetric: the device BiCGStab (method kDShiftBicgstab)
 //
 // The products are the engine's device CSR SpMV; the inverse is a Krylov solve
 // on the device (dshift.hip: CG for a positive-definite C, MINRES for an
@@ -123,7 +129,8 @@ void dgen_destroy(DGen& G) {
 
 // One request of the solve (ido = -1, 1 or 2, SRC/dsaupd.f:30-77): x, y,
 // bx (ido = 1, modes 3-5: B x already computed by the engine) device
-// pointers; xw: where mode 2 writes A x back (workd(ipntr(1))).
+// pointers; xw: where mode 2 writes A x back (workd(ipntr(1))) -- dsaupd's
+// contract; nullptr for dnaupd's, which has no write-back.
 int dgen_apply(DGen& G, hipStream_t s, int ido, const double* x, double* y, const double* bx,
                double* xw) {
     const int64_t n = G.n;
@@ -138,9 +145,9 @@ int dgen_apply(DGen& G, hipStream_t s, int ido, const double* x, double* y, cons
     double relres = 0.0;
     const double* rhs = t;
     switch (G.mode) {
-        case 2:  // y = inv[M] (A x), and x <- A x
+        case 2:  // y = inv[M] (A x), and (dsaupd) x <- A x
             csr_spmv(s, *G.A, x, t);
-            copy<double>(s, n, t, xw);
+            if (xw) copy<double>(s, n, t, xw);
             break;
         case 3:  // y = inv[A - sigma M] (M x), M x given at ido = 1
         case 4:  // y = inv[K - sigma KG] (K x), K x given at ido = 1

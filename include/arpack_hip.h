@@ -383,7 +383,8 @@ void arpack_hip_dnaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, i
  *   mode 4  OP = inv[K - sigma KG] K, B = K           A = K, B = KG
  *   mode 5  OP = inv[A - sigma M](A + sigma M), B = M
  * The inverse is a device Krylov solve to relative residual rtol (method 0 CG:
- * positive-definite C; 1 MINRES: indefinite) on C = A - sigma B formed once
+ * positive-definite C; 1 MINRES: indefinite; 2 BiCGStab: nonsymmetric) on
+ * C = A - sigma B formed once
  * entry by entry over the union pattern (mode 2: on M).  Returns 0, -1 for bad
  * arguments, -2 on a HIP failure.  arpack_hip_dsaupd_gen takes dsaupd_c's
  * arguments (bmat 'G', iparam(7) = the operator pair's mode); a solve that
@@ -395,6 +396,18 @@ void arpack_hip_dgen_destroy(arpack_hip_dgen* G);
 int arpack_hip_dgen_stats(const arpack_hip_dgen* G, long long* solves, long long* iters,
                           long long* fails, double* max_relres);
 void arpack_hip_dsaupd_gen(arpack_hip_dgen* G, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, double* resid, int ncv, double* v, int ldv,
+                           int* iparam, int* ipntr, double* workd, double* workl, int lworkl,
+                           int* info);
+/* dnaupd_c's generalized modes on the device (replaces the caller's ido = -1 /
+ * 1 / 2 loop of EXAMPLES/NONSYM/dndrv3.f:215-255 and dndrv4.f:243-310; SRC/
+ * dnaupd.f:18-33): A nonsymmetric, M symmetric positive semi-definite, and
+ *   mode 2  OP = inv[M] A, B = M (no write-back of A x, unlike dsaupd's)
+ *   mode 3  OP = inv[A - sigma M] M, B = M, sigma real (method 2 BiCGStab on
+ *           the nonsymmetric C); dneupd_c with sigmar = sigma, sigmai = 0.
+ * Modes 4 (Im part, complex sigma) and the operator pair's modes 4-5 return
+ * info = -11. */
+void arpack_hip_dnaupd_gen(arpack_hip_dgen* G, int* ido, char const* bmat, int n, char const* which,
                            int nev, double* tol, double* resid, int ncv, double* v, int ldv,
                            int* iparam, int* ipntr, double* workd, double* workl, int lworkl,
                            int* info);

@@ -1,4 +1,5 @@
-"""GPU: dsaupd's generalized modes (bmat = 'G', modes 2-5) free-running on the
+"""GPU: dsaupd's generalized modes (bmat = 'G', modes 2-5) and dnaupd's
+(modes 2-3, real shift; VERDICT r05 missing #4) free-running on the
 device (VERDICT r04 missing #3): OP*x and B*x served by the device operator
 pair (arpack_hip_dsaupd_gen: device CSR products, the inverse by the device CG
 or MINRES on C = A - sigma M), against the reference fixtures m3-m6 the
@@ -56,6 +57,55 @@ def test_dsaupd_generalized_on_device(pkg, golden, name):
     for k in range(nconv):
         r = A @ z[:, k] - d[k] * (Mm @ z[:, k])
         assert np.linalg.norm(r) / (anorm * np.linalg.norm(z[:, k])) <= 1e-8
+
+
+# dnaupd (EXAMPLES/NONSYM/dndrv3.f mode 2, dndrv4.f mode 3 with a real shift):
+# A the 1-D convection-diffusion operator, M the FEM mass matrix (SPD).  Mode 2
+# solves with M (CG); mode 3's C = A - sigma M is nonsymmetric (BiCGStab)
+NS_CASES = {"m8_ns_gen": 0, "m9_ns_gen_si": 2}
+
+
+@pytest.mark.parametrize("name", sorted(NS_CASES))
+def test_dnaupd_generalized_on_device(pkg, golden, name):
+    """Free-running dnaupd with bmat = 'G' (arpack_hip_dnaupd_gen): the
+    reference's info, nconv, restart cycles and OP*x / B*x counts; every
+    eigenvalue of the reference's dneupd within 1e-9 (relative to the largest)
+    of one of ours; generalized residuals of the Ritz vectors."""
+    g = golden(name)
+    mode, n, sigma = int(g["mode"]), int(g["n"]), float(g["sigma"])
+    A, Mm = modes.convdiff1d(n, 10.0)
+    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), mode, sigma, rtol=1e-13, maxit=50 * n,
+                 method=NS_CASES[name])
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat="G",
+                  mode=mode, mxiter=300, v0=g["v0"], device=True)
+    assert s.aupd_gen(G) == 99
+    st = G.stats()
+    assert st["fails"] == 0 and st["solves"] > 0, st
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    assert int(s.iparam[2]) == int(g["iparam"][2]), (int(s.iparam[2]), int(g["iparam"][2]))
+    assert (int(s.iparam[8]), int(s.iparam[9])) == (int(g["nopx"]), int(g["nbx"]))
+    dr, di, z, nconv = s.eupd(sigmar=sigma)
+    lam, ref = dr[:nconv] + 1j * di[:nconv], g["dr"] + 1j * g["di"]
+    for x in ref:
+        assert np.abs(lam - x).min() <= 1e-9 * np.abs(ref).max(), (x, lam)
+    z = z.numpy() if hasattr(z, "numpy") else z
+    z = z.reshape(-1, n)[:nconv].T
+    anorm = abs(A).sum(axis=0).max()
+    for k in range(nconv):
+        if di[k] == 0.0:  # real eigenpairs (complex pairs: real/imaginary parts in 2 columns)
+            r = A @ z[:, k] - dr[k] * (Mm @ z[:, k])
+            assert np.linalg.norm(r) / (anorm * np.linalg.norm(z[:, k])) <= 1e-8
+
+
+def test_dnaupd_gen_rejects_symmetric_only_modes(pkg):
+    """dnaupd takes the operator pair in modes 2 and 3 only: a pair made for
+    the buckling (4) or Cayley (5) transformation gives info = -11."""
+    A, Mm = modes.convdiff1d(50, 10.0)
+    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), 5, 1.0, method=2)
+    s = pkg.NsRci(50, 4, 12, "LM", 1e-10, bmat="G", mode=5, device=True, v0=np.ones(50))
+    assert s.aupd_gen(G) == 99
+    assert int(s.info[0]) == -11
 
 
 def test_dgen_rejects_mismatch(pkg):
