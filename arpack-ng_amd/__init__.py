@@ -683,6 +683,15 @@ class ZCSR:
             raise RuntimeError("zcsr_create failed")
         return cls(h.value)
 
+    def tile_info(self):
+        """(form, stored): the product's layout (arpack_hip_zcsr_tile_info: 0
+        CSR, 1 slice CSRs, 2 sorted tiles, 3 packed tiles) and entries streamed."""
+        L = lib()
+        L.arpack_hip_zcsr_tile_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int64)]
+        f, st = C.c_int(), C.c_int64()
+        L.arpack_hip_zcsr_tile_info(self.h, C.byref(f), C.byref(st))
+        return f.value, st.value
+
     @classmethod
     def random(cls, n, per_row=100, seed=5, dshift=100.0):
         """BASELINE config 5 operator generated in HBM (oracle twin: matrices.zrandom)."""

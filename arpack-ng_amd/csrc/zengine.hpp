@@ -72,11 +72,19 @@ struct ZCsr {
     double* s_val = nullptr;
     double* s_y = nullptr;
     // column-sorted tiles (zsplit.hip, default when the slice width < 2^20): the
-    // entries of each (row block of kTileRows rows, slice) sorted by column;
-    // t_idx = row_local << 20 | slice column; the block's range comes from s_rp
+    // entries of each (row block of kTileRows rows, slice) sorted by column,
+    // segment q = slice * t_nrb + row block at [t_seg[q], t_seg[q + 1]); t_idx:
+    // uint32 row_local << 20 | slice column (20 B an entry with the value), or
+    // packed (t_pk): uint16 row_local << 4 | column step in the 64-entry chunk,
+    // t_cbase[chunk] its first column (18.06 B an entry; t_stored entries incl.
+    // zero-valued fillers and chunk padding)
     bool tile = false;
+    bool t_pk = false;
     int64_t t_nrb = 0;
-    uint32_t* t_idx = nullptr;
+    int64_t t_stored = 0;
+    int64_t* t_seg = nullptr;
+    void* t_idx = nullptr;
+    int32_t* t_cbase = nullptr;
     double* t_val = nullptr;
     // deterministic mode's tile form (k_ztile_det: the row sums as 64-bit
     // fixed-point integers): per-(slice, row block) largest |re|, |im| of the
@@ -92,6 +100,10 @@ struct ZCsr {
 // the row's stream); AHIP_ZSPLIT=0 disables.  0: built, 1: not applicable, < 0: error.
 int zcsr_build_split(ZCsr& A);
 void zcsr_free_split(ZCsr& A);
+// algorithmic HBM bytes of the split product's matrix stream (values + the
+// entry encoding: 20 B an entry, or the packed tiles' 18 B + a base column per
+// 64-entry chunk over the stored entries)
+double zcsr_split_matrix_bytes(const ZCsr& A);
 // y = A x through the split (8 slice launches in one grid + the fixed-order combine);
 // gate (device int, may be null): the kernels return at once while *gate != 0
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y,

@@ -306,7 +306,7 @@ void zshift_destroy(ZShift& S) {
 double zshift_iter_bytes(const ZShift& S) {
     const double n = (double)S.n, nnz = (double)S.A->nnz;
     if (S.A->split)  // the products feed v and t directly: no w stored and re-read
-        return 2.0 * (20.0 * nnz + 8.0 * (n + 1) + 16.0 * n) + 304.0 * n;  // 19 n-vectors
+        return 2.0 * (zcsr_split_matrix_bytes(*S.A) + 8.0 * (n + 1) + 16.0 * n) + 304.0 * n;  // 19 n-vectors
     const double spmv = 20.0 * nnz + 8.0 * (n + 1) + 32.0 * n;  // val+col, rowptr, x, y
     return 2.0 * spmv + 336.0 * n;  // + v, s, t, (y, r), p passes (21 complex n-vectors)
 }

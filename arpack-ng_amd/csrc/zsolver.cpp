@@ -1118,6 +1118,13 @@ int arpack_hip_zcsr_info(const arpack_hip_zcsr* Z, int64_t* n, int64_t* nnz) {
     return 0;
 }
 
+int arpack_hip_zcsr_tile_info(const arpack_hip_zcsr* Z, int* form, int64_t* stored) {
+    const auto& A = Z->A;
+    *form = !A.split ? 0 : !A.tile ? 1 : A.t_pk ? 3 : 2;
+    *stored = A.tile ? A.t_stored : A.nnz;
+    return 0;
+}
+
 int arpack_hip_zcsr_download(const arpack_hip_zcsr* Z, int64_t* rowptr, int32_t* col, double* val) {
     const auto& A = Z->A;
     if (hipMemcpy(rowptr, A.rowptr, sizeof(int64_t) * (A.n + 1), hipMemcpyDeviceToHost) ||

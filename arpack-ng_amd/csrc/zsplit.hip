@@ -123,51 +123,116 @@ __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, doub
 constexpr int kTileRows = 4096;  // 64 KB of LDS row sums: two blocks a CU
 constexpr int kTileU = 4;        // entries a lane keeps in flight
 
-template <int S>
-__global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int32_t* __restrict__ srp,
-                                               const int64_t* __restrict__ base,
-                                               const uint32_t* __restrict__ idx,
+// Two encodings of a tile's column-sorted entries (segment q = slice * nrb +
+// row block: entries [seg[q], seg[q + 1])):
+//  * PK = false: idx = row << 20 | slice column (4 B) + the 16-B value: 20 B an entry;
+//  * PK = true (packed, default where it fits): idx16 = row << 4 | dcol (2 B),
+//    dcol = the column step from the previous entry of the same 64-entry
+//    chunk (0 for a chunk's first), and one int32 base column a chunk: 18.06 B
+//    an entry.  A segment starts on a chunk boundary, so every wave's load is
+//    one whole chunk and the columns are its base plus a wave-wide inclusive
+//    scan of the steps.  Steps above 15 get zero-valued filler entries between
+//    them, and every segment is padded to whole chunks with zero values (both
+//    at the segment's own columns; built only where they stay below 3% of the
+//    entries, ztile_pack).
+__device__ __forceinline__ int wave_iscan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+template <bool PK, int U>
+__device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ idx,
+                                           const int32_t* __restrict__ cbase,
+                                           const double2* __restrict__ val, int (&row)[U], int (&col)[U],
+                                           double2 (&v)[U]) {
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    if constexpr (PK) {
+        uint16_t id[U];
+        int cb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // every load of the batch issued first
+            id[u] = __builtin_nontemporal_load(static_cast<const uint16_t*>(idx) + e + u * 256);
+            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+            v[u] = make_double2(w.x, w.y);
+            cb[u] = cbase[(e + u * 256) >> 6];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            row[u] = id[u] >> 4;
+            col[u] = cb[u] + wave_iscan(id[u] & 15);
+        }
+    } else {
+        uint32_t id[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            id[u] = __builtin_nontemporal_load(static_cast<const uint32_t*>(idx) + e + u * 256);
+            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+            v[u] = make_double2(w.x, w.y);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            row[u] = (int)(id[u] >> 20);
+            col[u] = (int)(id[u] & 0xfffffu);
+        }
+    }
+}
+
+// The tile walk of both products below: for each batch of entries, the x
+// gathers of the slice, then add(row, re, im) per entry (LDS row sums).  A
+// packed segment's length is a multiple of 64, so the tail loop's condition is
+// uniform across a wave (its scan needs every lane).
+template <bool PK, class Add>
+__device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __restrict__ idx,
+                                          const int32_t* __restrict__ cbase,
+                                          const double2* __restrict__ val, const double2* __restrict__ xs,
+                                          Add add) {
+    int64_t e = e0 + threadIdx.x;
+    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
+        int row[kTileU], col[kTileU];
+        double2 v[kTileU];
+        tile_batch<PK, kTileU>(e, idx, cbase, val, row, col, v);
+        double2 xv[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u) xv[u] = xs[col[u]];
+#pragma unroll
+        for (int u = 0; u < kTileU; ++u)
+            add(row[u], v[u].x * xv[u].x - v[u].y * xv[u].y, v[u].x * xv[u].y + v[u].y * xv[u].x);
+    }
+    for (; e < e1; e += 256) {
+        int row[1], col[1];
+        double2 v[1];
+        tile_batch<PK, 1>(e, idx, cbase, val, row, col, v);
+        const double2 xv = xs[col[0]];
+        add(row[0], v[0].x * xv.x - v[0].y * xv.y, v[0].x * xv.y + v[0].y * xv.x);
+    }
+}
+
+template <int S, bool PK>
+__global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+                                               int64_t nrb, const void* __restrict__ idx,
+                                               const int32_t* __restrict__ cbase,
                                                const double2* __restrict__ val,
                                                const double2* __restrict__ x,
                                                double2* __restrict__ yp, const int* __restrict__ gate) {
     if (gate && *gate) return;
-    typedef double dv2 __attribute__((ext_vector_type(2)));
     __shared__ double ylds[2 * kTileRows];
     const int s = (int)(blockIdx.x % S);  // the XCD (S = 4: one of two) this block runs on
-    const int64_t r0 = (int64_t)(blockIdx.x / S) * kTileRows;
+    const int64_t rb = blockIdx.x / S;
+    const int64_t r0 = rb * kTileRows;
     const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
     for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
     __syncthreads();
-    const int32_t* rp = srp + (int64_t)s * (n + 1);
-    const int64_t e0 = base[s] + rp[r0], e1 = base[s] + rp[r0 + rows];
-    const double2* xs = x + (int64_t)s * sw;
-    int64_t e = e0 + threadIdx.x;
-    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
-        uint32_t id[kTileU];
-        dv2 v[kTileU];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) {  // every load of the batch issued first
-            id[u] = __builtin_nontemporal_load(&idx[e + u * 256]);
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
-        }
-        double2 xv[kTileU];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) xv[u] = xs[id[u] & 0xfffffu];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) {
-            const int r = (int)(id[u] >> 20);
-            atomicAdd(&ylds[2 * r], v[u].x * xv[u].x - v[u].y * xv[u].y);
-            atomicAdd(&ylds[2 * r + 1], v[u].x * xv[u].y + v[u].y * xv[u].x);
-        }
-    }
-    for (; e < e1; e += 256) {
-        const uint32_t id = idx[e];
-        const dv2 v = reinterpret_cast<const dv2*>(val)[e];
-        const double2 xv = xs[id & 0xfffffu];
-        const int r = (int)(id >> 20);
-        atomicAdd(&ylds[2 * r], v.x * xv.x - v.y * xv.y);
-        atomicAdd(&ylds[2 * r + 1], v.x * xv.y + v.y * xv.x);
-    }
+    const int64_t q = s * nrb + rb;
+    tile_walk<PK>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
+                  [&](int r, double re, double im) {
+                      atomicAdd(&ylds[2 * r], re);
+                      atomicAdd(&ylds[2 * r + 1], im);
+                  });
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
     for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
@@ -185,18 +250,16 @@ static_assert(kZMaxBlocks == 256, "k_ztile_det reduces one block maximum a threa
 // wave order; y_s = (double)(sum q) 2^(E-B).  B = min(51, 62 - bits(L)) for at
 // most L entries a row in a slice.  The slice partials are summed in
 // zc::slice_sum's fixed order as before.
-template <int S>
-__global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const int32_t* __restrict__ srp,
-                                                   const int64_t* __restrict__ base,
-                                                   const uint32_t* __restrict__ idx,
+template <int S, bool PK>
+__global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+                                                   int64_t nrb, const void* __restrict__ idx,
+                                                   const int32_t* __restrict__ cbase,
                                                    const double2* __restrict__ val,
                                                    const double2* __restrict__ x,
                                                    double2* __restrict__ yp, const int* __restrict__ gate,
                                                    const double* __restrict__ amax,
-                                                   const unsigned long long* __restrict__ xmax, int bits,
-                                                   int64_t nrb) {
+                                                   const unsigned long long* __restrict__ xmax, int bits) {
     if (gate && *gate) return;
-    typedef double dv2 __attribute__((ext_vector_type(2)));
     constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
     const unsigned long long kMagicBits = (unsigned long long)__double_as_longlong(kMagic);
     __shared__ unsigned long long ylds[2 * kTileRows];
@@ -213,47 +276,23 @@ __global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const 
     }
     __syncthreads();
     const double X = __longlong_as_double((long long)max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+    const int64_t q = s * nrb + rb;
     int ea = 0, ex = 0;
-    (void)frexp(amax[s * nrb + rb], &ea);
+    (void)frexp(amax[q], &ea);
     (void)frexp(X, &ex);
     const int E = max(ea + ex + 1, bits - 1000);
     const double inv = ldexp(1.0, bits - E);
     const double sc = X <= DBL_MAX ? ldexp(1.0, E - bits) : __longlong_as_double(0x7ff8000000000000ll);
     __syncthreads();
-    const int32_t* rp = srp + (int64_t)s * (n + 1);
-    const int64_t e0 = base[s] + rp[r0], e1 = base[s] + rp[r0 + rows];
-    const double2* xs = x + (int64_t)s * sw;
-    auto add = [&](int r, double p, int part) {
+    auto q64 = [&](double p) {
         const double f = fma(p, inv, kMagic);
-        atomicAdd(&ylds[2 * r + part], (unsigned long long)__double_as_longlong(f) - kMagicBits);
+        return (unsigned long long)__double_as_longlong(f) - kMagicBits;
     };
-    int64_t e = e0 + threadIdx.x;
-    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
-        uint32_t id[kTileU];
-        dv2 v[kTileU];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) {
-            id[u] = __builtin_nontemporal_load(&idx[e + u * 256]);
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
-        }
-        double2 xv[kTileU];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) xv[u] = xs[id[u] & 0xfffffu];
-#pragma unroll
-        for (int u = 0; u < kTileU; ++u) {
-            const int r = (int)(id[u] >> 20);
-            add(r, v[u].x * xv[u].x - v[u].y * xv[u].y, 0);
-            add(r, v[u].x * xv[u].y + v[u].y * xv[u].x, 1);
-        }
-    }
-    for (; e < e1; e += 256) {
-        const uint32_t id = idx[e];
-        const dv2 v = reinterpret_cast<const dv2*>(val)[e];
-        const double2 xv = xs[id & 0xfffffu];
-        const int r = (int)(id >> 20);
-        add(r, v.x * xv.x - v.y * xv.y, 0);
-        add(r, v.x * xv.y + v.y * xv.x, 1);
-    }
+    tile_walk<PK>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
+                  [&](int r, double re, double im) {
+                      atomicAdd(&ylds[2 * r], q64(re));
+                      atomicAdd(&ylds[2 * r + 1], q64(im));
+                  });
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
     for (int i = threadIdx.x; i < rows; i += 256)
@@ -346,6 +385,83 @@ __global__ void k_ztile_gather(int64_t nnz, const uint32_t* __restrict__ perm,
     }
 }
 
+// ---- packing (ztile_pack): the 20-B encoding -> the 18-B one -------------------
+__device__ __forceinline__ int64_t seg_of(const int64_t* __restrict__ seg, int64_t nseg, int64_t k) {
+    int64_t lo = 0, hi = nseg;  // the last q with seg[q] <= k
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (seg[mid] <= k) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+// fillers before sorted entry k: steps above 15 inside a segment
+__global__ void k_zpk_fills(int64_t nnz, const uint32_t* __restrict__ idx, const int64_t* __restrict__ seg,
+                            int64_t nseg, int64_t* __restrict__ fills) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nnz;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t f = 0;
+        if (k < nnz) {
+            const int64_t q = seg_of(seg, nseg, k);
+            if (k > seg[q]) {
+                const int32_t g = (int32_t)(idx[k] & 0xfffffu) - (int32_t)(idx[k - 1] & 0xfffffu);
+                f = g > 15 ? (g + 14) / 15 - 1 : 0;
+            }
+        }
+        fills[k] = f;
+    }
+}
+// every entry at its packed position, its fillers just before it (columns
+// col - 15 i, zero values; rows and values were zeroed)
+__global__ void k_zpk_scatter(int64_t nnz, const uint32_t* __restrict__ idx, const double2* __restrict__ val,
+                              const int64_t* __restrict__ seg, int64_t nseg, const int64_t* __restrict__ fscan,
+                              const int64_t* __restrict__ poff, int32_t* __restrict__ pcol,
+                              uint16_t* __restrict__ prow, double2* __restrict__ pval) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = seg_of(seg, nseg, k);
+        const int64_t pos = poff[q] + (k - seg[q]) + (fscan[k] - fscan[seg[q]]);
+        const int32_t c = (int32_t)(idx[k] & 0xfffffu);
+        pcol[pos] = c;
+        prow[pos] = (uint16_t)(idx[k] >> 20);
+        pval[pos] = val[k];
+        const int64_t f = fscan[k + 1] - fscan[k];
+        for (int64_t i = 1; i <= f; ++i) pcol[pos - i] = c - (int32_t)(15 * i);
+    }
+}
+__global__ void k_zpk_segfill(int64_t nseg, const int64_t* __restrict__ seg, const int64_t* __restrict__ fscan,
+                              int64_t* __restrict__ out) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= nseg;
+         q += (int64_t)gridDim.x * blockDim.x)
+        out[q] = fscan[seg[q]];
+}
+// a segment's padding to whole chunks: its last column, zero values
+__global__ void k_zpk_pad(int64_t nseg, const int64_t* __restrict__ seg, const int64_t* __restrict__ fscan,
+                          const int64_t* __restrict__ poff, int32_t* __restrict__ pcol) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nseg;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t len = (seg[q + 1] - seg[q]) + (fscan[seg[q + 1]] - fscan[seg[q]]);
+        const int32_t last = len > 0 ? pcol[poff[q] + len - 1] : 0;
+        for (int64_t p = poff[q] + len; p < poff[q + 1]; ++p) pcol[p] = last;
+    }
+}
+// idx16 = row << 4 | step, one base column a 64-entry chunk; *bad counts steps
+// outside [0, 15] (none by construction: the build checks)
+__global__ void k_zpk_encode(int64_t stored, const int32_t* __restrict__ pcol, const uint16_t* __restrict__ prow,
+                             uint16_t* __restrict__ idx16, int32_t* __restrict__ cbase, int* __restrict__ bad) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < stored;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        int32_t d = 0;
+        if ((p & 63) == 0) cbase[p >> 6] = pcol[p];
+        else d = pcol[p] - pcol[p - 1];
+        if (d < 0 || d > 15 || prow[p] >= kTileRows) {
+            atomicAdd(bad, 1);
+            d = 0;
+        }
+        idx16[p] = (uint16_t)((prow[p] << 4) | d);
+    }
+}
+
 inline int grid1(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
@@ -355,6 +471,11 @@ inline int grid1(int64_t n) {
 void zcsr_free_split(ZCsr& A) {
     if (A.t_idx) (void)hipFree(A.t_idx);
     if (A.t_val) (void)hipFree(A.t_val);
+    if (A.t_cbase) (void)hipFree(A.t_cbase);
+    if (A.t_seg) (void)hipFree(A.t_seg);
+    A.t_cbase = nullptr;
+    A.t_seg = nullptr;
+    A.t_pk = false;
     if (A.t_amax) (void)hipFree(A.t_amax);
     if (A.t_xmax) (void)hipFree(A.t_xmax);
     A.t_idx = nullptr;
@@ -374,6 +495,95 @@ void zcsr_free_split(ZCsr& A) {
     A.s_val = nullptr;
     A.s_y = nullptr;
     A.split = false;
+}
+
+// The packed (18-B) encoding of the sorted tiles (k_ztile PK): from the 20-B
+// arrays A.t_idx / A.t_val over A.t_seg, which it replaces.  0: packed; 1: not
+// built (AHIP_ZTILE_PACK=0, or fillers + padding above 3% of the entries --
+// a sparse slice); < 0: error (the 20-B form stays).
+static int ztile_pack(ZCsr& A, int64_t nseg) {
+    static const bool off = [] {
+        const char* e = getenv("AHIP_ZTILE_PACK");
+        return e && e[0] == '0';
+    }();
+    if (off) return 1;
+    const int64_t nnz = A.nnz;
+    int64_t *fills = nullptr, *fscan = nullptr, *segf = nullptr, *poff = nullptr;
+    int32_t *pcol = nullptr, *cbase = nullptr;
+    uint16_t *prow = nullptr, *idx16 = nullptr;
+    double2* pval = nullptr;
+    int* bad = nullptr;
+    void* tmp = nullptr;
+    size_t tmpb = 0;
+    auto release = [&](bool outputs) {
+        for (void* q : {(void*)fills, (void*)fscan, (void*)segf, (void*)pcol, (void*)prow, (void*)bad, tmp})
+            if (q) (void)hipFree(q);
+        if (outputs)
+            for (void* q : {(void*)poff, (void*)idx16, (void*)pval, (void*)cbase})
+                if (q) (void)hipFree(q);
+    };
+    const auto* idx = static_cast<const uint32_t*>(A.t_idx);
+    if (hipMalloc(&fills, sizeof(int64_t) * (nnz + 1)) || hipMalloc(&fscan, sizeof(int64_t) * (nnz + 1)) ||
+        hipMalloc(&segf, sizeof(int64_t) * (nseg + 1))) {
+        release(true);
+        return -2;
+    }
+    hipLaunchKernelGGL(k_zpk_fills, dim3(grid1(nnz + 1)), dim3(256), 0, nullptr, nnz, idx, A.t_seg, nseg, fills);
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, fills, fscan, (int)(nnz + 1)) != hipSuccess ||
+        hipMalloc(&tmp, tmpb ? tmpb : 1) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, fills, fscan, (int)(nnz + 1)) != hipSuccess) {
+        release(true);
+        return -2;
+    }
+    hipLaunchKernelGGL(k_zpk_segfill, dim3(grid1(nseg + 1)), dim3(256), 0, nullptr, nseg, A.t_seg, fscan, segf);
+    std::vector<int64_t> hseg((size_t)nseg + 1), hf((size_t)nseg + 1), hp((size_t)nseg + 1, 0);
+    if (hipMemcpy(hseg.data(), A.t_seg, sizeof(int64_t) * (nseg + 1), hipMemcpyDeviceToHost) ||
+        hipMemcpy(hf.data(), segf, sizeof(int64_t) * (nseg + 1), hipMemcpyDeviceToHost)) {
+        release(true);
+        return -2;
+    }
+    for (int64_t q = 0; q < nseg; ++q) {
+        const int64_t len = (hseg[q + 1] - hseg[q]) + (hf[q + 1] - hf[q]);
+        hp[q + 1] = hp[q] + (len + 63) / 64 * 64;
+    }
+    const int64_t stored = hp[nseg];
+    if ((double)(stored - nnz) > 0.03 * (double)nnz || stored >= (int64_t(1) << 32)) {
+        release(true);
+        return 1;
+    }
+    const int64_t nch = stored / 64;
+    if (hipMalloc(&poff, sizeof(int64_t) * (nseg + 1)) || hipMalloc(&pcol, sizeof(int32_t) * (stored + 1)) ||
+        hipMalloc(&prow, sizeof(uint16_t) * (stored + 1)) || hipMalloc(&pval, 16 * (size_t)(stored + 1)) ||
+        hipMalloc(&idx16, sizeof(uint16_t) * (stored + 1)) ||
+        hipMalloc(&cbase, sizeof(int32_t) * (nch + 1)) || hipMalloc(&bad, sizeof(int)) ||
+        hipMemcpy(poff, hp.data(), sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice) ||
+        hipMemset(prow, 0, sizeof(uint16_t) * (stored + 1)) || hipMemset(pval, 0, 16 * (size_t)(stored + 1)) ||
+        hipMemset(bad, 0, sizeof(int))) {
+        release(true);
+        return -2;
+    }
+    hipLaunchKernelGGL(k_zpk_scatter, dim3(grid1(nnz)), dim3(256), 0, nullptr, nnz, idx,
+                       (const double2*)A.t_val, A.t_seg, nseg, fscan, poff, pcol, prow, pval);
+    hipLaunchKernelGGL(k_zpk_pad, dim3(grid1(nseg)), dim3(256), 0, nullptr, nseg, A.t_seg, fscan, poff, pcol);
+    hipLaunchKernelGGL(k_zpk_encode, dim3(grid1(stored)), dim3(256), 0, nullptr, stored, pcol, prow, idx16,
+                       cbase, bad);
+    int hbad = 1;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || hbad != 0) {
+        release(true);
+        return -1;
+    }
+    release(false);
+    (void)hipFree(A.t_idx);
+    (void)hipFree(A.t_val);
+    (void)hipFree(A.t_seg);
+    A.t_idx = idx16;
+    A.t_val = reinterpret_cast<double*>(pval);
+    A.t_seg = poff;
+    A.t_cbase = cbase;
+    A.t_stored = stored;
+    A.t_pk = true;
+    return 0;
 }
 
 // Column-sorted tiles from the slice CSR (A.split): a stable segmented radix sort
@@ -402,6 +612,7 @@ static int ztile_build(ZCsr& A) {
     if (hipMalloc(&key, eb) || hipMalloc(&key2, eb) || hipMalloc(&erow, eb) || hipMalloc(&perm, eb) ||
         hipMalloc(&perm2, eb) || hipMalloc(&seg, sizeof(int64_t) * (nseg + 1)) ||
         hipMalloc(&A.t_idx, eb) || hipMalloc(&A.t_val, 16 * (size_t)nnz)) {
+        // (A.t_idx: the 20-B form's uint32 entries until ztile_pack)
         rc = -2;
     } else {
         if (A.s_col16)
@@ -422,15 +633,23 @@ static int ztile_build(ZCsr& A) {
             rc = -1;
         } else {
             hipLaunchKernelGGL(k_ztile_gather, dim3(grid1(nnz)), dim3(256), 0, nullptr, nnz, perm2, key2, erow,
-                               (const double2*)A.s_val, A.t_idx, (double2*)A.t_val);
+                               (const double2*)A.s_val, static_cast<uint32_t*>(A.t_idx),
+                               (double2*)A.t_val);
             if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+            if (rc == 0) {  // the segment bounds stay with the tiles; the 18-B form where it fits
+                A.t_seg = seg;
+                seg = nullptr;
+                A.t_stored = nnz;
+                if (ztile_pack(A, nseg) < 0) rc = 0;  // (an error leaves the 20-B form, still valid)
+            }
             // the deterministic form's scale inputs (optional: without them
             // deterministic mode keeps the CSR split)
             int* dl = nullptr;
             if (rc == 0 && hipMalloc(&A.t_amax, sizeof(double) * (size_t)nseg) == hipSuccess &&
                 hipMalloc(&A.t_xmax, sizeof(unsigned long long) * kZMaxBlocks) == hipSuccess &&
                 hipMalloc(&dl, sizeof(int)) == hipSuccess && hipMemset(dl, 0, sizeof(int)) == hipSuccess) {
-                hipLaunchKernelGGL(k_ztile_amax, dim3((unsigned)nseg), dim3(256), 0, nullptr, seg, A.t_val, A.t_amax);
+                hipLaunchKernelGGL(k_ztile_amax, dim3((unsigned)nseg), dim3(256), 0, nullptr, A.t_seg, A.t_val,
+                                   A.t_amax);
                 hipLaunchKernelGGL(k_zslice_lmax, dim3(grid1(n)), dim3(256), 0, nullptr, n, A.s_n, A.s_rp, dl);
                 std::vector<double> am((size_t)nseg);
                 int L = 0;
@@ -452,6 +671,11 @@ static int ztile_build(ZCsr& A) {
     if (rc != 0) {
         if (A.t_idx) (void)hipFree(A.t_idx);
         if (A.t_val) (void)hipFree(A.t_val);
+        if (A.t_seg) (void)hipFree(A.t_seg);
+        if (A.t_cbase) (void)hipFree(A.t_cbase);
+        A.t_seg = nullptr;
+        A.t_cbase = nullptr;
+        A.t_pk = false;
         if (A.t_amax) (void)hipFree(A.t_amax);
         if (A.t_xmax) (void)hipFree(A.t_xmax);
         A.t_idx = nullptr;
@@ -550,9 +774,14 @@ int zcsr_build_split(ZCsr& A) {
 namespace {
 template <int S>
 void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp, const int* gate) {
+    const dim3 tg((unsigned)(S * A.t_nrb)), tb(256);
     if (A.tile && !deterministic()) {  // (LDS-atomic row sums: not bitwise run to run)
-        hipLaunchKernelGGL(k_ztile<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w, A.s_rp,
-                           A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
+                               (const double2*)A.t_val, x2, yp, gate);
+        };
+        if (A.t_pk) go(k_ztile<S, true>);
+        else go(k_ztile<S, false>);
         return;
     }
     if (A.tile && A.t_det) {  // deterministic: the fixed-point tile form (else the CSR split, kept)
@@ -560,9 +789,12 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
         // include/arpack_hip.h -- ADVICE r05)
         hipLaunchKernelGGL(k_zabsmax, dim3(kZMaxBlocks), dim3(256), 0, s, 2 * A.n,
                            reinterpret_cast<const double*>(x2), A.t_xmax, gate);
-        hipLaunchKernelGGL(k_ztile_det<S>, dim3((unsigned)(S * A.t_nrb)), dim3(256), 0, s, A.n, A.s_w,
-                           A.s_rp, A.s_base, A.t_idx, (const double2*)A.t_val, x2, yp, gate, A.t_amax,
-                           A.t_xmax, A.t_bits, A.t_nrb);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
+                               (const double2*)A.t_val, x2, yp, gate, A.t_amax, A.t_xmax, A.t_bits);
+        };
+        if (A.t_pk) go(k_ztile_det<S, true>);
+        else go(k_ztile_det<S, false>);
         return;
     }
     const int g = 1024;  // 128 workgroups a slice at S = 8 (tools/zspmv_split.hip)
@@ -574,6 +806,11 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
                            A.s_base, (const int32_t*)A.s_col, (const double2*)A.s_val, x2, yp, gate);
 }
 }  // namespace
+
+double zcsr_split_matrix_bytes(const ZCsr& A) {
+    if (A.tile && A.t_pk) return 18.0 * (double)A.t_stored + 4.0 * (double)(A.t_stored / 64);
+    return 20.0 * (double)A.nnz;
+}
 
 const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x, const int* gate) {
     if (!A.split) return nullptr;

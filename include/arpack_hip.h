@@ -290,6 +290,11 @@ int arpack_hip_gen_zrandom(arpack_hip_zcsr** A, int64_t n, int per_row, uint32_t
                            double dshift);
 void arpack_hip_zcsr_destroy(arpack_hip_zcsr* A);
 int arpack_hip_zcsr_info(const arpack_hip_zcsr* A, int64_t* n, int64_t* nnz);
+/* The product's layout: *form 0 wave-per-row CSR, 1 XCD column split (slice
+ * CSRs), 2 column-sorted tiles (20 B an entry), 3 packed tiles (16-B value +
+ * 16-bit row/column-step code + a base column per 64 entries); *stored: the
+ * entries the product streams (packed: incl. zero-valued fillers and padding). */
+int arpack_hip_zcsr_tile_info(const arpack_hip_zcsr* A, int* form, int64_t* stored);
 int arpack_hip_zcsr_download(const arpack_hip_zcsr* A, int64_t* rowptr, int32_t* col,
                              double* val);
 int arpack_hip_zcsr_spmv(const arpack_hip_zcsr* A, const double* x, double* y);

@@ -122,6 +122,24 @@ def test_zcsr_spmv_xcd_split(pkg, n, per, seed):
     Z2 = pkg.ZCSR.from_arrays(rp, col, val)  # the arpack_hip_zcsr_create path
     # column-sorted tiles add into LDS row sums in schedule order: equal to rounding
     assert np.abs(Z2.matvec(x) - y).max() <= 1e-13 * np.abs(yref).max()
+    form, stored = Z.tile_info()
+    if n >= 2 ** 18:  # the packed tiles where fillers + padding stay <= 3%
+        assert form == 3 and Z.nnz <= stored <= 1.03 * Z.nnz, (form, stored, Z.nnz)
+
+
+def test_zcsr_tiles_sparse_slices_keep_20_byte_form(pkg):
+    """An operator whose column slices are sparse (n = 2^20, 40 entries a row,
+    8 slices of 131,072 columns: ~5 entries a row in a tile, mean column step
+    ~6.5) would need fillers for too many steps above 15: the 20-B tiles stay,
+    and the product still equals SciPy's."""
+    import scipy.sparse as sp
+    n = 2 ** 20
+    Z = pkg.ZCSR.random(n, 40, 11, 100.0)
+    assert Z.tile_info()[0] == 2
+    rp, col, val = Z.download()
+    x = np.random.default_rng(1).uniform(-1, 1, n) + 0.25j
+    yref = sp.csr_matrix((val, col, rp), shape=(n, n)) @ x
+    assert np.abs(Z.matvec(x) - yref).max() <= 1e-13 * np.abs(yref).max()
 
 
 _CSR_SPLIT = """
@@ -131,6 +149,7 @@ from bench import load_pkg
 pkg = load_pkg()
 for n, per, seed in [(300000, 64, 7), (524289, 40, 3)]:
     Z = pkg.ZCSR.random(n, per, seed, 100.0)
+    assert Z.tile_info()[0] == FORM, Z.tile_info()
     rp, col, val = Z.download()
     x = np.random.default_rng(seed).uniform(-1, 1, n) + 0.5j
     y, yref = Z.matvec(x), sp.csr_matrix((val, col, rp), shape=(n, n)) @ x
@@ -150,6 +169,19 @@ def test_zcsr_spmv_csr_split_form():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, AHIP_ZSPLIT="csr")
-    r = subprocess.run([sys.executable, "-c", _CSR_SPLIT % root], env=env, capture_output=True,
-                       text=True, timeout=240)
+    r = subprocess.run([sys.executable, "-c", "FORM = 1\n" + _CSR_SPLIT % root], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_zcsr_spmv_unpacked_tile_form():
+    """The column-sorted tiles in their 20-B encoding (AHIP_ZTILE_PACK=0: the
+    form before round 6, and the one sparse slices keep) against SciPy."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AHIP_ZTILE_PACK="0")
+    r = subprocess.run([sys.executable, "-c", "FORM = 2\n" + _CSR_SPLIT % root], env=env,
+                       capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

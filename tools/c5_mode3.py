@@ -62,11 +62,16 @@ def run(pkg, cycles=4, rtol=1e-12, n=500_000, sigma=0j):
         solver_roofline=dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                              frac=(gbs / HBM_PEAK_GBS) if gbs else None,
                              bytes_per_iter=st["bytes_per_iter"],
-                             bytes_model="per BiCGStab iteration: two CSR products at 20 B a "
-                                         "stored complex entry (16 B value + 4 B column) + 8 B "
-                                         "rowptr + 16 B x a row, feeding v and t directly, and "
-                                         "19 complex n-vector passes of the fused updates "
-                                         "(csrc/zsolve.hip zshift_iter_bytes)"))
+                             tile_form=Z.tile_info()[0], stored_entries=Z.tile_info()[1],
+                             bytes_model="per BiCGStab iteration: two products over the "
+                                         "column-sorted tiles -- packed (tile_form 3): 18 B a "
+                                         "stored complex entry (16 B value + 2 B row / column-"
+                                         "step code) + 4 B a 64-entry chunk, stored entries "
+                                         "incl. fillers and padding; tile_form 2: 20 B an entry "
+                                         "(16 B value + 4 B row | column) -- + 8 B rowptr + 16 B "
+                                         "x a row, feeding v and t directly, and 19 complex "
+                                         "n-vector passes of the fused updates (csrc/zsolve.hip "
+                                         "zshift_iter_bytes)"))
 
 
 def main():
