@@ -402,6 +402,21 @@ class CSR:
             raise RuntimeError("symmetric storage not applicable to this matrix (rc=%d)" % rc)
         self.symmetric = bool(on)
 
+    def set_sym_accumulator(self, acc: str = "fixed"):
+        """The symmetric kernel's transposed-term accumulator: "fixed" (the
+        fixed-point form, bitwise reproducible; default) or "fp64" (LDS fp64
+        atomics in schedule order) -- arpack_hip_csr_set_sym_accumulator."""
+        lib().arpack_hip_csr_set_sym_accumulator.argtypes = [C.c_void_p, C.c_int]
+        if lib().arpack_hip_csr_set_sym_accumulator(self.h, {"fixed": 0, "fp64": 1}[acc]) != 0:
+            raise RuntimeError("set_sym_accumulator failed")
+
+    @property
+    def sym_form(self):
+        """"full", "sym_fp64" or "sym_fixed": the SpMV form the operator runs
+        now (arpack_hip_csr_sym_form)."""
+        lib().arpack_hip_csr_sym_form.argtypes = [C.c_void_p]
+        return ("full", "sym_fp64", "sym_fixed")[lib().arpack_hip_csr_sym_form(self.h)]
+
     def time_spmv(self, reps=20):
         x = DeviceBuffer(self.n)
         x.write(np.linspace(-1, 1, self.n))

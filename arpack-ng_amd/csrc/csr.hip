@@ -421,6 +421,18 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     return 0;
 }
 
+int arpack_hip_csr_set_sym_accumulator(arpack_hip_csr* A, int acc) {
+    if (!A || (acc != 0 && acc != 1)) return -1;
+    A->A.ss_acc = acc;
+    return 0;
+}
+
+int arpack_hip_csr_sym_form(const arpack_hip_csr* A) {
+    const ahip::dev::Csr& M = A->A;
+    if (M.kernel != ahip::dev::kCsrSymSell || !M.ss_val || ahip::dev::csr_sym_det_fallback(M)) return 0;
+    return M.ss_det_all && (M.ss_acc == 0 || ahip::deterministic()) ? 2 : 1;
+}
+
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {
     if (kernel == ahip::dev::kCsrSymSell) {  // tile selects the variant
         const int rc = arpack_hip_csr_set_symmetric(A, 1);

@@ -341,6 +341,11 @@ struct Csr {
     // the operator was declared symmetric runs the full-storage (fixed-order)
     // SpMV on every rank when this is 0 (csr_sym_det_fallback)
     int ss_det_all = 0;
+    // the transposed terms' accumulator where ss_det_all holds: 0 (default
+    // since round 6) the fixed-point form -- y bitwise reproducible; 1 the LDS
+    // fp64 atomics (schedule order; arpack_hip_csr_set_sym_accumulator).
+    // Deterministic mode always takes the fixed-point form.
+    int ss_acc = 0;
     int ss_detq = 0;  // most slices one wave walks in a superblock
 };
 enum CsrKernel : int {

@@ -966,8 +966,10 @@ static bool spmv_ynt() {
     return on;
 }
 
-// deterministic mode takes the fixed-point form where the plan allows it
-static bool sym_det(const Csr& A) { return A.ss_det && deterministic(); }
+// the fixed-point form wherever it serves the operator on every rank: by
+// default, or always in deterministic mode (an operator outside the form runs
+// the LDS fp64 form by default, the full-storage kernel in deterministic mode)
+static bool sym_det(const Csr& A) { return A.ss_det_all && (A.ss_acc == 0 || deterministic()); }
 // AHIP_HANDOFF=2: the fused chain-head hand-off in the memory model's acq_rel
 // form instead of the measured sc1 form (k_csr_ssell FUSE = 2 vs 1, A/B)
 static int handoff_form() {

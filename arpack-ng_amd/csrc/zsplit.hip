@@ -420,7 +420,9 @@ __global__ void k_zpk_scatter(int64_t nnz, const uint32_t* __restrict__ idx, con
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz;
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t q = seg_of(seg, nseg, k);
-        const int64_t pos = poff[q] + (k - seg[q]) + (fscan[k] - fscan[seg[q]]);
+        // after the fillers of every entry up to and including k (its own
+        // precede it): the inclusive count fscan[k + 1]
+        const int64_t pos = poff[q] + (k - seg[q]) + (fscan[k + 1] - fscan[seg[q]]);
         const int32_t c = (int32_t)(idx[k] & 0xfffffu);
         pcol[pos] = c;
         prow[pos] = (uint16_t)(idx[k] >> 20);

@@ -143,7 +143,7 @@ def kernel_family(name: str):
 
 
 # the keys a PMC summary's workload block must share with the line it serves
-PMC_KEYS = ("workload", "n", "nnz", "storage", "deterministic")
+PMC_KEYS = ("workload", "n", "nnz", "storage", "spmv_form")
 
 
 def pmc_traffic(families, workload, profiles_dir=None):
@@ -315,7 +315,7 @@ def main():
     ap.add_argument("--steady-cycles", type=int, default=3,
                     help="restart cycles 1..k of one solve timed on GPU and CPU alike")
     ap.add_argument("--no-full-storage", action="store_true",
-                    help="skip the secondary full-storage and deterministic-mode measurements of --storage sym")
+                    help="skip the secondary full-storage and other-accumulator measurements of --storage sym")
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: engine collectives over gloo instead of RCCL, so N ranks "
                          "can share one GPU (every rank uses device 0)")
@@ -328,6 +328,10 @@ def main():
                          "(1-rank RCCL communicator, DistOp) to price its machinery")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-kernel hipEvents in the timed region (overhead check)")
+    ap.add_argument("--sym-acc", choices=("fixed", "fp64"), default="fixed",
+                    help="symmetric storage's transposed-term accumulator: fixed (the "
+                         "fixed-point form, bitwise reproducible; default) or fp64 (LDS fp64 "
+                         "atomics in schedule order); the other one runs beside as a companion")
     ap.add_argument("--deterministic", action="store_true",
                     help="deterministic mode (arpack_hip_set_deterministic): only fixed-order "
                          "SpMV forms (--storage sym: the fixed-point symmetric kernel "
@@ -416,6 +420,11 @@ def main():
             storage = "sym" if A.symmetric else "full"
         except RuntimeError:
             pass
+    # the symmetric kernel's accumulator: the fixed-point form by default (y
+    # bitwise reproducible), --sym-acc fp64 the LDS fp64 atomics
+    if storage == "sym":
+        A.set_sym_accumulator(args.sym_acc)
+    sym_form = A.sym_form
     gen_s = time.time() - t
     nnz = A.nnz
     if dist:
@@ -489,23 +498,23 @@ def main():
                             lanczos_steps_per_s=nopx_f / el_f)
         del s_f
         A.set_symmetric(True)
-    det_mode = None
+    acc_companion = None
     if storage == "sym" and world == 1 and not args.no_full_storage and not args.deterministic:
-        # the same K cycles in deterministic mode (the fixed-point symmetric
-        # form of k_csr_ssell: bitwise reproducible solves), reported beside
-        pkg.set_deterministic(True)
-        A.set_symmetric(True)  # 0: the fixed-point form serves this operator
-        if A.last_rc == 0 and A.symmetric:
+        # the same K cycles with the OTHER accumulator of the symmetric kernel
+        # (fixed point <-> LDS fp64 atomics), reported beside
+        other = "fp64" if args.sym_acc == "fixed" else "fixed"
+        A.set_sym_accumulator(other)
+        if A.sym_form != sym_form:
             s_d, ido_d, el_d, nopx_d, _ = timed_run()
-            det_mode = dict(value=args.steps / el_d, ms_per_step=1e3 * el_d / args.steps,
-                            lanczos_steps_per_s=nopx_d / el_d, bitwise_reproducible=True,
-                            kernel="k_csr_ssell, DET form (64-bit fixed-point transposed terms)")
+            acc_companion = dict(accumulator=other, value=args.steps / el_d,
+                                 ms_per_step=1e3 * el_d / args.steps,
+                                 lanczos_steps_per_s=nopx_d / el_d,
+                                 bitwise_reproducible=A.sym_form == "sym_fixed")
             del s_d
         else:
-            det_mode = dict(value=None, note="operator outside the fixed-point form "
-                                             "(deterministic mode keeps full storage)")
-        pkg.set_deterministic(False)
-        A.set_symmetric(True)
+            acc_companion = dict(accumulator=other, value=None,
+                                 note="operator outside the fixed-point form")
+        A.set_sym_accumulator(args.sym_acc)
     s, ido, elapsed, nopx, nsolves = timed_run()
     # Per-kernel roofline: the next K cycles of the same solve with hipEvents on
     # every kernel's dispatch (start event on a span's first kernel, stop event
@@ -617,12 +626,11 @@ def main():
     # counter traffic from a committed PMC summary of THIS workload (same
     # operator, size, storage and mode), single GPU only
     # (one symmetric kernel, k_csr_ssell<..., DET, ...>, since round 6; the
-    # deterministic form's former name is kept for older summaries -- the
-    # workload's "deterministic" key tells the two modes apart)
+    # fixed-point form's former name is kept for older summaries -- the
+    # workload's "spmv_form" key tells the two accumulators apart)
     families = {"k_csr_ssell", "k_csr_ssell_det"} if storage == "sym" \
         else {"k_csr_sell", "k_csr_sell_fin"}
-    wl = dict(workload=args.workload, n=n, nnz=nnz, storage=storage,
-              deterministic=bool(args.deterministic))
+    wl = dict(workload=args.workload, n=n, nnz=nnz, storage=storage, spmv_form=sym_form)
     if world == 1 and D is None:
         traffic, traffic_src, traffic_note = pmc_traffic(families, wl)
     else:
@@ -652,10 +660,11 @@ def main():
                    "n": n, "nnz": nnz, "nnz_per_row": nnz / n, "nev": nev, "ncv": ncv,
                    "which": "LA", "tol": "eps (a solve that converges inside the timed window is followed by a fresh one)",
                    "spmv_storage": "symmetric (upper triangle)" if storage == "sym" else "full CSR",
-                   # sym: the transposed terms meet in LDS in wave order (Ritz values
-                   # reproducible to ~6e-15, not bitwise); full, and sym in
-                   # deterministic mode (fixed-point transposed terms): fixed-order sums
-                   "bitwise_reproducible": storage == "full" or bool(args.deterministic),
+                   # full storage and the symmetric kernel's fixed-point form: fixed-
+                   # order sums throughout; the fp64 accumulator's transposed terms
+                   # meet in LDS in wave order (Ritz values to ~6e-15, not bitwise)
+                   "spmv_form": sym_form,
+                   "bitwise_reproducible": sym_form in ("full", "sym_fixed"),
                    "deterministic_mode": bool(args.deterministic),
                    "parallelism": "single GPU" if world == 1 else
                    f"row-block x{world} (RCCL allreduce + halo)" if not args.host_transport else
@@ -671,12 +680,13 @@ def main():
                      "traffic_source": traffic_src, "traffic_note": traffic_note,
                      "traffic_ratio": (traffic / spmv_bytes) if traffic and spmv_bytes else None,
                      "kernel": ("csr_spmv symmetric storage (k_csr_ssell: upper-triangle SELL-64 "
-                                "slices over LDS x/y windows, LDS atomic transposed terms, 16-bit "
-                                "window-relative cols; on one GPU the chain-head combine and the "
-                                "step's deferred finalize run inside it, else k_ssell_combine "
-                                "follows)" + ("; deterministic mode: the same walk with the "
-                                              "transposed terms as 64-bit fixed-point LDS sums"
-                                              if args.deterministic else "")) if storage == "sym"
+                                "slices over LDS x/y windows, 16-bit window-relative cols, the "
+                                "transposed terms " + ("as 64-bit fixed-point LDS sums (bitwise "
+                                                       "reproducible)" if sym_form == "sym_fixed"
+                                                       else "as LDS fp64 atomics") +
+                                "; on one GPU the chain-head combine and the step's deferred "
+                                "finalize run inside it, else k_ssell_combine follows)")
+                               if storage == "sym"
                                else ("csr_spmv (k_csr_sell: SELL-64 length-sorted slices over LDS "
                                      "x windows, 16-bit window-relative cols, XCD-contiguous "
                                      "superblocks)"),
@@ -711,7 +721,7 @@ def main():
         "gen_s": gen_s,
         "storage": storage,
         "full_storage": full_storage,
-        "deterministic": det_mode,
+        "accumulator_companion": acc_companion,
     }
     # SURVEY.md §8(d)'s byte model of the reference's arithmetic on the same
     # product / cycle, divided by OUR times: an "effective" rate that can exceed

@@ -236,14 +236,25 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * allreduce) and if any rank's plan fails every rank keeps the full-storage
  * kernel and returns nonzero (its own plan error, or -2 when only another
  * rank's plan failed); -3 if the distribution's communicator has been
- * destroyed.  In deterministic mode (arpack_hip_set_deterministic) on = 1
- * selects the fixed-point form of the same kernel (transposed terms summed as
- * exact 64-bit integers: y bitwise reproducible) and returns 0, or, when the
- * operator does not fit that form on every rank (no free LDS word past a
- * window, rows receiving more than 2^22 transposed terms, or a largest
- * off-diagonal magnitude outside [2^-900, 2^900]), keeps the full-storage
- * kernel and returns 1. */
+ * destroyed.  The transposed terms are summed in the kernel's fixed-point
+ * form (exact 64-bit integers: y bitwise reproducible, each term rounded to
+ * 2^-51 of the window's largest |a_ij| max|x|) wherever the operator fits it
+ * on every rank -- the default since round 6 -- else as LDS fp64 atomics in
+ * schedule order (y reproducible to ~1 ulp, not bitwise; also selected by
+ * arpack_hip_csr_set_sym_accumulator(A, 1)).  The form does not fit with no
+ * free LDS word past a window, columns receiving more than 2^22 transposed
+ * terms, or a largest off-diagonal magnitude outside [2^-900, 2^900].  In
+ * deterministic mode (arpack_hip_set_deterministic) on = 1 returns 0 with the
+ * fixed-point form, or keeps the full-storage kernel and returns 1 for an
+ * operator outside it. */
 int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on);
+/* The symmetric kernel's accumulator for A: 0 the fixed-point form where it
+ * fits (default), 1 the LDS fp64 atomics.  -1 on a bad argument.  Takes
+ * effect at the next product; deterministic mode overrides 1. */
+int arpack_hip_csr_set_sym_accumulator(arpack_hip_csr* A, int acc);
+/* The SpMV form A runs now: 0 full storage, 1 symmetric with the fp64
+ * accumulator (not bitwise reproducible), 2 symmetric fixed-point (bitwise). */
+int arpack_hip_csr_sym_form(const arpack_hip_csr* A);
 /* Average device time (ms, hipEvents) of `reps` back-to-back SpMVs. */
 double arpack_hip_csr_time(const arpack_hip_csr* A, const double* x, double* y, int reps);
 /* y = A x on device (x, y device pointers). */

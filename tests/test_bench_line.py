@@ -28,8 +28,8 @@ def _summary(path, workload, kernels):
     path.write_text(json.dumps(doc))
 
 
-def _wl(n, nnz, storage="sym", det=False, w="ns"):
-    return dict(workload=w, n=n, nnz=nnz, storage=storage, deterministic=det)
+def _wl(n, nnz, storage="sym", form="sym_fixed", w="ns"):
+    return dict(workload=w, n=n, nnz=nnz, storage=storage, spmv_form=form)
 
 
 def test_kernel_family():
@@ -51,8 +51,8 @@ def test_traffic_is_keyed_by_workload(tmp_path):
     assert t == 2.8776e9          # the det kernel's family is not k_csr_ssell
     t, src, _ = bench.pmc_traffic({"k_csr_ssell"}, c2, str(tmp_path))
     assert src == "r05w_c23_pmc.json" and t == 5.9559e7
-    t, src, _ = bench.pmc_traffic({"k_csr_ssell_det"}, dict(ns, deterministic=True), str(tmp_path))
-    assert t is None and src is None  # that summary is a default-mode run
+    t, src, _ = bench.pmc_traffic({"k_csr_ssell"}, dict(ns, spmv_form="sym_fp64"), str(tmp_path))
+    assert t is None and src is None  # that summary is the fixed-point accumulator's run
 
 
 def test_traffic_null_with_reason(tmp_path):
@@ -60,7 +60,7 @@ def test_traffic_null_with_reason(tmp_path):
     # a summary without a workload block is never used, whatever it holds
     _summary(tmp_path / "r09_pmc.json", None, {K_SYM: (10, 1.0)})
     # same workload, other storage
-    _summary(tmp_path / "r08_pmc.json", _wl(10_000_000, 510_000_000, storage="full"),
+    _summary(tmp_path / "r08_pmc.json", _wl(10_000_000, 510_000_000, storage="full", form="full"),
              {K_FIN: (10, 5.4e9)})
     t, src, note = bench.pmc_traffic({"k_csr_ssell"}, ns, str(tmp_path))
     assert t is None and src is None
@@ -68,7 +68,7 @@ def test_traffic_null_with_reason(tmp_path):
 
 
 def test_traffic_launch_weighted_over_family(tmp_path):
-    full = _wl(10_000_000, 510_000_000, storage="full")
+    full = _wl(10_000_000, 510_000_000, storage="full", form="full")
     _summary(tmp_path / "r06_pmc.json", full, {K_FIN: (3, 10.0), K_SELL: (1, 30.0)})
     t, src, _ = bench.pmc_traffic({"k_csr_sell", "k_csr_sell_fin"}, full, str(tmp_path))
     assert src == "r06_pmc.json" and t == (3 * 10.0 + 30.0) / 4

@@ -220,14 +220,16 @@ def test_declared_first_then_deterministic_runs_full_storage(pkg):
             ys.append(yd.numpy().copy())
         for y in ys:
             np.testing.assert_array_equal(y.view(np.int64), y_full.view(np.int64))
-        # and a solve through it is bitwise repeatable
+        # and a (capped) solve through it is bitwise repeatable
         v0 = M.dlarnv_uniform(n)[0]
         runs = []
         for _ in range(2):
-            s = pkg.SymRci(n, 4, 20, "LA", 1e-10, mxiter=300, device=True, v0=v0)
-            assert s.aupd_csr(A) == 99 and int(s.info[0]) == 0
-            runs.append(s.eupd(rvec=False)[0].copy())
-        np.testing.assert_array_equal(runs[0], runs[1])
+            s = pkg.SymRci(n, 4, 20, "LA", 1e-10, mxiter=20, device=True, v0=v0)
+            assert s.aupd_csr(A) == 99 and int(s.info[0]) in (0, 1)
+            o5 = int(s.ipntr[5]) - 1
+            runs.append((int(s.iparam[2]), int(s.iparam[8]), s.workl[o5:o5 + 20].copy()))
+        assert runs[0][:2] == runs[1][:2]
+        np.testing.assert_array_equal(runs[0][2], runs[1][2])
     finally:
         pkg.set_deterministic(False)
     A.matvec_device(xd, yd)  # the symmetric kernel again: SciPy's product to rounding

@@ -100,12 +100,15 @@ def test_dnaupd_generalized_on_device(pkg, golden, name):
 
 def test_dnaupd_gen_rejects_symmetric_only_modes(pkg):
     """dnaupd takes the operator pair in modes 2 and 3 only: a pair made for
-    the buckling (4) or Cayley (5) transformation gives info = -11."""
+    the buckling transformation in dnaupd's mode 4 (its complex-shift mode)
+    gives info = -11; mode 5 is no dnaupd mode at all: -10, the reference's
+    code (SRC/dnaupd.f:275, 520)."""
     A, Mm = modes.convdiff1d(50, 10.0)
-    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), 5, 1.0, method=2)
-    s = pkg.NsRci(50, 4, 12, "LM", 1e-10, bmat="G", mode=5, device=True, v0=np.ones(50))
-    assert s.aupd_gen(G) == 99
-    assert int(s.info[0]) == -11
+    for mode, info in ((4, -11), (5, -10)):
+        G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), mode, 1.0, method=2)
+        s = pkg.NsRci(50, 4, 12, "LM", 1e-10, bmat="G", mode=mode, device=True, v0=np.ones(50))
+        assert s.aupd_gen(G) == 99
+        assert int(s.info[0]) == info, (mode, int(s.info[0]))
 
 
 def test_dgen_rejects_mismatch(pkg):

@@ -32,15 +32,26 @@ def _hook(pkg):
     return f
 
 
-def test_fused_handoff_every_word_under_uneven_load(pkg):
+@pytest.mark.parametrize("acc", ["fp64", "fixed"])
+def test_fused_handoff_every_word_under_uneven_load(pkg, acc):
+    """Both accumulators share the walk and the hand-off: fp64 -- the fused and
+    unfused forms differ by the LDS order (64 eps (|A||x|) a row); fixed point
+    -- they must be bitwise equal."""
     A = pkg.CSR.banded_sym(N, 99, BAND, PER_ROW)
     rp, col, val = A.download()
     A.set_symmetric(True)
+    A.set_sym_accumulator(acc)
     assert A.symmetric
     import scipy.sparse as sp
     S = sp.csr_matrix((val, col, rp), shape=(N, N))
     x = np.random.default_rng(8).standard_normal(N)
     bound = 64 * np.finfo(float).eps * (abs(S) @ np.abs(x))
+    ref_bound = bound
+    if acc == "fixed":  # against SciPy: + the fixed-point rounding; fused vs unfused: bitwise
+        rows_ = np.repeat(np.arange(N), np.diff(rp))
+        up = col > rows_
+        L = int(np.bincount(col[up], minlength=N).max())
+        ref_bound = bound + (L + 1) * 2.0 ** -50 * float(np.abs(val[up]).max()) * np.abs(x).max()
     xd = pkg.DeviceBuffer.from_numpy(x)
     load = pkg.DeviceBuffer(256 * 1024 * 1024 // 8)  # a 256 MB read / write stream
     f = _hook(pkg)
@@ -53,14 +64,17 @@ def test_fused_handoff_every_word_under_uneven_load(pkg):
     rows = np.concatenate([np.arange(heads[2 * k], heads[2 * k] + heads[2 * k + 1])
                            for k in range(nh)])
     assert len(rows) > 0.1 * N  # the NS-like band: most chain-head rows are combined
-    # the unfused form is SciPy's product to the LDS-order rounding
-    assert np.all(np.abs(y_split - S @ x) <= bound)
+    # the unfused form is SciPy's product to the LDS-order (fixed point: its) rounding
+    assert np.all(np.abs(y_split - S @ x) <= ref_bound)
     yf = pkg.DeviceBuffer(N)
     for rep in range(REPS):
         pkg.lib().arpack_hip_memset(yf.ptr, 0xFF, 8 * N)  # NaN: an unwritten row cannot pass
         rc = f(A.h, xd.ptr, yf.ptr, 1, load.ptr, load.n, heads.ctypes.data, 4096, None)
         assert rc == nh, rc
         y = yf.numpy()
+        if acc == "fixed":
+            np.testing.assert_array_equal(y.view(np.int64), y_split.view(np.int64))
+            continue
         bad = ~(np.abs(y - y_split) <= bound)
         assert not bad.any(), (rep, int(bad.sum()), np.flatnonzero(bad)[:8])
     # sensitivity: a stale (zero) slot half on the head rows is caught

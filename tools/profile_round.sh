@@ -28,7 +28,8 @@ line = [l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1]
 d = json.loads(line)
 c = d["config"]
 print(json.dumps(dict(workload=c.get("workload_key", "ns"), n=c["n"], nnz=c["nnz"],
-                      storage=d["storage"], deterministic=bool(c.get("deterministic_mode")),
+                      storage=d["storage"], spmv_form=c.get("spmv_form"),
+                      deterministic=bool(c.get("deterministic_mode")),
                       command="python3 " + sys.argv[2].replace(sys.argv[2].split()[0], "bench.py", 1))))
 EOF
 ) || exit 1

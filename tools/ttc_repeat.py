@@ -3,11 +3,11 @@ case: NS operator n = 1e7, LA, nev 10, ncv 30, tol 1e-6, start vector = the
 reference's first dlarnv draw), repeated R times in one process with each SpMV
 storage:
 
-  sym   the bench default: upper-triangle SpMV whose transposed terms land in
-        LDS in wave-schedule order -- y reproducible to rounding, not bitwise;
-  full  SELL-64 full storage, bitwise SciPy's csr_matvec: bitwise reproducible;
-  sym_det  deterministic mode's upper-triangle SpMV (k_csr_ssell_det: the
-        transposed terms as 64-bit fixed-point sums): bitwise reproducible.
+  sym   the bench default (since round 6): upper-triangle SpMV with the
+        transposed terms as 64-bit fixed-point sums -- bitwise reproducible;
+  sym_fp64  the same kernel with the LDS fp64 accumulator: the transposed terms
+        land in wave-schedule order -- y reproducible to rounding, not bitwise;
+  full  SELL-64 full storage, bitwise SciPy's csr_matvec: bitwise reproducible.
 
 Reported per storage: restart cycles and OP*x of every run, the largest spread
 of each Ritz value across the runs (relative), and, for sym, the largest
@@ -42,9 +42,10 @@ def main():
                                     v0.ctypes.data_as(pkg.C.POINTER(pkg.C.c_double)))
     out = {}
     ref = None
-    for storage in ("full", "sym", "sym_det"):
-        pkg.set_deterministic(storage == "sym_det")
+    for storage in ("full", "sym", "sym_fp64"):
         A.set_symmetric(storage != "full")
+        if storage != "full":
+            A.set_sym_accumulator("fp64" if storage == "sym_fp64" else "fixed")
         runs, ds = [], []
         for _ in range(a.repeats):
             s = pkg.SymRci(n, 10, 30, "LA", 1e-6, mxiter=300, device=True, v0=v0)
@@ -60,7 +61,7 @@ def main():
             del s
         D = np.array(ds)
         spread = float(np.max((D.max(0) - D.min(0)) / np.abs(D).max(0)))
-        rec = dict(runs=runs, ritz_spread_rel=spread,
+        rec = dict(runs=runs, ritz_spread_rel=spread, spmv_form=A.sym_form,
                    cycles_distinct=sorted({r["cycles"] for r in runs}),
                    bitwise_identical=bool(np.all(D.view(np.int64) == D[0].view(np.int64))),
                    seconds_median=float(np.median([r["seconds"] for r in runs])))
@@ -70,7 +71,6 @@ def main():
             rec["max_rel_diff_to_full"] = float(np.max(np.abs(D - ref) / np.abs(ref)))
         out[storage] = rec
         print(json.dumps({storage: rec}), file=sys.stderr, flush=True)
-    pkg.set_deterministic(False)
     out["ritz_full"] = [float(x) for x in ref]
     print(json.dumps(out), flush=True)
 
