@@ -135,13 +135,20 @@ constexpr int kTileU = 4;        // entries a lane keeps in flight
 //    them, and every segment is padded to whole chunks with zero values (both
 //    at the segment's own columns; built only where they stay below 3% of the
 //    entries, ztile_pack).
+// Inclusive scan over the 64 lanes in DPP moves (VALU only: the first form,
+// six __shfl_up's a scan, went through LDS beside the tile's LDS atomics and
+// made the packed product 5% SLOWER than the 20-B one, profiles/r06c):
+// Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8), then row 0's
+// total into row 1 and row 2's into row 3 (row_bcast:15), then the first two
+// rows' total into rows 2 and 3 (row_bcast:31).  Lanes without a source keep
+// `old` = 0 (bound_ctrl off); rows outside a move's row mask add 0.
 __device__ __forceinline__ int wave_iscan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -159,7 +166,9 @@ __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ i
             id[u] = __builtin_nontemporal_load(static_cast<const uint16_t*>(idx) + e + u * 256);
             const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
             v[u] = make_double2(w.x, w.y);
-            cb[u] = cbase[(e + u * 256) >> 6];
+            // one base a wave: the chunk index is wave-uniform (a segment
+            // starts on a chunk, a wave loads one whole chunk), so a scalar load
+            cb[u] = cbase[__builtin_amdgcn_readfirstlane((int)((e + u * 256) >> 6))];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
