@@ -50,7 +50,11 @@ def _comm_profile_ok(d, ranks):
         assert 2.0 <= r["allreduce_per_step"] <= 3.0, r
         assert r["allreduce_us_per_step"] > 0 and r["halo_us_per_step"] >= 0
         assert r["kernels_us_per_step"] > 0
-    assert 0.0 < cp["comm_share"] < 1.0
+    # (a rehearsal's host-staged spans hold host round trips and the other
+    # ranks' waits, measured in the profiled cycles: the share may exceed 1)
+    assert cp["comm_share"] > 0.0
+    if d["rccl_ranks"] > 0:
+        assert cp["comm_share"] < 1.0
 
 
 def test_two_ranks_one_json_line():
