@@ -121,7 +121,7 @@ __global__ void k_zsplit_combine(int64_t n, const double2* __restrict__ yp, doub
 // as the slice's partial y: 0.226 ms, same results to 5e-16 (the LDS adds land
 // in schedule order, so y is reproducible to rounding, not bitwise).
 constexpr int kTileRows = 4096;  // 64 KB of LDS row sums: two blocks a CU
-constexpr int kTileU = 4;        // entries a lane keeps in flight
+constexpr int kTileU = 4;        // entries a lane keeps in flight (default; AHIP_ZTILE_U=8 for A/B)
 
 // Two encodings of a tile's column-sorted entries (segment q = slice * nrb +
 // row block: entries [seg[q], seg[q + 1])):
@@ -195,21 +195,21 @@ __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ i
 // gathers of the slice, then add(row, re, im) per entry (LDS row sums).  A
 // packed segment's length is a multiple of 64, so the tail loop's condition is
 // uniform across a wave (its scan needs every lane).
-template <bool PK, class Add>
+template <bool PK, int TU, class Add>
 __device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __restrict__ idx,
                                           const int32_t* __restrict__ cbase,
                                           const double2* __restrict__ val, const double2* __restrict__ xs,
                                           Add add) {
     int64_t e = e0 + threadIdx.x;
-    for (; e + (kTileU - 1) * 256 < e1; e += kTileU * 256) {
-        int row[kTileU], col[kTileU];
-        double2 v[kTileU];
-        tile_batch<PK, kTileU>(e, idx, cbase, val, row, col, v);
-        double2 xv[kTileU];
+    for (; e + (TU - 1) * 256 < e1; e += TU * 256) {
+        int row[TU], col[TU];
+        double2 v[TU];
+        tile_batch<PK, TU>(e, idx, cbase, val, row, col, v);
+        double2 xv[TU];
 #pragma unroll
-        for (int u = 0; u < kTileU; ++u) xv[u] = xs[col[u]];
+        for (int u = 0; u < TU; ++u) xv[u] = xs[col[u]];
 #pragma unroll
-        for (int u = 0; u < kTileU; ++u)
+        for (int u = 0; u < TU; ++u)
             add(row[u], v[u].x * xv[u].x - v[u].y * xv[u].y, v[u].x * xv[u].y + v[u].y * xv[u].x);
     }
     for (; e < e1; e += 256) {
@@ -221,7 +221,7 @@ __device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __
     }
 }
 
-template <int S, bool PK>
+template <int S, bool PK, int TU = kTileU>
 __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
                                                int64_t nrb, const void* __restrict__ idx,
                                                const int32_t* __restrict__ cbase,
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int6
     for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
     __syncthreads();
     const int64_t q = s * nrb + rb;
-    tile_walk<PK>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
+    tile_walk<PK, TU>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
                   [&](int r, double re, double im) {
                       atomicAdd(&ylds[2 * r], re);
                       atomicAdd(&ylds[2 * r + 1], im);
@@ -259,7 +259,7 @@ static_assert(kZMaxBlocks == 256, "k_ztile_det reduces one block maximum a threa
 // wave order; y_s = (double)(sum q) 2^(E-B).  B = min(51, 62 - bits(L)) for at
 // most L entries a row in a slice.  The slice partials are summed in
 // zc::slice_sum's fixed order as before.
-template <int S, bool PK>
+template <int S, bool PK, int TU = kTileU>
 __global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
                                                    int64_t nrb, const void* __restrict__ idx,
                                                    const int32_t* __restrict__ cbase,
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const 
         const double f = fma(p, inv, kMagic);
         return (unsigned long long)__double_as_longlong(f) - kMagicBits;
     };
-    tile_walk<PK>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
+    tile_walk<PK, TU>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
                   [&](int r, double re, double im) {
                       atomicAdd(&ylds[2 * r], q64(re));
                       atomicAdd(&ylds[2 * r + 1], q64(im));
@@ -783,6 +783,15 @@ int zcsr_build_split(ZCsr& A) {
 }
 
 namespace {
+// AHIP_ZTILE_U=8: the packed tile walk keeps 8 entries a lane in flight (A/B)
+int tile_u() {
+    static const int u = [] {
+        const char* e = getenv("AHIP_ZTILE_U");
+        return e && e[0] == '8' ? 8 : kTileU;
+    }();
+    return u;
+}
+
 template <int S>
 void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp, const int* gate) {
     const dim3 tg((unsigned)(S * A.t_nrb)), tb(256);
@@ -791,7 +800,7 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
                                (const double2*)A.t_val, x2, yp, gate);
         };
-        if (A.t_pk) go(k_ztile<S, true>);
+        if (A.t_pk) tile_u() == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
         else go(k_ztile<S, false>);
         return;
     }

@@ -17,5 +17,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -- python3 $
     > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -- python3 $ARGS \
     > "$OUT/write.log" 2>&1 || exit $?
-python3 "$ROOT/tools/pmc_summary.py" "$OUT/fetch" "$OUT/write" "$OUT/trace" > "$OUT/pmc.json" &&
+python3 "$ROOT/tools/pmc_summary.py" --workload "{\"workload\": \"c5_mode3\", \"n\": 500000, \"command\": \"python3 tools/c5_mode3.py --cycles 2\"}" "$OUT/fetch" "$OUT/write" "$OUT/trace" > "$OUT/pmc.json" &&
 python3 "$ROOT/tools/pmc_summary.py" --stats "$OUT/trace" > "$OUT/kernel_stats.csv"
