@@ -405,6 +405,8 @@ int arpack_hip_csr_set_symmetric(arpack_hip_csr* A, int on) {
     // fixed-order full-storage SpMV stays, reported as kept (1) on every rank
     const bool det = A->A.ss_det != 0;
     A->A.ss_det_all = (c ? ahip::dist_all_ok(c, det) : det) ? 1 : 0;
+    const bool fx = A->A.ss_fx_ok != 0;
+    A->A.ss_fx_all = (c ? ahip::dist_all_ok(c, fx) : fx) ? 1 : 0;
     if (ahip::deterministic() && !A->A.ss_det_all) {
         csr_full_storage(A);
         return 1;
@@ -430,7 +432,7 @@ int arpack_hip_csr_set_sym_accumulator(arpack_hip_csr* A, int acc) {
 int arpack_hip_csr_sym_form(const arpack_hip_csr* A) {
     const ahip::dev::Csr& M = A->A;
     if (M.kernel != ahip::dev::kCsrSymSell || !M.ss_val || ahip::dev::csr_sym_det_fallback(M)) return 0;
-    return M.ss_det_all && (M.ss_acc == 0 || ahip::deterministic()) ? 2 : 1;
+    return M.ss_det_all && ((M.ss_acc == 0 && M.ss_fx_all) || ahip::deterministic()) ? 2 : 1;
 }
 
 int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile) {

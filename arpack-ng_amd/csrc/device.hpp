@@ -346,6 +346,12 @@ struct Csr {
     // fp64 atomics (schedule order; arpack_hip_csr_set_sym_accumulator).
     // Deterministic mode always takes the fixed-point form.
     int ss_acc = 0;
+    // the fixed-point form as the DEFAULT accumulator also needs the upper
+    // off-diagonal magnitudes within 2^20 of each other (ss_fx_ok; on every
+    // rank: ss_fx_all) -- a graded operator keeps the fp64 form unless
+    // deterministic mode asks for the fixed-point one
+    int ss_fx_ok = 0;
+    int ss_fx_all = 0;
     int ss_detq = 0;  // most slices one wave walks in a superblock
 };
 enum CsrKernel : int {

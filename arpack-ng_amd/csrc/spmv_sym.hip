@@ -63,8 +63,10 @@ __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict
                               const int32_t* __restrict__ col, const double* __restrict__ val,
                               int32_t* __restrict__ cnt, int32_t* __restrict__ cmax,
                               unsigned long long* __restrict__ amax, int32_t* __restrict__ ccol) {
+    // amax[0]: the largest |a_ij| above the diagonal; amax[1]: the smallest
+    // nonzero one (both as the bits of non-negative doubles)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    double am = 0.0;
+    double am = 0.0, an = DBL_MAX;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         int32_t c = 0, m = (int32_t)i, low = 0;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
@@ -73,7 +75,9 @@ __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict
                 ++c;
                 m = max(m, j);
                 if (j > i) {
-                    am = fmax(am, fabs(val[k]));
+                    const double a = fabs(val[k]);
+                    am = fmax(am, a);
+                    if (a > 0.0) an = fmin(an, a);
                     atomicAdd(&ccol[j], 1);
                 }
             }
@@ -82,8 +86,14 @@ __global__ void k_upper_stats(int64_t n, int64_t coff, const int64_t* __restrict
         cnt[i] = c | (low << 30);
         cmax[i] = m;
     }
-    for (int o = 32; o > 0; o >>= 1) am = fmax(am, __shfl_xor(am, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(amax, (unsigned long long)__double_as_longlong(am));
+    for (int o = 32; o > 0; o >>= 1) {
+        am = fmax(am, __shfl_xor(am, o, 64));
+        an = fmin(an, __shfl_xor(an, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(amax, (unsigned long long)__double_as_longlong(am));
+        atomicMin(amax + 1, (unsigned long long)__double_as_longlong(an));
+    }
 }
 
 // one 64-thread block per slice, lane = row: the row's upper entries in CSR
@@ -754,7 +764,7 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     if (ncols != coff + n + spill_out || n <= 0 || ncols >= (int64_t)INT32_MAX) return -1;
     const int64_t nc = n + spill_out;  // columns that receive transposed terms
     int32_t *dcnt = nullptr, *dcm = nullptr, *dcc = nullptr;
-    unsigned long long* dst = nullptr;  // amax bits
+    unsigned long long* dst = nullptr;  // amax, amin bits
     auto free_all = [&]() {
         (void)hipFree(dcnt);
         (void)hipFree(dcm);
@@ -764,24 +774,26 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
     if (fault_filter(hipMalloc(&dcnt, sizeof(int32_t) * n)) != hipSuccess ||
         fault_filter(hipMalloc(&dcm, sizeof(int32_t) * n)) != hipSuccess ||
         fault_filter(hipMalloc(&dcc, sizeof(int32_t) * nc)) != hipSuccess ||
-        fault_filter(hipMalloc(&dst, sizeof(unsigned long long))) != hipSuccess) {
+        fault_filter(hipMalloc(&dst, 2 * sizeof(unsigned long long))) != hipSuccess) {
         free_all();
         return -2;
     }
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
-    bool got = fault_filter(hipMemset(dst, 0, sizeof(unsigned long long))) == hipSuccess &&
+    const unsigned long long init[2] = {0ull, (unsigned long long)0x7fefffffffffffffll};  // 0, DBL_MAX
+    bool got = fault_filter(hipMemcpy(dst, init, sizeof(init), hipMemcpyHostToDevice)) == hipSuccess &&
                fault_filter(hipMemset(dcc, 0, sizeof(int32_t) * nc)) == hipSuccess;
     if (got)
         AHIP_LAUNCH(k_upper_stats, dim3((unsigned)g), dim3(256), 0, nullptr, n, coff, A.rowptr, A.col,
                     A.val, dcnt, dcm, dst, dcc);
     std::vector<int32_t> cnt(n), cm(n), ccol(nc);
-    unsigned long long hst[2] = {0, 0};
+    unsigned long long hst[2] = {0, 0}, hmin = 0;
     got = got &&
           fault_filter(hipMemcpy(cnt.data(), dcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
           fault_filter(hipMemcpy(cm.data(), dcm, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) == hipSuccess &&
           fault_filter(hipMemcpy(ccol.data(), dcc, sizeof(int32_t) * nc, hipMemcpyDeviceToHost)) == hipSuccess &&
-          fault_filter(hipMemcpy(hst, dst, sizeof(unsigned long long), hipMemcpyDeviceToHost)) == hipSuccess;
+          fault_filter(hipMemcpy(hst, dst, sizeof(unsigned long long), hipMemcpyDeviceToHost)) == hipSuccess &&
+          fault_filter(hipMemcpy(&hmin, dst + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost)) == hipSuccess;
     free_all();
     if (!got) return -2;
     // the most transposed terms one word sums (per column, not the
@@ -947,6 +959,14 @@ int csr_build_symsell(Csr& A, int64_t ncols, int64_t coff, int64_t spill_in, int
         A.ss_bits = std::min(51, 62 - hb);
         const bool scaled = amax == 0.0 || (amax >= 0x1p-900 && amax <= 0x1p900);  // (NaN: no)
         A.ss_det = (maxspan <= kSymWin - 1 && A.ss_bits >= 40 && scaled) ? 1 : 0;
+        // the DEFAULT accumulator takes the fixed-point form only where the
+        // off-diagonal magnitudes span <= 2^20: every term is then rounded to
+        // <= 2^-31 of the smallest entry's product with the window's max|x|
+        // (a graded operator's small entries keep the fp64 form's
+        // relative accuracy; deterministic mode takes the form regardless)
+        double amin;
+        std::memcpy(&amin, &hmin, sizeof amin);
+        A.ss_fx_ok = A.ss_det && (amax == 0.0 || amax <= 0x1p20 * amin) ? 1 : 0;
         int64_t ms = 0;
         for (int64_t b = 0; b < nsb; ++b) ms = std::max<int64_t>(ms, slice0[b + 1] - slice0[b]);
         A.ss_detq = (int)((ms + NW - 1) / NW);
@@ -969,7 +989,9 @@ static bool spmv_ynt() {
 // the fixed-point form wherever it serves the operator on every rank: by
 // default, or always in deterministic mode (an operator outside the form runs
 // the LDS fp64 form by default, the full-storage kernel in deterministic mode)
-static bool sym_det(const Csr& A) { return A.ss_det_all && (A.ss_acc == 0 || deterministic()); }
+static bool sym_det(const Csr& A) {
+    return A.ss_det_all && ((A.ss_acc == 0 && A.ss_fx_all) || deterministic());
+}
 // AHIP_HANDOFF=2: the fused chain-head hand-off in the memory model's acq_rel
 // form instead of the measured sc1 form (k_csr_ssell FUSE = 2 vs 1, A/B)
 static int handoff_form() {

@@ -239,7 +239,9 @@ int arpack_hip_csr_set_kernel(arpack_hip_csr* A, int kernel, int tile);
  * destroyed.  The transposed terms are summed in the kernel's fixed-point
  * form (exact 64-bit integers: y bitwise reproducible, each term rounded to
  * 2^-51 of the window's largest |a_ij| max|x|) wherever the operator fits it
- * on every rank -- the default since round 6 -- else as LDS fp64 atomics in
+ * on every rank and its upper off-diagonal magnitudes span at most 2^20 -- the
+ * default since round 6 -- else (a graded operator, unless deterministic mode
+ * asks for the fixed-point form) as LDS fp64 atomics in
  * schedule order (y reproducible to ~1 ulp, not bitwise; also selected by
  * arpack_hip_csr_set_sym_accumulator(A, 1)).  The form does not fit with no
  * free LDS word past a window, columns receiving more than 2^22 transposed

@@ -196,3 +196,33 @@ def test_symmetric_storage_run_to_run(pkg, acc):
     if acc == "fixed":
         for c, o, d in res["sym"][1:]:
             np.testing.assert_array_equal(d, res["sym"][0][2])
+
+
+def test_graded_operator_keeps_fp64_accumulator(pkg):
+    """the fixed-point form rounds every transposed term to 2^-51 of
+    the window's largest product, so the DEFAULT accumulator takes it only when
+    the upper off-diagonal magnitudes span at most 2^20.  A graded operator
+    (D A D with D over twelve decades) keeps the fp64 form, whose small rows
+    stay accurate relative to their own terms; deterministic mode still takes
+    the fixed-point form, and the products meet their bounds."""
+    import scipy.sparse as sp
+    rp, col, val = _mat(("banded_sym", 20000, 7, 256, 9))
+    n = len(rp) - 1
+    d = 10.0 ** np.linspace(-12, 0, n)
+    S = sp.diags(d) @ M.to_scipy(rp, col, val) @ sp.diags(d)
+    S = sp.csr_matrix(S)
+    S.sort_indices()
+    grp, gcol, gval = S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data
+    x = np.random.default_rng(5).standard_normal(n)
+    y, Ad = _spmv_sym(pkg, grp, gcol, gval, x)
+    assert Ad.sym_form == "sym_fp64"
+    _close(grp, gcol, gval, x, y, "fp64")
+    pkg.set_deterministic(True)
+    try:
+        Ad.set_symmetric(True)
+        assert Ad.sym_form == "sym_fixed"
+        xd, yd = pkg.DeviceBuffer.from_numpy(x), pkg.DeviceBuffer(n)
+        Ad.matvec_device(xd.at(0), yd.at(0))
+        _close(grp, gcol, gval, x, yd.numpy(), "fixed")
+    finally:
+        pkg.set_deterministic(False)

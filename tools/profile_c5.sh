@@ -18,4 +18,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -- python3 $
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -- python3 $ARGS \
     > "$OUT/write.log" 2>&1 || exit $?
 python3 "$ROOT/tools/pmc_summary.py" --workload "{\"workload\": \"c5_mode3\", \"n\": 500000, \"command\": \"python3 tools/c5_mode3.py --cycles 2\"}" "$OUT/fetch" "$OUT/write" "$OUT/trace" > "$OUT/pmc.json" &&
-python3 "$ROOT/tools/pmc_summary.py" --stats "$OUT/trace" > "$OUT/kernel_stats.csv"
+python3 "$ROOT/tools/pmc_summary.py" --stats "$OUT/trace" > "$OUT/kernel_stats.csv" &&
+# the raw rocprofv3 output stays on the box (gpurun_out/ travels back only below 64 MiB)
+rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write"

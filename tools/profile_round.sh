@@ -34,4 +34,6 @@ print(json.dumps(dict(workload=c.get("workload_key", "ns"), n=c["n"], nnz=c["nnz
 EOF
 ) || exit 1
 python3 "$ROOT/tools/pmc_summary.py" --workload "$WL" "$OUT/fetch" "$OUT/write" "$OUT/trace" > "$OUT/pmc.json" &&
-python3 "$ROOT/tools/pmc_summary.py" --stats "$OUT/trace" > "$OUT/kernel_stats.csv"
+python3 "$ROOT/tools/pmc_summary.py" --stats "$OUT/trace" > "$OUT/kernel_stats.csv" &&
+# the raw rocprofv3 output stays on the box (gpurun_out/ travels back only below 64 MiB)
+rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write"
