@@ -785,8 +785,9 @@ class DShift:
 
     def __init__(self, A: "CSR", sigma=0.0, rtol=1e-12, maxit=1000, method="cg"):
         """method: "cg" (A - sigma I positive definite), "minres" (any symmetric
-        A - sigma I, e.g. sigma inside the spectrum) or "bicgstab" (a nonsymmetric
-        A: dnaupd's real shift-invert)."""
+        A - sigma I, e.g. sigma inside the spectrum), "bicgstab" (a nonsymmetric
+        A: dnaupd's real shift-invert) or "tridiag" (a direct solve of a
+        tridiagonal A - sigma I: dgttrf + device scans)."""
         self.A = A  # keeps the operator alive
         self.sigma = float(sigma)
         h = C.c_void_p()
@@ -795,8 +796,8 @@ class DShift:
             raise RuntimeError("arpack_hip_dshift_create failed (%d)" % rc)
         self.h = h.value
         self.n = A.n
-        if lib().arpack_hip_dshift_set_method(self.h, {"cg": 0, "minres": 1,
-                                                       "bicgstab": 2}[method]) != 0:
+        if lib().arpack_hip_dshift_set_method(self.h, {"cg": 0, "minres": 1, "bicgstab": 2,
+                                                       "tridiag": 3}[method]) != 0:
             raise ValueError(method)
 
     def __del__(self):

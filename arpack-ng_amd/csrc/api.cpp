@@ -167,7 +167,9 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
             if (dist || bmat[0] != 'G' || mode != gen->mode || gen->n != n ||
                 (ns && mode != 2 && mode != 3))
                 ierr = (ierr ? ierr : -11);
-        } else if (csr && ((shift ? mode != 3 || dist || (ns && shift->method != dev::kDShiftBicgstab)
+        } else if (csr && ((shift ? mode != 3 || dist ||
+                                        (ns && shift->method != dev::kDShiftBicgstab &&
+                                         shift->method != dev::kDShiftTridiag)
                                   : mode != 1) ||
                            bmat[0] != 'I' || csr->n != n)) {
             ierr = (ierr ? ierr : -11);
@@ -534,7 +536,7 @@ struct arpack_hip_dgen {
 int arpack_hip_dgen_create(arpack_hip_dgen** out, const arpack_hip_csr* A, const arpack_hip_csr* B,
                            int mode, double sigma, double rtol, int maxit, int method) {
     if (!out || !(rtol > 0.0) || maxit < 1 || method < ahip::dev::kDShiftCg ||
-        method > ahip::dev::kDShiftBicgstab)
+        method > ahip::dev::kDShiftTridiag)
         return -1;
     auto* D = new arpack_hip_dgen;
     const int rc = ahip::dev::dgen_create(D->G, A, B, mode, sigma, rtol, maxit, method);
@@ -605,7 +607,9 @@ int arpack_hip_dshift_create(arpack_hip_dshift** out, const arpack_hip_csr* A, d
 }
 
 int arpack_hip_dshift_set_method(arpack_hip_dshift* D, int method) {
-    if (!D || method < ahip::dev::kDShiftCg || method > ahip::dev::kDShiftBicgstab) return -1;
+    if (!D || method < ahip::dev::kDShiftCg || method > ahip::dev::kDShiftTridiag) return -1;
+    ahip::dev::dshift_tridiag_free(D->S);
+    if (method == ahip::dev::kDShiftTridiag && ahip::dev::dshift_tridiag_factor(D->S) != 0) return -1;
     D->S.method = method;
     D->S.chunk = 8;  // the previous method's iteration count says nothing here
     return 0;

@@ -112,6 +112,10 @@ int dgen_create(DGen& G, const arpack_hip_csr* A, const arpack_hip_csr* B, int m
         return -2;
     }
     G.S.method = method;
+    if (method == kDShiftTridiag && dshift_tridiag_factor(G.S) != 0) {  // C tridiagonal: direct
+        dgen_destroy(G);
+        return -1;
+    }
     if (hipMalloc(&G.t, sizeof(double) * 2 * (size_t)na) != hipSuccess) {
         G.t = nullptr;
         dgen_destroy(G);

@@ -459,6 +459,7 @@ int dshift_create(DShift& S, const Csr* A, double sigma, double rtol, int maxit)
 }
 
 void dshift_destroy(DShift& S) {
+    dshift_tridiag_free(S);
     for (double* q : S.vec)
         if (q) (void)hipFree(q);
     if (S.part) (void)hipFree(S.part);
@@ -477,10 +478,26 @@ double dshift_iter_bytes(const DShift& S) {
     // BiCGStab: two products and 18 passes -- k_bs_v (w, p, rh; v), k_bs_s (r, v; s),
     // k_bs_t (w, s; t), k_bs_xr (x, p, s, t, rh; x, r), k_bs_p (r, p, v; p)
     if (S.method == kDShiftBicgstab) return 2.0 * csr_bytes(*S.A) + 144.0 * (double)S.n;
+    // the direct solve: each scan reads its factor rows twice (segment
+    // composites, then the re-application) -- forward dl, ipiv, b (20 B) and
+    // y written, backward d, du, du2, y (32 B) and x written
+    if (S.method == kDShiftTridiag) return 2.0 * 20.0 * S.n + 8.0 * S.n + 2.0 * 32.0 * S.n + 8.0 * S.n;
     return csr_bytes(*S.A) + (S.method == kDShiftMinres ? 128.0 : 88.0) * (double)S.n;
 }
 
 int dshift_apply(DShift& S, hipStream_t strm, const double* b, double* y, double* relres) {
+    if (S.method == kDShiftTridiag) {  // the direct solve: no iterations, no residual estimate
+        if (!S.tri_d || hipEventRecord(S.ev0, strm) != hipSuccess ||
+            dshift_tridiag_apply(S, strm, b, y) != 0 || hipEventRecord(S.ev1, strm) != hipSuccess ||
+            hipEventSynchronize(S.ev1) != hipSuccess)
+            return -2;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, S.ev0, S.ev1) == hipSuccess) S.ms_total += ms;
+        if (relres) *relres = 0.0;
+        S.n_solves += 1;
+        S.n_iters += 1;
+        return 1;
+    }
     const int64_t n = S.n;
     const int nb = S.nblk;
     double* P0 = S.part;

@@ -49,7 +49,10 @@ struct CgState {
 
 // CG: A - sigma I symmetric positive definite; MINRES: symmetric; BiCGStab:
 // general (dnaupd's real shift-invert)
-enum DShiftMethod { kDShiftCg = 0, kDShiftMinres = 1, kDShiftBicgstab = 2 };
+// Tridiag: a direct solve (dgttrf on the host once, the triangular solves as
+// device scans, dtri.hip) for a tridiagonal A - sigma I -- the operators a
+// Krylov solve cannot serve (dndrv2's non-normal convection-diffusion)
+enum DShiftMethod { kDShiftCg = 0, kDShiftMinres = 1, kDShiftBicgstab = 2, kDShiftTridiag = 3 };
 
 struct DShift {
     const Csr* A = nullptr;
@@ -69,6 +72,12 @@ struct DShift {
     double max_relres = 0.0;
     double ms_total = 0.0;  // device time of the solves (hipEvents)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // kDShiftTridiag: the LU factors (dgttrf layout, 0-based pivots) and the
+    // scans' block composites / carries
+    double *tri_dl = nullptr, *tri_d = nullptr, *tri_du = nullptr, *tri_du2 = nullptr;
+    int* tri_ipiv = nullptr;
+    void* tri_bc = nullptr;
+    double* tri_cin = nullptr;
 };
 
 // 0, or a hipError_t on allocation failure (nothing leaks)
@@ -80,7 +89,12 @@ void dshift_destroy(DShift& S);
 // then holds the last iterate), -2 on a HIP error.
 int dshift_apply(DShift& S, hipStream_t stream, const double* b, double* y, double* relres);
 // algorithmic HBM bytes of one iteration (the CSR product in its storage and
-// the fused vector passes of the method)
+// the fused vector passes of the method; Tridiag: one direct solve)
 double dshift_iter_bytes(const DShift& S);
+// kDShiftTridiag (dtri.hip): factor A - sigma I (0; -1 not tridiagonal or
+// singular; -2 HIP failure), free the factors, one solve (0 or -2)
+int dshift_tridiag_factor(DShift& S);
+void dshift_tridiag_free(DShift& S);
+int dshift_tridiag_apply(DShift& S, hipStream_t s, const double* b, double* y);
 
 }  // namespace ahip::dev

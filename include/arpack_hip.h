@@ -366,8 +366,12 @@ void arpack_hip_dshift_destroy(arpack_hip_dshift* S);
 /* 0: conjugate gradients (the default; A - sigma I positive definite), 1: MINRES
  * (any symmetric A - sigma I, e.g. sigma inside the spectrum for interior
  * eigenvalues; 16 instead of 11 vector passes an iteration), 2: BiCGStab (a
- * nonsymmetric A: dnaupd's real shift-invert; two products an iteration).
- * 0 or -1. */
+ * nonsymmetric A: dnaupd's real shift-invert; two products an iteration),
+ * 3: a DIRECT solve for a tridiagonal A - sigma I (LAPACK's dgttrf restated,
+ * once on the host; the two triangular solves as device scans of affine maps,
+ * csrc/dtri.hip) -- what the reference's drivers do (EXAMPLES/NONSYM/dndrv2.f,
+ * dsdrv2.f), for operators a Krylov solve cannot serve (dndrv2's).  0, or -1
+ * (unknown method; method 3 with A not tridiagonal or A - sigma I singular). */
 int arpack_hip_dshift_set_method(arpack_hip_dshift* S, int method);
 /* x, y device pointers (y != x); synchronous.  The iterations (>= 0; *relres =
  * ||r||/||x||), -1 on breakdown / missed rtol, -2 on a HIP error. */
