@@ -405,8 +405,9 @@ void arpack_hip_dnaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, i
  *   mode 4  OP = inv[K - sigma KG] K, B = K           A = K, B = KG
  *   mode 5  OP = inv[A - sigma M](A + sigma M), B = M
  * The inverse is a device Krylov solve to relative residual rtol (method 0 CG:
- * positive-definite C; 1 MINRES: indefinite; 2 BiCGStab: nonsymmetric) on
- * C = A - sigma B formed once
+ * positive-definite C; 1 MINRES: indefinite; 2 BiCGStab: nonsymmetric; 3 a
+ * direct tridiagonal solve, dgttrf + device scans, for a tridiagonal C -- the
+ * reference drivers' own dgttrf/dgttrs) on C = A - sigma B formed once
  * entry by entry over the union pattern (mode 2: on M).  Returns 0, -1 for bad
  * arguments, -2 on a HIP failure.  arpack_hip_dsaupd_gen takes dsaupd_c's
  * arguments (bmat 'G', iparam(7) = the operator pair's mode); a solve that

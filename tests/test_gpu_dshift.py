@@ -199,3 +199,64 @@ def test_eigs_real_shift_invert(pkg):
     for k in range(len(d)):
         r = np.linalg.norm(As @ z[:, k] - d[k] * z[:, k])
         assert r <= 1e-9 * an * np.linalg.norm(z[:, k])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 4099, 1_000_003])
+def test_tridiag_direct_solve(pkg, n):
+    """DShift method "tridiag" (csrc/dtri.hip): dgttrf on the host, the two
+    triangular solves as device scans of affine maps -- against SciPy's
+    (LAPACK) dgttrs on a random nonsymmetric tridiagonal that pivots, at sizes
+    that put the segment and block boundaries everywhere (1 .. 10^6 rows)."""
+    import scipy.linalg.lapack as lapack
+    rng = np.random.default_rng(n)
+    dl, d, du = rng.standard_normal(n - 1), rng.standard_normal(n) + 0.5, rng.standard_normal(n - 1)
+    sigma = 0.25
+    A = sp.diags([dl, d, du], [-1, 0, 1], shape=(n, n), format="csr")
+    A.sort_indices()
+    Ad = pkg.CSR.from_arrays(A.indptr, A.indices, A.data)
+    S = pkg.DShift(Ad, sigma, method="tridiag")
+    b = rng.standard_normal(n)
+    y, it, rr = S.solve(b)
+    assert it == 1
+    if n >= 3:
+        f = lapack.dgttrf(dl, d - sigma, du)
+        xr, info = lapack.dgttrs(*f[:5], b)
+        assert info == 0
+    else:
+        xr = np.linalg.solve((A - sigma * sp.identity(n)).toarray(), b)
+    np.testing.assert_allclose(y, xr, rtol=0, atol=1e-10 * np.abs(xr).max())
+    r = (A - sigma * sp.identity(n)) @ y - b
+    assert np.linalg.norm(r) <= 1e-9 * np.linalg.norm(b) * max(1.0, np.abs(xr).max())
+
+
+def test_tridiag_refuses_wider_operator(pkg):
+    """method "tridiag" needs a tridiagonal A: anything wider is refused."""
+    A = pkg.CSR.laplace2d(10)
+    with pytest.raises(ValueError):
+        pkg.DShift(A, 0.0, method="tridiag")
+
+
+def test_dnaupd_mode3_tridiag_m7(pkg, golden):
+    """dndrv2 as the reference runs it (the m7 fixture: A - sigma I factored
+    directly, EXAMPLES/NONSYM/dndrv2.f:197-258) with the device's direct
+    tridiagonal solve as OP: the reference's info, nconv, restart cycles and
+    OP*x, and every eigenvalue of its dneupd within 1e-9 (relative to the
+    largest) of one of ours -- the case BiCGStab cannot serve (above)."""
+    g = golden("m7_ns_std_si")
+    n, sigma = int(g["n"]), float(g["sigma"])
+    c = modes.StdShiftInvert(str(g["kind"]), n, sigma)
+    Acsr = c.A.tocsr()
+    Acsr.sort_indices()
+    A = pkg.CSR.from_arrays(Acsr.indptr, Acsr.indices, Acsr.data)
+    S = pkg.DShift(A, sigma, method="tridiag")
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
+                  mxiter=300, v0=g["v0"], device=True)
+    assert s.aupd_shift(S) == 99
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    assert int(s.iparam[2]) == int(g["iparam"][2]), (int(s.iparam[2]), int(g["iparam"][2]))
+    assert int(s.iparam[8]) == int(g["iparam"][8])
+    dr, di, z, nconv = s.eupd(sigmar=sigma)
+    lam, ref = dr[:nconv] + 1j * di[:nconv], g["dr"] + 1j * g["di"]
+    for x in ref:
+        assert np.abs(lam - x).min() <= 1e-9 * np.abs(ref).max(), (x, lam)

@@ -62,11 +62,11 @@ def test_dsaupd_generalized_on_device(pkg, golden, name):
 # dnaupd (EXAMPLES/NONSYM/dndrv3.f mode 2, dndrv4.f mode 3 with a real shift):
 # A the 1-D convection-diffusion operator, M the FEM mass matrix (SPD).  Mode 2
 # solves with M (CG); mode 3's C = A - sigma M is nonsymmetric (BiCGStab)
-NS_CASES = {"m8_ns_gen": 0, "m9_ns_gen_si": 2}
+NS_CASES = [("m8_ns_gen", 0), ("m9_ns_gen_si", 2), ("m8_ns_gen", 3), ("m9_ns_gen_si", 3)]
 
 
-@pytest.mark.parametrize("name", sorted(NS_CASES))
-def test_dnaupd_generalized_on_device(pkg, golden, name):
+@pytest.mark.parametrize("name,method", NS_CASES)
+def test_dnaupd_generalized_on_device(pkg, golden, name, method):
     """Free-running dnaupd with bmat = 'G' (arpack_hip_dnaupd_gen): the
     reference's info, nconv, restart cycles and OP*x / B*x counts; every
     eigenvalue of the reference's dneupd within 1e-9 (relative to the largest)
@@ -75,7 +75,7 @@ def test_dnaupd_generalized_on_device(pkg, golden, name):
     mode, n, sigma = int(g["mode"]), int(g["n"]), float(g["sigma"])
     A, Mm = modes.convdiff1d(n, 10.0)
     G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), mode, sigma, rtol=1e-13, maxit=50 * n,
-                 method=NS_CASES[name])
+                 method=method)
     s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat="G",
                   mode=mode, mxiter=300, v0=g["v0"], device=True)
     assert s.aupd_gen(G) == 99
