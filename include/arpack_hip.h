@@ -678,6 +678,14 @@ void arpack_hip_kit_dsapps_host(int kev, int np, const double* shift, double* h,
                                 double* q, int ldq);
 void arpack_hip_kit_dlarnv(int* iseed, int n, double* x);
 void arpack_hip_kit_slarnv(int* iseed, int n, float* x); /* slarnv(idist=2), LAPACK slaruv rules */
+/* LAPACK dgttrf / dgttrs (trans 'N', one right-hand side) restated: the host
+ * factor behind arpack_hip_dshift_set_method(S, 3) and its sequential solve
+ * (tests/test_kit_tri.py against the image's LAPACK).  dgttrf returns LAPACK's
+ * info (0, or k > 0 for a zero pivot u(k,k)); ipiv is 0-based (LAPACK's
+ * ipiv minus one). */
+int arpack_hip_kit_dgttrf(int64_t n, double* dl, double* d, double* du, double* du2, int* ipiv);
+void arpack_hip_kit_dgttrs(int64_t n, const double* dl, const double* d, const double* du,
+                           const double* du2, const int* ipiv, double* b);
 /* The device generators behind dgetv0/sgetv0's start vector on a device buffer
  * x (prec 'd': double, 's': float); iseed is advanced like dlarnv/slarnv's. */
 int arpack_hip_larnv_device(char prec, int* iseed, int64_t n, void* x);
