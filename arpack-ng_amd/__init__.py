@@ -864,6 +864,44 @@ class DGen:
         except Exception:
             pass
 
+class ZGen:
+    """Device operator pair of znaupd's generalized modes (bmat = 'G'; modes 2
+    and 3, arpack_hip_zgen_create): mode 2 OP = inv[M] A, mode 3 OP = inv[A -
+    sigma M] M with a complex sigma, B = M.  The inverse is the device BiCGStab
+    to relative residual rtol on C = A - sigma M (mode 2: on M); ZRci.aupd_gen
+    runs the whole loop with it."""
+
+    def __init__(self, A: "ZCSR", M: "ZCSR", mode: int, sigma=0j, rtol: float = 1e-12,
+                 maxit: int = 5000):
+        L = lib()
+        L.arpack_hip_zgen_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_double, C.c_double, C.c_double, C.c_int]
+        L.arpack_hip_zgen_destroy.argtypes = [C.c_void_p]
+        sigma = complex(sigma)
+        h = C.c_void_p()
+        rc = L.arpack_hip_zgen_create(C.byref(h), A.h, M.h, int(mode), sigma.real, sigma.imag,
+                                      float(rtol), int(maxit))
+        if rc != 0:
+            raise RuntimeError(f"arpack_hip_zgen_create failed ({rc})")
+        self.h, self.A, self.M, self.mode, self.sigma = h, A, M, int(mode), sigma
+
+    def stats(self):
+        L = lib()
+        L.arpack_hip_zgen_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_longlong)] * 3 + [_PD]
+        v = [C.c_longlong() for _ in range(3)]
+        r = C.c_double()
+        L.arpack_hip_zgen_stats(self.h, *[C.byref(x) for x in v], C.byref(r))
+        return dict(solves=v[0].value, iters=v[1].value, fails=v[2].value, max_relres=r.value)
+
+    def __del__(self):
+        try:
+            if self.h and _lib is not None:
+                _lib.arpack_hip_zgen_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
 class ZRci:
     """znaupd/zneupd state (SRC/znaupd.f, SRC/zneupd.f): complex128 arrays,
     ipntr(14), lworkl = 3*ncv^2 + 5*ncv, rwork(ncv).  Host arrays; the caller
@@ -923,6 +961,22 @@ class ZRci:
                                        self.n, _ip(self.iparam), _ip(self.ipntr),
                                        self.workd.ctypes.data, self.workl.ctypes.data,
                                        self.lworkl, self.rwork.ctypes.data, _ip(self.info))
+        self.tol = tol.value
+        return int(self.ido[0])
+
+    def aupd_gen(self, G: "ZGen"):
+        """Whole loop on the GPU in znaupd's generalized modes (construct with
+        bmat="G" and G's mode): OP*x and B*x by the device operator pair G
+        (arpack_hip_znaupd_gen)."""
+        tol = C.c_double(self.tol)
+        L = lib()
+        L.arpack_hip_znaupd_gen.argtypes = L.arpack_hip_znaupd_zshift.argtypes
+        L.arpack_hip_znaupd_gen(G.h, _ip(self.ido), self.bmat.encode(), self.n,
+                                self.which.encode(), self.nev, C.byref(tol),
+                                self.resid.ctypes.data, self.ncv, self.v.ctypes.data, self.n,
+                                _ip(self.iparam), _ip(self.ipntr), self.workd.ctypes.data,
+                                self.workl.ctypes.data, self.lworkl, self.rwork.ctypes.data,
+                                _ip(self.info))
         self.tol = tol.value
         return int(self.ido[0])
 

@@ -17,6 +17,7 @@ namespace ahip {
 
 struct Comm;
 namespace zdev {
+struct ZGen;
 struct Ws {
     hipStream_t stream = nullptr;
     // row-distributed solve: every reduction of `dots` is allreduced over the
@@ -180,6 +181,7 @@ public:
     RciCtx ctx;
     std::optional<Task> root;
     const zdev::ZCsr* csr = nullptr;  // free-running OP (mode 1)
+    zdev::ZGen* gen = nullptr;        // generalized modes: OP and B on the device (zgen.cpp)
     const DistOp* dist = nullptr;      // row block of a distributed solve (or null)
     uint64_t dist_gen = 0;             // generation of dist->comm when the solve started
     int64_t row0 = 0, n_global = 0;

@@ -18,6 +18,7 @@
 #include "../../include/arpack_hip.h"
 #include "dist.hpp"
 #include "zengine.hpp"
+#include "zgen.hpp"
 #include "zsolve.hpp"
 
 const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
@@ -537,10 +538,10 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
                    std::complex<R>* resid, int ncv, std::complex<R>* v, int ldv, int* iparam,
                    int* ipntr, std::complex<R>* workd, std::complex<R>* workl, int lworkl,
                    R* rwork, int* info, const zdev::ZCsr* csr, zdev::ZShift* zs = nullptr,
-                   const DistOp* dist = nullptr) {
+                   const DistOp* dist = nullptr, zdev::ZGen* gen = nullptr) {
     constexpr bool kShadow = !std::is_same_v<R, double>;
     if (zs) csr = zs->A;  // free-running shift-invert: OP = (A - sigma I)^{-1} on the device
-    if (kShadow && csr) {
+    if (kShadow && (csr || gen)) {
         *info = -9999;
         *ido = 99;
         return;
@@ -572,6 +573,9 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         if (csr && ((zs ? mode != 3 || bmat[0] != 'I' : mode != 1) || csr->n != n))
             ierr = ierr ? ierr : -11;
         if (dist && (csr || dist->nloc != n)) ierr = ierr ? ierr : -1;
+        // generalized modes on the device: the operator pair fixes mode and n
+        if (gen && (bmat[0] != 'G' || mode != gen->mode || gen->n != n || csr || dist))
+            ierr = ierr ? ierr : -11;
         if (ierr != 0) {
             *info = ierr;
             *ido = 99;
@@ -619,6 +623,7 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         }
         S->ws.err = &S->a.err;
         S->csr = csr;
+        S->gen = gen;
         S->n_global = dist ? dist->n_global : n;
         if (dist) {  // row block of a distributed solve (PARPACK's pznaupd)
             S->dist = dist;
@@ -683,6 +688,24 @@ static void z_aupd(int* ido, const char* bmat, int n, const char* which, int nev
         const RciReq r = S->ctx.req;
         // free-running OP requests stay on the device: no agreement per product
         if (!(S->csr && (r.ido == -1 || r.ido == 1)) && comm_broken()) return;
+        if (S->gen && (r.ido == -1 || r.ido == 1 || r.ido == 2)) {
+            // generalized modes: OP*x and B*x on the device, on the request's
+            // workd slices in HBM (complex offsets; bx: M x at ido = 1, mode 3)
+            if constexpr (!kShadow) {
+                double* W = reinterpret_cast<double*>(S->a.d_workd);
+                const double* bx = (r.ido == 1 && r.bx >= 0) ? W + 2 * r.bx : nullptr;
+                if (zdev::zgen_apply(*S->gen, S->a.stream, r.ido, W + 2 * r.x, W + 2 * r.y, bx) < 0) {
+                    // a solve missed its tolerance (or a HIP error): OP is not
+                    // what was asked, so the Arnoldi run stops
+                    S->a.sync();
+                    *info = -9999;
+                    *ido = 99;
+                    g_z.erase(v);
+                    return;
+                }
+            }
+            continue;
+        }
         if (S->csr && (r.ido == -1 || r.ido == 1)) {
             if constexpr (!kShadow) {
                 if (!zs) {
@@ -940,6 +963,8 @@ static int z_eupd(bool rvec, char howmny, std::complex<R>* d_out, std::complex<R
 struct arpack_hip_zcsr {
     ahip::zdev::ZCsr A;
 };
+
+const ahip::zdev::ZCsr* ahip_zcsr_view(const arpack_hip_zcsr* Z) { return Z ? &Z->A : nullptr; }
 
 using ahip::cd;
 
@@ -1236,6 +1261,54 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* Z, int* ido, char const* bmat, 
                               a_dcomplex* workl, int lworkl, double* rwork, int* info) {
     ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr,
                  (cd*)workd, (cd*)workl, lworkl, rwork, info, nullptr, &Z->S);
+}
+
+// ---- znaupd's generalized modes on the device (zgen.cpp) ----
+struct arpack_hip_zgen {
+    ahip::zdev::ZGen G;
+};
+
+int arpack_hip_zgen_create(arpack_hip_zgen** out, const arpack_hip_zcsr* A, const arpack_hip_zcsr* M,
+                           int mode, double sigma_re, double sigma_im, double rtol, int maxit) {
+    if (!out || !(rtol > 0.0) || maxit < 1) return -1;
+    auto* Z = new arpack_hip_zgen;
+    const int rc = ahip::zdev::zgen_create(Z->G, A, M, mode, cd(sigma_re, sigma_im), rtol, maxit);
+    if (rc != 0) {
+        delete Z;
+        return rc;
+    }
+    *out = Z;
+    return 0;
+}
+
+void arpack_hip_zgen_destroy(arpack_hip_zgen* Z) {
+    if (!Z) return;
+    ahip::zdev::zgen_destroy(Z->G);
+    delete Z;
+}
+
+int arpack_hip_zgen_stats(const arpack_hip_zgen* Z, long long* solves, long long* iters,
+                          long long* failures, double* max_relres) {
+    if (!Z) return -1;
+    const auto& S = Z->G.S;
+    if (solves) *solves = S.n_solves;
+    if (iters) *iters = S.n_iters;
+    if (failures) *failures = S.n_fail;
+    if (max_relres) *max_relres = S.max_relres;
+    return 0;
+}
+
+void arpack_hip_znaupd_gen(arpack_hip_zgen* Z, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, a_dcomplex* resid, int ncv, a_dcomplex* v, int ldv,
+                           int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl,
+                           double* rwork, int* info) {
+    if (!Z) {
+        *info = -9999;
+        *ido = 99;
+        return;
+    }
+    ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr,
+                 (cd*)workd, (cd*)workl, lworkl, rwork, info, nullptr, nullptr, nullptr, &Z->G);
 }
 
 }  // extern "C"

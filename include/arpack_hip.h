@@ -349,6 +349,31 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, 
                               a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
                               a_dcomplex* workl, int lworkl, double* rwork, int* info);
 
+/* ---- znaupd's generalized modes on the device (bmat = 'G') -------------------
+ * The caller's half of znaupd's modes 2-3 (SRC/znaupd.f:23-31; the reference's
+ * drivers EXAMPLES/COMPLEX/zndrv3.f and zndrv4.f factor M, or A - sigma M, with
+ * zgttrf on the host) served on the GPU: mode 2 OP = inv[M] A, mode 3 OP =
+ * inv[A - sigma M] M (complex sigma), B = M.  The inverse is the device
+ * BiCGStab (as arpack_hip_zshift) to relative residual rtol on C = A - sigma M,
+ * formed once entry by entry over the union pattern (mode 2: on M).  A and M
+ * must outlive the pair.  Returns 0, -1 (bad arguments: sizes differ, mode not
+ * 2 or 3), -2 (HIP / allocation failure). */
+typedef struct arpack_hip_zgen arpack_hip_zgen;
+int arpack_hip_zgen_create(arpack_hip_zgen** G, const arpack_hip_zcsr* A, const arpack_hip_zcsr* M,
+                           int mode, double sigma_re, double sigma_im, double rtol, int maxit);
+void arpack_hip_zgen_destroy(arpack_hip_zgen* G);
+/* solves, BiCGStab iterations, failed solves, worst final relative residual */
+int arpack_hip_zgen_stats(const arpack_hip_zgen* G, long long* solves, long long* iters,
+                          long long* failures, double* max_relres);
+/* znaupd with bmat = 'G' and iparam[6] = the pair's mode, every OP*x and B*x on
+ * the device; returns with ido = 99 (info = -11 when bmat, mode or n do not
+ * match the pair; -9999 when a solve misses rtol).  zneupd_c follows as usual
+ * (bmat 'G', the pair's sigma). */
+void arpack_hip_znaupd_gen(arpack_hip_zgen* G, int* ido, char const* bmat, int n, char const* which,
+                           int nev, double* tol, a_dcomplex* resid, int ncv, a_dcomplex* v, int ldv,
+                           int* iparam, int* ipntr, a_dcomplex* workd, a_dcomplex* workl, int lworkl,
+                           double* rwork, int* info);
+
 /* ---- shift-invert on the device, symmetric (dsaupd mode 3) ------------------
  * y = (A - sigma I)^{-1} x by conjugate gradients (or MINRES, below) on the device CSR operator A
  * (full or symmetric storage), to ||r|| <= rtol ||x|| within maxit iterations:

@@ -186,6 +186,30 @@ def complex_fixtures():
     run_z("z4_zrandom_sr", zr, ["zrandom", 2000, 20, 5, 100.0], 5, 20, "SR", 1e-9, mxiter=3000)
 
 
+def zmode_fixtures():
+    """znaupd's generalized modes (EXAMPLES/COMPLEX/zndrv3.f mode 2, zndrv4.f
+    mode 3: the 1-D convection-diffusion pair, n = 100, nev 4, ncv 20, LM),
+    plus a complex rho with a complex shift, with the caller operators of
+    tests/modes.py (sparse LU on the host, as the drivers' zgttrf/zgttrs)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import modes
+    n = 100
+    v0 = M.dlarnv_uniform(2 * n)[0].view(np.complex128)
+    cases = [("z5_zgen", 2, 0j, 10.0), ("z6_zgen_si", 3, 1 + 0j, 10.0),
+             ("z7_zgen_si_complex", 3, 1 + 0.5j, 10 + 10j)]
+    for name, mode, sigma, rho in cases:
+        c = modes.ZCaller(mode, n, sigma, rho)
+        r = ref.znaupd_solve(c.op, n, 4, 20, "LM", 1e-10, v0=v0, mxiter=300, mode=mode,
+                             bmat="G", bop=c.bop, sigma=sigma, return_state=True)
+        assert r["info"] >= 0 and r["eupd_info"] == 0, (name, r["info"], r.get("eupd_info"))
+        o = 20 * 20
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), mode=mode, n=n, rho=complex(rho),
+                            sigma=sigma, nev=4, ncv=20, which=np.array("LM"), tol=1e-10, v0=v0,
+                            info=r["info"], iparam=r["iparam"], d=r["d"], z=r["z"],
+                            ritz=r["workl"][o:o + 20], bounds=r["workl"][o + 20:o + 40])
+        print(name, "mode", mode, "iparam", r["iparam"][[2, 4, 8, 9, 10]], "d", r["d"][:4])
+
+
 def g7_dlarnv():
     lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
                                  "scipy.libs", "libscipy_openblas*.so"))[0]
@@ -250,6 +274,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["z"]:
         complex_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["zmodes"]:
+        zmode_fixtures()
+        sys.exit(0)
     g7_dlarnv()
     r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
                  keep_z=True)
@@ -275,3 +302,4 @@ if __name__ == "__main__":
     nonsym_fixtures()
     complex_fixtures()
     mode_fixtures()
+    zmode_fixtures()

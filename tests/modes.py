@@ -69,6 +69,37 @@ class Caller:
         self.bop = (lambda x: A @ x) if mode == 4 else (lambda x: Mm @ x)
 
 
+def zconvdiff1d(n, rho):
+    """EXAMPLES/COMPLEX/zndrv3.f / zndrv4.f operator pair: -u'' + rho u' on (0,1)
+    with a complex rho, M = (h/6) tridiag(1, 4, 1), both complex128."""
+    h = 1.0 / (n + 1)
+    e = np.ones(n, np.complex128)
+    s = complex(rho) / 2.0
+    A = sp.diags([(-1.0 / h - s) * e[1:], (2.0 / h) * e, (-1.0 / h + s) * e[1:]], [-1, 0, 1],
+                 format="csc", dtype=np.complex128)
+    Mm = sp.diags([e[1:], 4 * e, e[1:]], [-1, 0, 1], format="csc", dtype=np.complex128) * (h / 6.0)
+    return A, Mm
+
+
+class ZCaller:
+    """znaupd's generalized modes (bmat = 'G'; SRC/znaupd.f:23-31): mode 2 OP =
+    inv(M) A, mode 3 OP = inv(A - sigma M) M (M x handed over at ido = 1),
+    B = M -- the caller loops of zndrv3.f / zndrv4.f with a sparse LU."""
+
+    def __init__(self, mode, n, sigma=0j, rho=10.0):
+        self.mode, self.sigma, self.bmat = mode, complex(sigma), "G"
+        A, Mm = zconvdiff1d(n, rho)
+        self.A, self.M = A, Mm
+        if mode == 2:
+            lu = spl.splu(Mm.tocsc())
+            self.op = lambda x, ido=None, bx=None: lu.solve(A @ x)
+        else:
+            lu = spl.splu((A - self.sigma * Mm).tocsc())
+            self.op = lambda x, ido=None, bx=None: lu.solve(Mm @ x if bx is None or ido == -1
+                                                            else bx)
+        self.bop = lambda x: Mm @ x
+
+
 class StdShiftInvert:
     """Standard shift-invert, bmat = 'I': OP = inv(A - sigma I) (dsdrv2 / dndrv2)."""
 
