@@ -36,9 +36,10 @@ struct Ws {
     double* host = nullptr;  // pinned
     double* scratch = nullptr;  // ncv > 64: nblk * kB * ncv complex (k_zgemm_generic)
     // device-resident Arnoldi step (zstep.hip, bmat = 'I'): the decisions'
-    // state, the coefficient vectors (3 x cstride complex: CGS, DGKS-1, DGKS-2
-    // -- slot 0 also stages the host-driven update's h), the recorded columns
-    // h(1:j,j) (hld = ncv) and the subdiagonals h(j,j-1) per step
+    // state, the coefficient vectors (4 x cstride complex: CGS, DGKS-1, DGKS-2
+    // and the fold's t = H s -- slot 0 also stages the host-driven update's h),
+    // the recorded columns h(1:j,j) (hld = ncv) and the subdiagonals h(j,j-1)
+    // per step
     dev::LzState* st = nullptr;
     dev::LzState* st_host = nullptr;  // pinned mirror
     int cstride = 0;
@@ -151,6 +152,14 @@ template <class R>
 void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int which, const R* rin,
                  R* rout, bool spec, int gate);
 void step_finalize(const Ws& ws, int m, dev::FinPhase ph, int j, int rstart, int gate);
+// folded step j (zstep.hip; free-running znaupd mode 1, complex128): r' and
+// A r' from the raw residual r and y = A r, the CGS sums (k_zfold_dots), then
+// v_j, r_j and the next sweep's sums (k_zfold_update); j - 1 <= kZFoldMax
+constexpr int kZFoldMax = 39;
+void step_fold_dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* r,
+                    const double* y);
+void step_fold_update(const Ws& ws, int64_t n, int j, double* V, int64_t ld, const double* y,
+                      double* r);
 template <class R>
 void step_zero_if(const Ws& ws, int64_t n, R* r);
 void zcsr_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate = nullptr);
@@ -200,6 +209,9 @@ private:
     Task naitr(int k, int npk, int& iinfo);
     RciAwait rci(int ido, int64_t x, int64_t y, int64_t bx = -1);
     RciAwait op(int ido, int64_t x, int64_t y, int64_t bx);
+    // free-running OP on a device vector that is not a workd slice (the folded
+    // step's raw residual)
+    RciAwait op_raw(R* x, int64_t y);
     R* col(int j) { return a.d_v + (int64_t)(j - 1) * a.d_ld; }  // 1-based, reals
     R* wd(int64_t off) { return a.d_workd + 2 * off; }           // complex offset
     int64_t ldc() const { return a.d_ld / 2; }                    // ld in complex units

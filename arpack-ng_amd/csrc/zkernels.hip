@@ -412,7 +412,8 @@ static hipError_t ws_alloc(Ws& ws, int64_t n, int ncv, hipStream_t s) {
     if ((e = hipMalloc(&ws.part, sizeof(double) * (size_t)ws.nblk * slots))) return e;
     if ((e = hipMalloc(&ws.sums, sizeof(double) * slots))) return e;
     ws.cstride = ncv + 2;
-    if ((e = hipMalloc(&ws.coef, sizeof(double) * 2 * 3 * (size_t)ws.cstride))) return e;
+    // coefficient slots: CGS h, DGKS-1, DGKS-2, and the fold's t = H s
+    if ((e = hipMalloc(&ws.coef, sizeof(double) * 2 * 4 * (size_t)ws.cstride))) return e;
     ws.hld = ncv;
     if ((e = hipMalloc(&ws.hcol, sizeof(double) * 2 * (size_t)ncv * ncv))) return e;
     if ((e = hipMalloc(&ws.rec, sizeof(double) * (size_t)(ncv + 1)))) return e;

@@ -8,6 +8,7 @@
 //   host             zneigh / zngets / zsortc / znapps chase (zdense.cpp)
 //   z_aupd           SRC/znaupd.f  (checks, workl layout, iparam)
 //   z_eupd           SRC/zneupd.f  (Schur form, ztrsen, Ritz vectors)
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -24,6 +25,9 @@
 const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
 
 namespace ahip {
+
+// folded complex steps enqueued by this process (arpack_hip_zfold_steps: tests)
+static std::atomic<long long> g_zfold_steps{0};
 
 using cd = std::complex<double>;
 
@@ -56,6 +60,13 @@ RciAwait ZSolverT<R>::op(int ido, int64_t x, int64_t y, int64_t bx) {
     op_x = wd(x);
     op_y = wd(y);
     return RciAwait{&ctx, RciReq{ido, x, y, bx}};
+}
+
+template <class R>
+RciAwait ZSolverT<R>::op_raw(R* x, int64_t y) {
+    op_x = x;
+    op_y = wd(y);
+    return RciAwait{&ctx, RciReq{1, -1, y, -1}};
 }
 
 template <class R>
@@ -160,6 +171,18 @@ void ZSolverT<R>::dgks2_tail(int j, int rstart) {
 // once, the RCI form once per step (where it returns to the caller anyway).  A
 // second DGKS sweep in the free-running form parks the rest of the extension
 // (st.abort = 2) and is finished here, as in the real engine.
+//
+// Folded steps (free-running mode 1, ncv <= kZFoldMax + 1; AHIP_ZFOLD=0
+// disables), as the real engine's (sym.cpp): step j-1's DGKS sweep is not a
+// pass of its own.  Its update pass leaves r (before the sweep) in resid, OP
+// runs on r, and step j's first pass (k_zfold_dots, reads only) forms r' = r -
+// V s in registers, rebuilds A r' from A r with the Arnoldi relation, and sums
+// step j's CGS coefficients and r'^H r' (step j-1's deferred refinement
+// check); the second pass (k_zfold_update) forms them again, stores v_j =
+// r'/||r'|| and r_j.  Two V passes a step instead of three (config 5 in mode 1
+// takes the sweep at every step), no k_zs_place pass, one finalize fewer.
+// The first step of a cycle (V(:,k+1) from the restart) and the last one
+// (no next step to carry its sweep) take the unfolded form.
 template <class R>
 Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
     const int64_t nn = n;
@@ -167,14 +190,39 @@ Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
     const int ldh = ncv;
     cd* h = workl + ih;
     const bool free_run = csr != nullptr;
+    static const bool zfold_env = [] {
+        const char* e = getenv("AHIP_ZFOLD");
+        return !(e && e[0] == '0');
+    }();
+    // exact OP only (A r' = A r - A V s): mode 1 with the device CSR -- not the
+    // shift-invert's iterative solve
+    const bool fold_ok = std::is_same_v<R, double> && zfold_env && free_run && mode == 1 &&
+                         ncv <= zdev::kZFoldMax + 1;
     iinfo = 0;
     dev::LzState& sh = *ws.st_host;
     sh.rnorm = rnorm;  // the host's rnorm (zgetv0, or after znapps) seeds the state
     sh.abort = 0;
     sh.dgks = 0;
     sh.zero = 0;
+    sh.fold = 0;
     write_state();
+    if (fold_ok && k > 0) {
+        // H(:, 1:k) after znapps for the fold's t = H s (the device records hold
+        // only this cycle's new steps): columns into hcol, the real nonnegative
+        // subdiagonals (SRC/znapps.f:405-415) into rec
+        std::vector<cd> hc((size_t)k * ncv, cd(0.0));
+        std::vector<double> rc((size_t)k, 0.0);
+        for (int c = 0; c < k; ++c) {
+            for (int i = 0; i <= c; ++i) hc[(size_t)c * ncv + i] = h[i + (size_t)c * ldh];
+            if (c > 0) rc[c] = h[c + (size_t)(c - 1) * ldh].real();
+        }
+        a.ck(hipMemcpyAsync(ws.hcol, hc.data(), sizeof(cd) * hc.size(), hipMemcpyHostToDevice, a.stream));
+        a.ck(hipMemcpyAsync(ws.rec, rc.data(), sizeof(double) * rc.size(), hipMemcpyHostToDevice,
+                            a.stream));
+        a.sync();  // (the staging vectors are about to go)
+    }
     bool restart_pending = !(rnorm > 0.0);
+    bool folded = false;  // step j's passes form v_j from resid (step j-1's raw r)
     int rstart_j = -1;
     int j = k + 1;
     for (;;) {
@@ -191,30 +239,51 @@ Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
                     co_return;
                 }
                 restart_pending = false;
+                folded = false;
                 rstart = 1;
                 rstart_j = j;
                 sh.abort = 0;
                 sh.rnorm = rnorm;
                 write_state();
             }
-            // v_j = r / rnorm; the OP input workd(ivj) and, as the reference keeps
-            // it, workd(ipj) = B v_j = v_j (znaitr.f:453-476)
-            zdev::step_place(ws, nn, a.d_resid, col(j), wd(ivj), free_run ? nullptr : wd(ipj),
-                             Prec<R>::safmin, j);
             g_stats.nopx += 1;
-            co_await op(1, ivj, irj, ipj);
-            const R* w = wd(irj);
-            // h(1:j,j) = V^H w, wnorm (znaitr.f:545-577)
-            zdev::step_dots(ws, nn, j, a.d_v, ldc(), w, -1);
-            zdev::step_finalize(ws, j + 1, dev::kFinCgs, j, rstart, -1);
-            // r = w - V h with the partials of [V^H r ; r^H r] (znaitr.f:585-640)
-            zdev::step_update(ws, nn, j, a.d_v, ldc(), 0, w, a.d_resid, true, -1);
-            zdev::step_finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
-            // DGKS sweeps, each gated on the device decision (znaitr.f:651-780)
-            zdev::step_update(ws, nn, j, a.d_v, ldc(), 1, a.d_resid, a.d_resid, true, 1);
-            const bool lazy = free_run;
-            zdev::step_finalize(ws, j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
-            if (!lazy) dgks2_tail(j, rstart);
+            if (folded) {
+                // OP on the raw residual, then the two fold passes (see above)
+                co_await op_raw(a.d_resid, irj);
+                g_zfold_steps.fetch_add(1, std::memory_order_relaxed);
+                if constexpr (std::is_same_v<R, double>) {
+                    zdev::step_fold_dots(ws, nn, j, a.d_v, ldc(), a.d_resid, wd(irj));
+                    zdev::step_finalize(ws, j + 1, dev::kFinCgsFolded, j, rstart, -1);
+                    zdev::step_fold_update(ws, nn, j, a.d_v, ldc(), wd(irj), a.d_resid);
+                }
+            } else {
+                // v_j = r / rnorm; the OP input workd(ivj) and, as the reference
+                // keeps it, workd(ipj) = B v_j = v_j (znaitr.f:453-476)
+                zdev::step_place(ws, nn, a.d_resid, col(j), wd(ivj), free_run ? nullptr : wd(ipj),
+                                 Prec<R>::safmin, j);
+                co_await op(1, ivj, irj, ipj);
+                const R* w = wd(irj);
+                // h(1:j,j) = V^H w, wnorm (znaitr.f:545-577)
+                zdev::step_dots(ws, nn, j, a.d_v, ldc(), w, -1);
+                zdev::step_finalize(ws, j + 1, dev::kFinCgs, j, rstart, -1);
+                // r = w - V h with the partials of [V^H r ; r^H r] (znaitr.f:585-640)
+                zdev::step_update(ws, nn, j, a.d_v, ldc(), 0, w, a.d_resid, true, -1);
+            }
+            const bool next_folded = fold_ok && j < k + npk && j <= zdev::kZFoldMax;
+            if (next_folded) {
+                // the DGKS decision; a sweep's coefficients s, t = H s and st.fold
+                // go to the next step's passes (znaitr.f:651-690)
+                zdev::step_finalize(ws, j + 1, dev::kFinPostCgsFold, j, rstart, -1);
+                folded = true;
+            } else {
+                zdev::step_finalize(ws, j + 1, dev::kFinPostCgs, j, rstart, -1);
+                // DGKS sweeps, each gated on the device decision (znaitr.f:651-780)
+                zdev::step_update(ws, nn, j, a.d_v, ldc(), 1, a.d_resid, a.d_resid, true, 1);
+                const bool lazy = free_run;
+                zdev::step_finalize(ws, j + 1, lazy ? dev::kFinDgks1Lazy : dev::kFinDgks1, j, rstart, 1);
+                if (!lazy) dgks2_tail(j, rstart);
+                folded = false;
+            }
             ++j;
             if (!free_run) {
                 read_state();
@@ -223,18 +292,49 @@ Task ZSolverT<R>::naitr_dev(int k, int npk, int& iinfo) {
             }
         }
         read_state();
+        // a park inside a folded cycle leaves resid = r of the step before the
+        // parked one, BEFORE its DGKS sweep when st.fold (the sweep was taken)
+        const bool was_folded = folded || sh.fold;
+        folded = false;  // a resumed cycle restarts with a formed v_j
+        auto unfold = [&](int jprev) {  // resid = r' = r - V(:,1:jprev) s
+            if (fold_ok && sh.fold)
+                zdev::step_update(ws, nn, jprev, a.d_v, ldc(), 1, a.d_resid, a.d_resid, false, -1);
+        };
         if (sh.abort == 2) {  // step abort_j needs its second DGKS sweep
             const int ja = sh.abort_j;
             g_stats.nopx -= (k + npk) - ja;  // the later steps were skipped
+            const bool parked_by_fold = fold_ok && was_folded && ja < k + npk && sh.fold;
             sh.abort = 0;
+            write_state();
+            if (parked_by_fold) {
+                // parked by step ja+1's kFinCgsFolded: r' was formed only in
+                // registers and the second sweep's coefficients V^H r' not summed
+                unfold(ja);
+                zdev::step_dots(ws, nn, ja, a.d_v, ldc(), a.d_resid, -1);
+                zdev::step_finalize(ws, ja + 1, dev::kFinFoldCoef2, ja, ja == rstart_j ? 1 : 0, -1);
+            }
+            sh.fold = 0;
             write_state();
             dgks2_tail(ja, ja == rstart_j ? 1 : 0);
             j = ja + 1;
             continue;
         }
+        if (sh.abort == 3) {  // folded step abort_j: rnorm outside the raw range --
+            const int ja = sh.abort_j;  // redo it with v_j formed
+            g_stats.nopx -= (k + npk) - ja + 1;
+            sh.abort = 0;
+            write_state();
+            unfold(ja - 1);  // r' of step ja-1
+            sh.fold = 0;
+            write_state();
+            j = ja;
+            continue;
+        }
         if (sh.abort) {  // rnorm == 0 at step abort_j: restart there
             const int ja = sh.abort_j;
             g_stats.nopx -= (k + npk) - ja + 1;
+            sh.fold = 0;
+            write_state();
             j = ja;
             restart_pending = true;
             continue;
@@ -1262,6 +1362,8 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* Z, int* ido, char const* bmat, 
     ahip::z_aupd(ido, bmat, n, which, nev, tol, (cd*)resid, ncv, (cd*)v, ldv, iparam, ipntr,
                  (cd*)workd, (cd*)workl, lworkl, rwork, info, nullptr, &Z->S);
 }
+
+long long arpack_hip_zfold_steps(void) { return ahip::g_zfold_steps.load(); }
 
 // ---- znaupd's generalized modes on the device (zgen.cpp) ----
 struct arpack_hip_zgen {

@@ -12,6 +12,12 @@
 //                                                               675-690)
 //   zs_finalize  fixed-order sums + the phase logic: h(1:j,j) recorded in hcol,
 //              wnorm / rnorm, the 0.717 tests, <= 2 refinements (znaitr.f:651-780)
+//   zfold_dots / zfold_update  the folded step (free-running mode 1, ncv <= 40):
+//              step j-1's DGKS sweep applied inside step j's two passes, as the
+//              real engine's fold.hip -- A r' = A r - V (H s) - s_J r' by the
+//              Arnoldi relation A V_J = V_J H_J + r' e_J^T (H_J with the sweep's
+//              correction in its last column), so OP runs on the raw residual r
+//              and the sweep is no pass of its own: two V passes a step, not three
 //
 // Partial layout: complex slot c -> real slots 2c (Re), 2c+1 (Im) of
 // part[slot * nblk + block]; the norm slot follows the j coefficients.
@@ -208,6 +214,145 @@ __global__ __launch_bounds__(kB) void k_zs_update_generic(int64_t n, int j,
     }
 }
 
+// r' = r - V(:,0:J) s (the DGKS update's zgemv order, k ascending; rounded to
+// the storage type as that update's store) and w = A r' = y - (V(:,0:J) t +
+// c r') with t = H_J s, c = s_J; explicit fma, so k_zfold_dots and
+// k_zfold_update form both bit-identically.  Without a pending sweep r' = r, w = y.
+template <class R, int J>
+__device__ __forceinline__ void zfold_rw(bool fold, const double2* vr, const double2* __restrict__ s,
+                                         const double2* __restrict__ t, double2 c, double2& rp,
+                                         double2& w) {
+    if (!fold) return;
+#pragma unroll
+    for (int k = 0; k < J; ++k) {
+        const double2 p = cmul(vr[k], s[k]);
+        rp.x -= p.x;
+        rp.y -= p.y;
+    }
+    rp = d2(st2<R>(rp));
+    double ax = 0.0, ay = 0.0;
+#pragma unroll
+    for (int k = 0; k < J; ++k) {
+        ax = fma(vr[k].x, t[k].x, fma(-vr[k].y, t[k].y, ax));
+        ay = fma(vr[k].x, t[k].y, fma(vr[k].y, t[k].x, ay));
+    }
+    ax = fma(c.x, rp.x, fma(-c.y, rp.y, ax));
+    ay = fma(c.x, rp.y, fma(c.y, rp.x, ay));
+    w.x -= ax;
+    w.y -= ay;
+}
+
+// Folded step j = J + 1, first pass (reads only): r' and w in registers;
+// partials of [V(:,0:J)^H w ; r'^H w] (complex slots 0..J) and (w^H w, r'^H r')
+// (complex slot J + 1): the CGS sums of step j and step j-1's deferred
+// refinement check (kFinCgsFolded).  s = coef slot 1, t = coef slot 3.
+template <class R, int J>
+__global__ __launch_bounds__(kB) void k_zfold_dots(int64_t n, const typename C2<R>::T* __restrict__ V,
+                                                   int64_t ld, const typename C2<R>::T* __restrict__ r,
+                                                   const typename C2<R>::T* __restrict__ y,
+                                                   const double2* __restrict__ s,
+                                                   const double2* __restrict__ t,
+                                                   double* __restrict__ part,
+                                                   const LzState* __restrict__ st) {
+    if (st->abort) return;
+    const bool fold = st->fold != 0;
+    const double2 c = fold ? s[J - 1] : make_double2(0.0, 0.0);
+    double2 acc[J + 1];
+#pragma unroll
+    for (int k = 0; k < J + 1; ++k) acc[k] = make_double2(0.0, 0.0);
+    double ww = 0.0, rr = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        double2 vr[J];
+#pragma unroll
+        for (int k = 0; k < J; ++k) vr[k] = ntld(V + i + (int64_t)k * ld);
+        double2 rp = d2(r[i]), w = d2(y[i]);
+        zfold_rw<R, J>(fold, vr, s, t, c, rp, w);
+#pragma unroll
+        for (int k = 0; k < J; ++k) {
+            const double2 p = cmulc(vr[k], w);
+            acc[k].x += p.x;
+            acc[k].y += p.y;
+        }
+        const double2 p = cmulc(rp, w);
+        acc[J].x += p.x;
+        acc[J].y += p.y;
+        ww += w.x * w.x + w.y * w.y;
+        rr += rp.x * rp.x + rp.y * rp.y;
+    }
+    constexpr int NV = 2 * J + 4;
+    double v[NV];
+#pragma unroll
+    for (int k = 0; k <= J; ++k) {
+        v[2 * k] = acc[k].x;
+        v[2 * k + 1] = acc[k].y;
+    }
+    v[2 * J + 2] = ww;
+    v[2 * J + 3] = rr;
+    zblock_partials<NV>(v, NV, part, 0);
+}
+
+// Folded step j = J + 1, second pass: the same r' and w; v_j = r' vs -> V(:,J)
+// (k_zs_place's product), r_j = w vs - V(:,0:J+1) h -> r (in place; h = coef
+// slot 0, the zgemv order), partials of [V(:,0:J+1)^H r_j ; r_j^H r_j] (the
+// layout of k_zs_update's: the next sweep's coefficients).
+template <class R, int J>
+__global__ __launch_bounds__(kB) void k_zfold_update(int64_t n, typename C2<R>::T* __restrict__ V,
+                                                     int64_t ld, const double2* __restrict__ h,
+                                                     const double2* __restrict__ s,
+                                                     const double2* __restrict__ t,
+                                                     const typename C2<R>::T* __restrict__ y,
+                                                     typename C2<R>::T* r, double* __restrict__ part,
+                                                     const LzState* __restrict__ st) {
+    if (st->abort) return;
+    const bool fold = st->fold != 0;
+    const double2 c = fold ? s[J - 1] : make_double2(0.0, 0.0);
+    const double vs = st->vscale;
+    double2 acc[J + 1];
+#pragma unroll
+    for (int k = 0; k < J + 1; ++k) acc[k] = make_double2(0.0, 0.0);
+    double rr = 0.0;
+    typename C2<R>::T* vj = V + (int64_t)J * ld;
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        double2 vr[J + 1];
+#pragma unroll
+        for (int k = 0; k < J; ++k) vr[k] = ntld(V + i + (int64_t)k * ld);
+        double2 rp = d2(r[i]), w = d2(y[i]);
+        zfold_rw<R, J>(fold, vr, s, t, c, rp, w);
+        const auto vst = st2<R>(make_double2(rp.x * vs, rp.y * vs));
+        vj[i] = vst;
+        vr[J] = d2(vst);
+        double2 rn = make_double2(w.x * vs, w.y * vs);
+#pragma unroll
+        for (int k = 0; k < J + 1; ++k) {  // the zgemv order: r -= V(:,k) h(k), k ascending
+            const double2 p = cmul(vr[k], h[k]);
+            rn.x -= p.x;
+            rn.y -= p.y;
+        }
+        const auto rs = st2<R>(rn);
+        r[i] = rs;
+        const double2 rd = d2(rs);
+        rr += rd.x * rd.x + rd.y * rd.y;
+#pragma unroll
+        for (int k = 0; k < J + 1; ++k) {
+            const double2 p = cmulc(vr[k], rd);
+            acc[k].x += p.x;
+            acc[k].y += p.y;
+        }
+    }
+    constexpr int NV = 2 * J + 4;
+    double v[NV];
+#pragma unroll
+    for (int k = 0; k <= J; ++k) {
+        v[2 * k] = acc[k].x;
+        v[2 * k + 1] = acc[k].y;
+    }
+    v[2 * J + 2] = rr;
+    v[2 * J + 3] = 0.0;
+    zblock_partials<NV>(v, NV, part, 0);
+}
+
 template <class R>
 __global__ void k_zs_zero_if(int64_t n, typename C2<R>::T* r, const LzState* st) {
     if (st->abort || !st->zero) return;
@@ -267,12 +412,81 @@ __device__ __forceinline__ void zs_fin_body(int m, int phase, int j, int rstart,
         if (t == 0) st->rnorm = nrm;
         return;
     }
+    if (phase == dev::kFinCgsFolded) {
+        // step j of a folded cycle (sums of k_zfold_dots: slots 0..j-2 V^H w,
+        // j-1 r'^H w, j (w^H w, r'^H r')): (1) step j-1's deferred first
+        // refinement check on ||r'|| (a needed second one parks the cycle, the
+        // host finishes it), (2) the CGS coefficients of v_j = r'/||r'||,
+        // rescaled from the raw residual's sums (st.vscale)
+        __shared__ int s_go;
+        if (t == 0) {
+            if (st->dgks == 1) {
+                const double rn = sqrt(fabs(s_sum[2 * jm + 1]));
+                if (rn > 0.717 * st->rnorm && !st->force_dgks2) {
+                    st->rnorm = rn;
+                    st->dgks = 0;
+                } else {
+                    st->nitref += 1;
+                    st->rnorm = rn;
+                    st->dgks = 2;
+                    st->abort = 2;
+                    st->abort_j = j - 1;
+                }
+            }
+            const double rn = st->rnorm;
+            int go = 0;
+            if (st->abort) {
+            } else if (!(rn > 0.0)) {  // invariant subspace at step j (znaitr.f:373)
+                st->abort = 1;
+                st->abort_j = j;
+            } else if (rn < 1e-150 || rn > 1e150) {  // raw-vector range guard: the host
+                st->abort = 3;                       // redoes step j with v_j formed first
+                st->abort_j = j;
+            } else {
+                go = 1;
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;
+        const double vs = 1.0 / st->rnorm;  // k_zs_place's factor for rnorm >= safmin
+        const int J = j - 1;
+        for (int k = t; k < J; k += nt) {
+            const double2 h = make_double2(s_sum[2 * k] * vs, s_sum[2 * k + 1] * vs);
+            coef[k] = h;
+            hcol[(int64_t)(j - 1) * hld + k] = h;
+        }
+        if (t == 0) {  // v_j^H w = vs^2 r'^H (A r')
+            const double2 h = make_double2((s_sum[2 * J] * vs) * vs, (s_sum[2 * J + 1] * vs) * vs);
+            coef[J] = h;
+            hcol[(int64_t)(j - 1) * hld + J] = h;
+            st->vscale = vs;
+            st->zero = 0;
+            st->dgks = 0;
+            st->wnorm = sqrt(fabs(s_sum[2 * jm])) * vs;
+            st->beta = (j == 1 || rstart) ? 0.0 : st->rnorm;
+            rec[j - 1] = st->beta;
+        }
+        return;
+    }
+    if (phase == dev::kFinFoldCoef2) {  // a folded park's second sweep (host path)
+        for (int k = t; k < jm; k += nt) {
+            const double2 c = make_double2(s_sum[2 * k], s_sum[2 * k + 1]);
+            coef[(int64_t)2 * cstride + k] = c;
+            double2 h = hcol[(int64_t)(j - 1) * hld + k];
+            h.x += c.x;
+            h.y += c.y;
+            hcol[(int64_t)(j - 1) * hld + k] = h;
+        }
+        return;
+    }
     // refinement phases (znaitr.f:651-780): decision on rnorm = ||r||, then the
     // next sweep's coefficients V^H r into coef slot `take`
     __shared__ int s_take;
+    const bool pfold = phase == dev::kFinPostCgsFold;
     if (t == 0) {
         int take = 0;
-        if (phase == dev::kFinPostCgs) {
+        if (phase == dev::kFinPostCgs || pfold) {
             st->rnorm = nrm;
             if (nrm > 0.717 * st->wnorm) {
                 st->dgks = 0;
@@ -305,12 +519,38 @@ __device__ __forceinline__ void zs_fin_body(int m, int phase, int j, int rstart,
             }
             st->dgks = 0;
         }
+        if (pfold) st->fold = take;
         s_take = take;
     }
     __syncthreads();
     // the correction of THIS sweep was added when its coefficients were taken;
     // the h(1:j,j) daxpy (znaitr.f:681) happens with the coefficients it used
     const int take = s_take;
+    if (pfold && take) {
+        // t = H_j s for the next step's fold, one row per thread: H(i, q) from
+        // the records (rows 0..q of column q; this step's column is h + s, read
+        // before the daxpy below), the real subdiagonal H(q+1, q) = rec[q+1]
+        for (int i = t; i < jm; i += nt) {
+            double tx = 0.0, ty = 0.0;
+            for (int q = i > 0 ? i - 1 : 0; q < jm; ++q) {
+                double2 hq;
+                if (i <= q) {
+                    hq = hcol[(int64_t)q * hld + i];
+                    if (q == jm - 1) {
+                        hq.x += s_sum[2 * i];
+                        hq.y += s_sum[2 * i + 1];
+                    }
+                } else {
+                    hq = make_double2(rec[q + 1], 0.0);
+                }
+                const double sx = s_sum[2 * q], sy = s_sum[2 * q + 1];
+                tx = fma(hq.x, sx, fma(-hq.y, sy, tx));
+                ty = fma(hq.x, sy, fma(hq.y, sx, ty));
+            }
+            coef[(int64_t)3 * cstride + i] = make_double2(tx, ty);
+        }
+        __syncthreads();
+    }
     if (take) {
         for (int k = t; k < jm; k += nt) {
             const double2 c = make_double2(s_sum[2 * k], s_sum[2 * k + 1]);
@@ -361,7 +601,8 @@ void step_place(const Ws& ws, int64_t n, const R* r, R* vcol, R* copy1, R* copy2
     M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
 #define AHIP_ZS_C32(M) \
     M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) M(31) M(32)
-#define AHIP_ZS_C40(M) M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40)
+#define AHIP_ZS_C39(M) M(33) M(34) M(35) M(36) M(37) M(38) M(39)
+#define AHIP_ZS_C40(M) AHIP_ZS_C39(M) M(40)
 
 template <class R>
 void step_dots(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, const R* u, int gate) {
@@ -436,6 +677,53 @@ void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int whi
         hipLaunchKernelGGL(k_zs_update_generic<R>, g, b, 0, ws.stream, n, j, V2, ld, c, ri, ro, ws.st,
                            gate);
         if (spec) step_dots<R>(ws, n, j, V, ld, rout, gate);
+    }
+}
+
+// folded step j (2 <= j <= kZFoldMax + 1; J = j - 1 formed columns): complex128 only
+// (the free-running complex engine is znaupd's)
+void step_fold_dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* r,
+                    const double* y) {
+    const double2* V2 = reinterpret_cast<const double2*>(V);
+    const double2* r2 = reinterpret_cast<const double2*>(r);
+    const double2* y2 = reinterpret_cast<const double2*>(y);
+    const double2* s = reinterpret_cast<const double2*>(ws.coef) + ws.cstride;
+    const double2* tt = reinterpret_cast<const double2*>(ws.coef) + 3 * (size_t)ws.cstride;
+    const dim3 g(sgrid(ws)), b(kB);
+    switch (j - 1) {
+#define AHIP_ZF_DOTS(J)                                                                            \
+    case J:                                                                                        \
+        hipLaunchKernelGGL((k_zfold_dots<double, J>), g, b, 0, ws.stream, n, V2, ld, r2, y2, s, tt, \
+                           ws.part, ws.st);                                                        \
+        break;
+        AHIP_ZS_C16(AHIP_ZF_DOTS)
+        AHIP_ZS_C32(AHIP_ZF_DOTS)
+        AHIP_ZS_C39(AHIP_ZF_DOTS)
+#undef AHIP_ZF_DOTS
+        default: break;
+    }
+}
+
+void step_fold_update(const Ws& ws, int64_t n, int j, double* V, int64_t ld, const double* y,
+                      double* r) {
+    double2* V2 = reinterpret_cast<double2*>(V);
+    const double2* y2 = reinterpret_cast<const double2*>(y);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    const double2* h = reinterpret_cast<const double2*>(ws.coef);
+    const double2* s = h + ws.cstride;
+    const double2* tt = h + 3 * (size_t)ws.cstride;
+    const dim3 g(sgrid(ws)), b(kB);
+    switch (j - 1) {
+#define AHIP_ZF_UPD(J)                                                                             \
+    case J:                                                                                        \
+        hipLaunchKernelGGL((k_zfold_update<double, J>), g, b, 0, ws.stream, n, V2, ld, h, s, tt, y2, \
+                           r2, ws.part, ws.st);                                                    \
+        break;
+        AHIP_ZS_C16(AHIP_ZF_UPD)
+        AHIP_ZS_C32(AHIP_ZF_UPD)
+        AHIP_ZS_C39(AHIP_ZF_UPD)
+#undef AHIP_ZF_UPD
+        default: break;
     }
 }
 

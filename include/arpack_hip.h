@@ -349,6 +349,11 @@ void arpack_hip_znaupd_zshift(arpack_hip_zshift* S, int* ido, char const* bmat, 
                               a_dcomplex* v, int ldv, int* iparam, int* ipntr, a_dcomplex* workd,
                               a_dcomplex* workl, int lworkl, double* rwork, int* info);
 
+/* Folded complex Arnoldi steps enqueued so far by this process (free-running
+ * znaupd mode 1, ncv <= 40: step j-1's DGKS sweep carried by step j's two
+ * passes; AHIP_ZFOLD=0 turns the fold off).  A diagnostic for tests. */
+long long arpack_hip_zfold_steps(void);
+
 /* ---- znaupd's generalized modes on the device (bmat = 'G') -------------------
  * The caller's half of znaupd's modes 2-3 (SRC/znaupd.f:23-31; the reference's
  * drivers EXAMPLES/COMPLEX/zndrv3.f and zndrv4.f factor M, or A - sigma M, with
