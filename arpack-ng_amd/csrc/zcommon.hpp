@@ -54,17 +54,19 @@ __device__ __forceinline__ double2 ntld(const float2* p) {
     return make_double2(v.x, v.y);
 }
 
-// The split operator's S slice partials of row r (slice-major, n apart; S = 4
-// or 8) summed in one fixed tree order: the split SpMV's combine (zsplit.hip)
+// The split operator's S slice partials of row r (slice-major, n apart; S = 2,
+// 4 or 8) summed in one fixed tree order: the split SpMV's combine (zsplit.hip)
 // and the solver kernels that fuse it (zsolve.hip) produce bit-identical sums
 constexpr int kZMaxSlices = 8;  // = XCDs
 template <int S>
 __device__ __forceinline__ double2 slice_sum(const double2* __restrict__ yp, int64_t n, int64_t r) {
-    static_assert(S == 4 || S == 8, "4 or 8 column slices");
+    static_assert(S == 2 || S == 4 || S == 8, "2, 4 or 8 column slices");
     double2 a[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) a[s] = yp[(int64_t)s * n + r];
-    if constexpr (S == 4)
+    if constexpr (S == 2)
+        return make_double2(a[0].x + a[1].x, a[0].y + a[1].y);
+    else if constexpr (S == 4)
         return make_double2((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y));
     else
         return make_double2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),

@@ -340,12 +340,12 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
         const int m = chunk < S.maxit - k ? chunk : S.maxit - k;
         for (int q = 0; q < m; ++q, ++k) {
             const D2* w = op(S.p);
-            hipLaunchKernelGGL(ns == 4 ? k_bi_v<4> : ns == 8 ? k_bi_v<8> : k_bi_v<0>, dim3(nb), dim3(kT), 0, strm, n,
+            hipLaunchKernelGGL(ns == 2 ? k_bi_v<2> : ns == 4 ? k_bi_v<4> : ns == 8 ? k_bi_v<8> : k_bi_v<0>, dim3(nb), dim3(kT), 0, strm, n,
                                w, V(S.p), V(S.rh), V(S.v), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_s, dim3(nb), dim3(kT), 0, strm, n, V(S.r), V(S.v), V(S.s), S.st,
                                k, P0, nb);
             w = op(S.s);
-            hipLaunchKernelGGL(ns == 4 ? k_bi_t<4> : ns == 8 ? k_bi_t<8> : k_bi_t<0>, dim3(nb), dim3(kT), 0, strm, n,
+            hipLaunchKernelGGL(ns == 2 ? k_bi_t<2> : ns == 4 ? k_bi_t<4> : ns == 8 ? k_bi_t<8> : k_bi_t<0>, dim3(nb), dim3(kT), 0, strm, n,
                                w, V(S.s), V(S.t), sig, S.st, P0, nb);
             hipLaunchKernelGGL(k_bi_xr, dim3(nb), dim3(kT), 0, strm, n, y2, V(S.p), V(S.s), V(S.t),
                                V(S.r), V(S.rh), S.st, P0, P1, nb);

@@ -718,7 +718,14 @@ int zcsr_build_split(ZCsr& A) {
     // s and s + 4), else 8: tools/ztile_probe.hip at config 5 (n = 5e5), 0.215 ms
     // a product against 0.237 with 8 slices -- half the partial-sum traffic, the
     // same column density per tile
-    const int ns = (n + 3) / 4 * 16 <= (int64_t(2) << 20) ? 4 : 8;
+    // (AHIP_ZSLICES=2|4|8 forces the count: A/B of the partial-sum traffic
+    // against x's L2 footprint)
+    static const int force_ns = [] {
+        const char* e = getenv("AHIP_ZSLICES");
+        const int v = e ? atoi(e) : 0;
+        return v == 2 || v == 4 || v == 8 ? v : 0;
+    }();
+    const int ns = force_ns ? force_ns : (n + 3) / 4 * 16 <= (int64_t(2) << 20) ? 4 : 8;
     const int64_t sw = (n + ns - 1) / ns;
     A.s_n = ns;
     A.s_w = sw;
@@ -737,7 +744,9 @@ int zcsr_build_split(ZCsr& A) {
         hipMalloc(&A.s_rp, sizeof(int32_t) * ns * (n + 1)) ||
         hipMalloc(&A.s_base, sizeof(int64_t) * (ns + 1)))
         return fail(-2);
-    if (ns == 4)
+    if (ns == 2)
+        hipLaunchKernelGGL(k_zsplit_count<2>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
+    else if (ns == 4)
         hipLaunchKernelGGL(k_zsplit_count<4>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
     else
         hipLaunchKernelGGL(k_zsplit_count<8>, dim3(grid1(n)), dim3(256), 0, nullptr, n, sw, A.rowptr, A.col, cnt);
@@ -771,11 +780,13 @@ int zcsr_build_split(ZCsr& A) {
                            A.s_base, sc, (double2*)A.s_val);
     };
     if (A.s_col16)
-        ns == 4 ? fill(k_zsplit_fill<4, uint16_t>, (uint16_t*)A.s_col)
-                : fill(k_zsplit_fill<8, uint16_t>, (uint16_t*)A.s_col);
+        ns == 2 ? fill(k_zsplit_fill<2, uint16_t>, (uint16_t*)A.s_col)
+        : ns == 4 ? fill(k_zsplit_fill<4, uint16_t>, (uint16_t*)A.s_col)
+                  : fill(k_zsplit_fill<8, uint16_t>, (uint16_t*)A.s_col);
     else
-        ns == 4 ? fill(k_zsplit_fill<4, int32_t>, (int32_t*)A.s_col)
-                : fill(k_zsplit_fill<8, int32_t>, (int32_t*)A.s_col);
+        ns == 2 ? fill(k_zsplit_fill<2, int32_t>, (int32_t*)A.s_col)
+        : ns == 4 ? fill(k_zsplit_fill<4, int32_t>, (int32_t*)A.s_col)
+                  : fill(k_zsplit_fill<8, int32_t>, (int32_t*)A.s_col);
     if (hipDeviceSynchronize() != hipSuccess) return fail(-1);
     A.split = true;
     (void)ztile_build(A);  // optional: the CSR split stays if the tiles cannot be built
@@ -836,7 +847,8 @@ const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x,
     if (!A.split) return nullptr;
     const auto* x2 = reinterpret_cast<const double2*>(x);
     auto* yp = reinterpret_cast<double2*>(A.s_y);
-    if (A.s_n == 4) split_partials<4>(s, A, x2, yp, gate);
+    if (A.s_n == 2) split_partials<2>(s, A, x2, yp, gate);
+    else if (A.s_n == 4) split_partials<4>(s, A, x2, yp, gate);
     else split_partials<8>(s, A, x2, yp, gate);
     return A.s_y;
 }
@@ -844,7 +856,8 @@ const double* zcsr_split_partials(hipStream_t s, const ZCsr& A, const double* x,
 void zcsr_split_spmv(hipStream_t s, const ZCsr& A, const double* x, double* y, const int* gate) {
     const auto* yp = reinterpret_cast<const double2*>(zcsr_split_partials(s, A, x, gate));
     auto* y2 = reinterpret_cast<double2*>(y);
-    if (A.s_n == 4) hipLaunchKernelGGL(k_zsplit_combine<4>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
+    if (A.s_n == 2) hipLaunchKernelGGL(k_zsplit_combine<2>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
+    else if (A.s_n == 4) hipLaunchKernelGGL(k_zsplit_combine<4>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
     else hipLaunchKernelGGL(k_zsplit_combine<8>, dim3(2048), dim3(256), 0, s, A.n, yp, y2, gate);
 }
 
