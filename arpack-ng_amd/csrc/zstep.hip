@@ -214,39 +214,102 @@ __global__ __launch_bounds__(kB) void k_zs_update_generic(int64_t n, int j,
     }
 }
 
-// r' = r - V(:,0:J) s (the DGKS update's zgemv order, k ascending; rounded to
-// the storage type as that update's store) and w = A r' = y - (V(:,0:J) t +
-// c r') with t = H_J s, c = s_J; explicit fma, so k_zfold_dots and
-// k_zfold_update form both bit-identically.  Without a pending sweep r' = r, w = y.
-template <class R, int J>
-__device__ __forceinline__ void zfold_rw(bool fold, const double2* vr, const double2* __restrict__ s,
+// The folded passes spread each row over L lanes (L = 1, 2 or 4): lane q of
+// the row's group holds columns [q JQ, (q+1) JQ) of V (JQ = ceil(J / L)) and
+// their accumulators -- a quarter of the registers at L = 4, so four waves a
+// SIMD instead of one at J = 39.  Sums over a row's columns are each lane's
+// sequential partial, then (p0 + p1) + (p2 + p3) across the group (xor
+// shuffles: every lane of the group ends with the same bits).
+template <int L>
+__device__ __forceinline__ double gsum(double v) {
+    if constexpr (L >= 2) v += __shfl_xor(v, 1, 64);
+    if constexpr (L >= 4) v += __shfl_xor(v, 2, 64);
+    return v;
+}
+
+// r' = r - V(:,0:J) s (rounded to the storage type as the DGKS update's store)
+// and w = A r' = y - (V(:,0:J) t + c r') with t = H_J s, c = s_J; explicit fma,
+// so k_zfold_dots and k_zfold_update form both bit-identically.  Without a
+// pending sweep r' = r, w = y.  vr: this lane's JQ columns from c0.
+template <class R, int J, int L>
+__device__ __forceinline__ void zfold_rw(bool fold, const double2* vr, int c0,
+                                         const double2* __restrict__ s,
                                          const double2* __restrict__ t, double2 c, double2& rp,
                                          double2& w) {
     if (!fold) return;
+    constexpr int JQ = (J + L - 1) / L;
+    double px = 0.0, py = 0.0;
 #pragma unroll
-    for (int k = 0; k < J; ++k) {
-        const double2 p = cmul(vr[k], s[k]);
-        rp.x -= p.x;
-        rp.y -= p.y;
+    for (int kk = 0; kk < JQ; ++kk) {
+        if (c0 + kk < J) {
+            const double2 p = cmul(vr[kk], s[c0 + kk]);
+            px += p.x;
+            py += p.y;
+        }
     }
+    rp.x -= gsum<L>(px);
+    rp.y -= gsum<L>(py);
     rp = d2(st2<R>(rp));
     double ax = 0.0, ay = 0.0;
 #pragma unroll
-    for (int k = 0; k < J; ++k) {
-        ax = fma(vr[k].x, t[k].x, fma(-vr[k].y, t[k].y, ax));
-        ay = fma(vr[k].x, t[k].y, fma(vr[k].y, t[k].x, ay));
+    for (int kk = 0; kk < JQ; ++kk) {
+        if (c0 + kk < J) {
+            const double2 tk = t[c0 + kk];
+            ax = fma(vr[kk].x, tk.x, fma(-vr[kk].y, tk.y, ax));
+            ay = fma(vr[kk].x, tk.y, fma(vr[kk].y, tk.x, ay));
+        }
     }
+    ax = gsum<L>(ax);
+    ay = gsum<L>(ay);
     ax = fma(c.x, rp.x, fma(-c.y, rp.y, ax));
     ay = fma(c.x, rp.y, fma(c.y, rp.x, ay));
     w.x -= ax;
     w.y -= ay;
 }
 
+// Block partials of a lane-split pass: accumulator kk of group lane q is column
+// q JQ + kk (< J); `extra` (NE values, held by group lane 0) follows in slots
+// 2J ...  Each column's sum over the block: the wave's lanes of the same q
+// (xor offsets L .. 32), then the four waves in zblock_partials' order.
+template <int J, int L, int NE>
+__device__ __forceinline__ void zsplit_partials(const double2 (&acc)[(J + L - 1) / L],
+                                                const double (&extra)[NE], double* part) {
+    constexpr int JQ = (J + L - 1) / L, NV = 2 * J + NE;
+    __shared__ double red[kB / 64][NV];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane % L;
+    const int c0 = q * JQ;
+#pragma unroll
+    for (int kk = 0; kk < JQ; ++kk) {
+        double x = acc[kk].x, y = acc[kk].y;
+#pragma unroll
+        for (int o = L; o < 64; o <<= 1) {
+            x += __shfl_xor(x, o, 64);
+            y += __shfl_xor(y, o, 64);
+        }
+        if (lane < L && c0 + kk < J) {
+            red[wave][2 * (c0 + kk)] = x;
+            red[wave][2 * (c0 + kk) + 1] = y;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        double x = extra[e];
+#pragma unroll
+        for (int o = L; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+        if (lane == 0) red[wave][2 * J + e] = x;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < NV; k += kB) {
+        const double v = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+        part[(size_t)k * gridDim.x + blockIdx.x] = v;
+    }
+}
+
 // Folded step j = J + 1, first pass (reads only): r' and w in registers;
 // partials of [V(:,0:J)^H w ; r'^H w] (complex slots 0..J) and (w^H w, r'^H r')
 // (complex slot J + 1): the CGS sums of step j and step j-1's deferred
 // refinement check (kFinCgsFolded).  s = coef slot 1, t = coef slot 3.
-template <class R, int J>
+template <class R, int J, int L>
 __global__ __launch_bounds__(kB) void k_zfold_dots(int64_t n, const typename C2<R>::T* __restrict__ V,
                                                    int64_t ld, const typename C2<R>::T* __restrict__ r,
                                                    const typename C2<R>::T* __restrict__ y,
@@ -255,48 +318,45 @@ __global__ __launch_bounds__(kB) void k_zfold_dots(int64_t n, const typename C2<
                                                    double* __restrict__ part,
                                                    const LzState* __restrict__ st) {
     if (st->abort) return;
+    constexpr int JQ = (J + L - 1) / L;
     const bool fold = st->fold != 0;
     const double2 c = fold ? s[J - 1] : make_double2(0.0, 0.0);
-    double2 acc[J + 1];
+    const int q = threadIdx.x % L, c0 = q * JQ;
+    double2 acc[JQ];
 #pragma unroll
-    for (int k = 0; k < J + 1; ++k) acc[k] = make_double2(0.0, 0.0);
-    double ww = 0.0, rr = 0.0;
-    const int64_t stride = (int64_t)gridDim.x * kB;
-    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        double2 vr[J];
+    for (int kk = 0; kk < JQ; ++kk) acc[kk] = make_double2(0.0, 0.0);
+    double ex[4] = {0.0, 0.0, 0.0, 0.0};  // r'^H w (re, im), w^H w, r'^H r' (group lane 0)
+    const int64_t stride = (int64_t)gridDim.x * (kB / L);
+    for (int64_t i = ((int64_t)blockIdx.x * kB + threadIdx.x) / L; i < n; i += stride) {
+        double2 vr[JQ];
 #pragma unroll
-        for (int k = 0; k < J; ++k) vr[k] = ntld(V + i + (int64_t)k * ld);
+        for (int kk = 0; kk < JQ; ++kk)
+            vr[kk] = c0 + kk < J ? ntld(V + i + (int64_t)(c0 + kk) * ld) : make_double2(0.0, 0.0);
         double2 rp = d2(r[i]), w = d2(y[i]);
-        zfold_rw<R, J>(fold, vr, s, t, c, rp, w);
+        zfold_rw<R, J, L>(fold, vr, c0, s, t, c, rp, w);
 #pragma unroll
-        for (int k = 0; k < J; ++k) {
-            const double2 p = cmulc(vr[k], w);
-            acc[k].x += p.x;
-            acc[k].y += p.y;
+        for (int kk = 0; kk < JQ; ++kk) {
+            const double2 p = cmulc(vr[kk], w);
+            acc[kk].x += p.x;
+            acc[kk].y += p.y;
         }
-        const double2 p = cmulc(rp, w);
-        acc[J].x += p.x;
-        acc[J].y += p.y;
-        ww += w.x * w.x + w.y * w.y;
-        rr += rp.x * rp.x + rp.y * rp.y;
+        if (q == 0) {
+            const double2 p = cmulc(rp, w);
+            ex[0] += p.x;
+            ex[1] += p.y;
+            ex[2] += w.x * w.x + w.y * w.y;
+            ex[3] += rp.x * rp.x + rp.y * rp.y;
+        }
     }
-    constexpr int NV = 2 * J + 4;
-    double v[NV];
-#pragma unroll
-    for (int k = 0; k <= J; ++k) {
-        v[2 * k] = acc[k].x;
-        v[2 * k + 1] = acc[k].y;
-    }
-    v[2 * J + 2] = ww;
-    v[2 * J + 3] = rr;
-    zblock_partials<NV>(v, NV, part, 0);
+    zsplit_partials<J, L, 4>(acc, ex, part);
 }
 
 // Folded step j = J + 1, second pass: the same r' and w; v_j = r' vs -> V(:,J)
 // (k_zs_place's product), r_j = w vs - V(:,0:J+1) h -> r (in place; h = coef
-// slot 0, the zgemv order), partials of [V(:,0:J+1)^H r_j ; r_j^H r_j] (the
-// layout of k_zs_update's: the next sweep's coefficients).
-template <class R, int J>
+// slot 0), partials of [V(:,0:J+1)^H r_j ; r_j^H r_j] (the layout of
+// k_zs_update's: the next sweep's coefficients).  Column J (= v_j, known to
+// every lane of the group) is group lane 0's extra term.
+template <class R, int J, int L>
 __global__ __launch_bounds__(kB) void k_zfold_update(int64_t n, typename C2<R>::T* __restrict__ V,
                                                      int64_t ld, const double2* __restrict__ h,
                                                      const double2* __restrict__ s,
@@ -305,52 +365,60 @@ __global__ __launch_bounds__(kB) void k_zfold_update(int64_t n, typename C2<R>::
                                                      typename C2<R>::T* r, double* __restrict__ part,
                                                      const LzState* __restrict__ st) {
     if (st->abort) return;
+    constexpr int JQ = (J + L - 1) / L;
     const bool fold = st->fold != 0;
     const double2 c = fold ? s[J - 1] : make_double2(0.0, 0.0);
     const double vs = st->vscale;
-    double2 acc[J + 1];
+    const double2 hj = h[J];
+    const int q = threadIdx.x % L, c0 = q * JQ;
+    double2 acc[JQ];
 #pragma unroll
-    for (int k = 0; k < J + 1; ++k) acc[k] = make_double2(0.0, 0.0);
-    double rr = 0.0;
+    for (int kk = 0; kk < JQ; ++kk) acc[kk] = make_double2(0.0, 0.0);
+    double ex[4] = {0.0, 0.0, 0.0, 0.0};  // v_j^H r_j (re, im), r_j^H r_j, 0 (group lane 0)
     typename C2<R>::T* vj = V + (int64_t)J * ld;
-    const int64_t stride = (int64_t)gridDim.x * kB;
-    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        double2 vr[J + 1];
+    const int64_t stride = (int64_t)gridDim.x * (kB / L);
+    for (int64_t i = ((int64_t)blockIdx.x * kB + threadIdx.x) / L; i < n; i += stride) {
+        double2 vr[JQ];
 #pragma unroll
-        for (int k = 0; k < J; ++k) vr[k] = ntld(V + i + (int64_t)k * ld);
+        for (int kk = 0; kk < JQ; ++kk)
+            vr[kk] = c0 + kk < J ? ntld(V + i + (int64_t)(c0 + kk) * ld) : make_double2(0.0, 0.0);
         double2 rp = d2(r[i]), w = d2(y[i]);
-        zfold_rw<R, J>(fold, vr, s, t, c, rp, w);
+        zfold_rw<R, J, L>(fold, vr, c0, s, t, c, rp, w);
         const auto vst = st2<R>(make_double2(rp.x * vs, rp.y * vs));
-        vj[i] = vst;
-        vr[J] = d2(vst);
-        double2 rn = make_double2(w.x * vs, w.y * vs);
+        const double2 v = d2(vst);
+        double px = 0.0, py = 0.0;  // this lane's part of V(:,0:J) h
 #pragma unroll
-        for (int k = 0; k < J + 1; ++k) {  // the zgemv order: r -= V(:,k) h(k), k ascending
-            const double2 p = cmul(vr[k], h[k]);
-            rn.x -= p.x;
-            rn.y -= p.y;
+        for (int kk = 0; kk < JQ; ++kk) {
+            if (c0 + kk < J) {
+                const double2 p = cmul(vr[kk], h[c0 + kk]);
+                px += p.x;
+                py += p.y;
+            }
         }
+        px = gsum<L>(px);
+        py = gsum<L>(py);
+        const double2 pj = cmul(v, hj);
+        const double2 rn = make_double2(w.x * vs - px - pj.x, w.y * vs - py - pj.y);
         const auto rs = st2<R>(rn);
-        r[i] = rs;
+        if (q == 0) {
+            vj[i] = vst;
+            r[i] = rs;
+        }
         const double2 rd = d2(rs);
-        rr += rd.x * rd.x + rd.y * rd.y;
 #pragma unroll
-        for (int k = 0; k < J + 1; ++k) {
-            const double2 p = cmulc(vr[k], rd);
-            acc[k].x += p.x;
-            acc[k].y += p.y;
+        for (int kk = 0; kk < JQ; ++kk) {
+            const double2 p = cmulc(vr[kk], rd);
+            acc[kk].x += p.x;
+            acc[kk].y += p.y;
+        }
+        if (q == 0) {
+            const double2 p = cmulc(v, rd);
+            ex[0] += p.x;
+            ex[1] += p.y;
+            ex[2] += rd.x * rd.x + rd.y * rd.y;
         }
     }
-    constexpr int NV = 2 * J + 4;
-    double v[NV];
-#pragma unroll
-    for (int k = 0; k <= J; ++k) {
-        v[2 * k] = acc[k].x;
-        v[2 * k + 1] = acc[k].y;
-    }
-    v[2 * J + 2] = rr;
-    v[2 * J + 3] = 0.0;
-    zblock_partials<NV>(v, NV, part, 0);
+    zsplit_partials<J, L, 4>(acc, ex, part);
 }
 
 template <class R>
@@ -680,6 +748,10 @@ void step_update(const Ws& ws, int64_t n, int j, const R* V, int64_t ld, int whi
     }
 }
 
+// lanes a row of the fold passes: the row's complex V entries and accumulators
+// per lane stay at <= 10 each (two or more waves a SIMD)
+constexpr int zfold_lanes(int J) { return J >= 12 ? 4 : J >= 6 ? 2 : 1; }
+
 // folded step j (2 <= j <= kZFoldMax + 1; J = j - 1 formed columns): complex128 only
 // (the free-running complex engine is znaupd's)
 void step_fold_dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld, const double* r,
@@ -693,8 +765,8 @@ void step_fold_dots(const Ws& ws, int64_t n, int j, const double* V, int64_t ld,
     switch (j - 1) {
 #define AHIP_ZF_DOTS(J)                                                                            \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_zfold_dots<double, J>), g, b, 0, ws.stream, n, V2, ld, r2, y2, s, tt, \
-                           ws.part, ws.st);                                                        \
+        hipLaunchKernelGGL((k_zfold_dots<double, J, zfold_lanes(J)>), g, b, 0, ws.stream, n, V2, ld, \
+                           r2, y2, s, tt, ws.part, ws.st);                                         \
         break;
         AHIP_ZS_C16(AHIP_ZF_DOTS)
         AHIP_ZS_C32(AHIP_ZF_DOTS)
@@ -716,8 +788,8 @@ void step_fold_update(const Ws& ws, int64_t n, int j, double* V, int64_t ld, con
     switch (j - 1) {
 #define AHIP_ZF_UPD(J)                                                                             \
     case J:                                                                                        \
-        hipLaunchKernelGGL((k_zfold_update<double, J>), g, b, 0, ws.stream, n, V2, ld, h, s, tt, y2, \
-                           r2, ws.part, ws.st);                                                    \
+        hipLaunchKernelGGL((k_zfold_update<double, J, zfold_lanes(J)>), g, b, 0, ws.stream, n, V2, ld, \
+                           h, s, tt, y2, r2, ws.part, ws.st);                                      \
         break;
         AHIP_ZS_C16(AHIP_ZF_UPD)
         AHIP_ZS_C32(AHIP_ZF_UPD)
