@@ -61,3 +61,18 @@ def test_folded_complex_step_forced_second_refinement(tmp_path):
     plain = _solve(tmp_path, "z2_zrandom_lm", False, force=True)
     assert int(fold["nitref"]) > 0 and int(fold["folded"]) > 0
     _agree(fold, plain)
+
+
+def test_folded_complex_step_restarts(tmp_path):
+    """An operator with 3 distinct eigenvalues closes every Krylov space after
+    3 steps: the residual falls to round-off, the refinement checks decide on
+    noise (a park, a give-up with r = 0 and a restart with a new start vector,
+    SRC/znaitr.f:373-422, or a noise vector taken as v_j), inside folded
+    cycles.  Both forms converge to Ritz values of the two largest eigenvalues
+    (their counts may differ: the decisions are taken on round-off there)."""
+    for fold in (True, False):
+        r = _solve(tmp_path, "zdiag3", fold)
+        assert int(r["info"]) == 0 and int(r["nconv"]) == 2, (fold, int(r["info"]), int(r["nconv"]))
+        assert (int(r["folded"]) > 0) == fold
+        for x in r["d"]:
+            assert np.abs(np.array([3 + 1j, 2.0]) - x).min() <= 1e-9, (fold, r["d"])

@@ -18,10 +18,21 @@ from conftest import GOLDEN, load_pkg  # noqa: E402
 
 def main():
     fixture, out = sys.argv[1], sys.argv[2]
-    g = dict(np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False))
-    spec = g["spec"]
     pkg = load_pkg()
-    Z = pkg.ZCSR.random(int(spec[1]), int(spec[2]), int(spec[3]), float(spec[4]))
+    if fixture == "zdiag3":
+        # a diagonal operator with 3 distinct eigenvalues: every Krylov space
+        # closes after 3 steps (rnorm -> 0, the second refinement, then a
+        # restart with a new start vector), inside folded cycles
+        from oracle import matrices as M
+        n = 3000
+        lam = np.array([3 + 1j, 2.0 + 0j, 1 - 1j])[np.arange(n) % 3]
+        Z = pkg.ZCSR.from_arrays(np.arange(n + 1), np.arange(n, dtype=np.int32), lam)
+        g = dict(nev=2, ncv=8, which="LM", tol=1e-10, mxiter=300,
+                 v0=M.dlarnv_uniform(2 * n)[0].view(np.complex128))
+    else:
+        g = dict(np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False))
+        spec = g["spec"]
+        Z = pkg.ZCSR.random(int(spec[1]), int(spec[2]), int(spec[3]), float(spec[4]))
     n = Z.n
     s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]),
                  mxiter=int(g["mxiter"]), v0=g["v0"])
@@ -32,6 +43,7 @@ def main():
     L.arpack_hip_zfold_steps.restype = ctypes.c_longlong
     np.savez(out, d=d, z=z, ritz=s.ritz, iters=int(s.iparam[2]), nconv=nconv,
              nopx=int(s.iparam[8]), nrorth=int(s.iparam[10]), nitref=st["nitref"],
+             nrstrt=st["nrstrt"],
              info=int(s.info[0]), folded=int(L.arpack_hip_zfold_steps()))
 
 
