@@ -648,7 +648,13 @@ static void sb_row_caps(int64_t n, int64_t& cap0, int64_t& rest) {
         cap0 = rest = rcap;
         return;
     }
-    cap0 = rcap / 2 > 256 ? rcap / 2 : rcap;
+    // (AHIP_LIGHT_SB=4: a quarter of the cap -- more room for the Arnoldi
+    // finalize's H staging, A/B)
+    static const int div = [] {
+        const char* e = getenv("AHIP_LIGHT_SB");
+        return e && e[0] == '4' ? 4 : 2;
+    }();
+    cap0 = rcap / div > 256 ? rcap / div : rcap;
     rest = (n - cap0 + slots - 2) / (slots - 1);
     if (rest < rcap) rest = rcap;  // small n: the 1,024-row floor (fewer superblocks than slots)
     if (rest < cap0) rest = cap0;
