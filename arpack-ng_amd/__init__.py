@@ -739,7 +739,9 @@ class ZShift:
     the caller-side solve the reference's drivers do with zgttrf/zgttrs
     (EXAMPLES/COMPLEX/zndrv2.f:179,250)."""
 
-    def __init__(self, A: "ZCSR", sigma=0j, rtol=1e-12, maxit=200):
+    def __init__(self, A: "ZCSR", sigma=0j, rtol=1e-12, maxit=200, method="bicgstab"):
+        """method: "bicgstab", or "tridiag" (a direct solve of a tridiagonal
+        A - sigma I: zgttrf + device scans, as zndrv2.f's zgttrf / zgttrs)."""
         self.A = A  # keeps the operator alive
         self.sigma = complex(sigma)
         h = C.c_void_p()
@@ -749,6 +751,11 @@ class ZShift:
             raise RuntimeError("arpack_hip_zshift_create failed (%d)" % rc)
         self.h = h.value
         self.n = A.n
+        if method != "bicgstab":
+            L = lib()
+            L.arpack_hip_zshift_set_method.argtypes = [C.c_void_p, C.c_int]
+            if L.arpack_hip_zshift_set_method(self.h, {"tridiag": 1}[method]) != 0:
+                raise ValueError(method)
 
     def __del__(self):
         try:

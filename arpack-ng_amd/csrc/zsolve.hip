@@ -293,6 +293,7 @@ int zshift_create(ZShift& S, const ZCsr* A, std::complex<double> sigma, double r
 }
 
 void zshift_destroy(ZShift& S) {
+    zshift_tridiag_free(S);
     double* vecs[] = {S.r, S.rh, S.p, S.v, S.s, S.t, S.w, S.part};
     for (double* q : vecs)
         if (q) (void)hipFree(q);
@@ -321,6 +322,17 @@ int zshift_apply(ZShift& S, hipStream_t strm, const double* b, double* y, double
     auto* y2 = reinterpret_cast<D2*>(y);
     auto V = [](double* q) { return reinterpret_cast<D2*>(q); };
     const int* gate = &S.st->done;
+    if (S.method == 1) {  // the direct tridiagonal solve (ztri.hip)
+        if (hipEventRecord(S.ev0, strm) != hipSuccess) return -2;
+        if (zshift_tridiag_apply(S, strm, b, y) != 0) return -2;
+        if (hipEventRecord(S.ev1, strm) != hipSuccess || hipEventSynchronize(S.ev1) != hipSuccess)
+            return -2;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, S.ev0, S.ev1) == hipSuccess) S.ms_total += ms;
+        if (relres) *relres = 0.0;
+        S.n_solves += 1;
+        return 0;
+    }
     // w = A x; on a split operator only its slice partials, summed by k_bi_v / k_bi_t
     const int ns = S.A->split ? S.A->s_n : 0;
     const bool split = ns > 0;

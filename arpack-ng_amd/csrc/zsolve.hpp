@@ -53,6 +53,14 @@ struct ZShift {
     double max_relres = 0.0;
     double ms_total = 0.0;         // device time of the solves (hipEvents)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // method 1 (zshift_set_tridiag): a DIRECT solve of a tridiagonal A - sigma I
+    // (zgttrf restated on the host, the triangular solves as device scans,
+    // ztri.hip) -- what EXAMPLES/COMPLEX/zndrv2.f does with zgttrf / zgttrs
+    int method = 0;
+    double *tri_dl = nullptr, *tri_d = nullptr, *tri_du = nullptr, *tri_du2 = nullptr;  // complex
+    int* tri_ipiv = nullptr;
+    void* tri_bc = nullptr;        // block composites of the scans
+    double* tri_cin = nullptr;     // the state entering each block (2 complex)
 };
 
 // 0, or a hipError_t on allocation failure (nothing leaks)
@@ -63,6 +71,12 @@ void zshift_destroy(ZShift& S);
 // of the recursively updated residual, -1 if BiCGStab broke down or did not
 // reach rtol within maxit (y then holds the last iterate), -2 on a HIP error.
 int zshift_apply(ZShift& S, hipStream_t stream, const double* b, double* y, double* relres);
+// method 1: factor A - sigma I (A tridiagonal): 0; -1 not tridiagonal or
+// singular; -2 HIP failure.  ztri_free releases the factors (method 0 again).
+int zshift_tridiag_factor(ZShift& S);
+void zshift_tridiag_free(ZShift& S);
+// y = (A - sigma I)^{-1} b by the factors (b, y device, not aliased): 0 or -2
+int zshift_tridiag_apply(ZShift& S, hipStream_t s, const double* b, double* y);
 // algorithmic HBM bytes of one BiCGStab iteration (two CSR products at 20 B a
 // stored entry + rowptr + x/y vectors, and the fused vector passes)
 double zshift_iter_bytes(const ZShift& S);

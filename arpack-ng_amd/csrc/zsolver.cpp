@@ -1336,6 +1336,15 @@ void arpack_hip_zshift_destroy(arpack_hip_zshift* Z) {
     delete Z;
 }
 
+// 0: BiCGStab (the default), 1: a direct solve of a tridiagonal A - sigma I
+// (zgttrf on the host, the triangular solves as device scans, ztri.hip)
+int arpack_hip_zshift_set_method(arpack_hip_zshift* Z, int method) {
+    if (!Z || method < 0 || method > 1) return -1;
+    ahip::zdev::zshift_tridiag_free(Z->S);  // (method 0 again)
+    if (method == 1) return ahip::zdev::zshift_tridiag_factor(Z->S) == 0 ? 0 : -1;
+    return 0;
+}
+
 int arpack_hip_zshift_solve(arpack_hip_zshift* Z, const double* x, double* y, double* relres) {
     if (!Z || !x || !y || x == y) return -2;  // as arpack_hip_dshift_solve
     return ahip::zdev::zshift_apply(Z->S, nullptr, x, y, relres);

@@ -334,6 +334,13 @@ void arpack_hip_zshift_destroy(arpack_hip_zshift* S);
  * iterations (>= 0; *relres = ||r||/||x||), -1 if BiCGStab broke down or missed
  * rtol within maxit, -2 on a HIP error. */
 int arpack_hip_zshift_solve(arpack_hip_zshift* S, const double* x, double* y, double* relres);
+/* The solve's method: 0 BiCGStab (the default), 1 a DIRECT solve of a
+ * tridiagonal A - sigma I -- LAPACK's zgttrf restated (pivoting by |re| + |im|),
+ * once on the host, the two triangular solves as device scans of complex affine
+ * maps (csrc/ztri.hip): what EXAMPLES/COMPLEX/zndrv2.f does with zgttrf /
+ * zgttrs.  Returns 0, or -1 (unknown method; method 1 with A not tridiagonal or
+ * A - sigma I singular: the solve stays BiCGStab). */
+int arpack_hip_zshift_set_method(arpack_hip_zshift* S, int method);
 /* Totals over the solves so far: solves, iterations, failures, worst final
  * relative residual, device time (ms, hipEvents around each solve) and the
  * algorithmic HBM bytes of one iteration (two CSR products at 20 B a stored
@@ -715,6 +722,10 @@ void arpack_hip_kit_slarnv(int* iseed, int n, float* x); /* slarnv(idist=2), LAP
  * ipiv minus one). */
 int arpack_hip_kit_dgttrf(int64_t n, double* dl, double* d, double* du, double* du2, int* ipiv);
 void arpack_hip_kit_dgttrs(int64_t n, const double* dl, const double* d, const double* du,
+                           const double* du2, const int* ipiv, double* b);
+/* zgttrf / zgttrs likewise (complex arrays interleaved re, im; pivoting by CABS1) */
+int arpack_hip_kit_zgttrf(int64_t n, double* dl, double* d, double* du, double* du2, int* ipiv);
+void arpack_hip_kit_zgttrs(int64_t n, const double* dl, const double* d, const double* du,
                            const double* du2, const int* ipiv, double* b);
 /* The device generators behind dgetv0/sgetv0's start vector on a device buffer
  * x (prec 'd': double, 's': float); iseed is advanced like dlarnv/slarnv's. */

@@ -210,6 +210,28 @@ def zmode_fixtures():
         print(name, "mode", mode, "iparam", r["iparam"][[2, 4, 8, 9, 10]], "d", r["d"][:4])
 
 
+def zndrv2_fixtures():
+    """EXAMPLES/COMPLEX/zndrv2.f's operator (the 1-D convection-diffusion with
+    1/h^2 scaling, rho = 10, n = 100) in shift-invert mode 3 -- the reference
+    driver's zgttrf / zgttrs solve stands as the LU of run_z -- at its sigma = 0
+    and at a complex shift."""
+    n, rho = 100, 10.0
+    h = 1.0 / (n + 1)
+    s = rho / 2.0
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        for j, v in ((i - 1, -1.0 / h**2 - s / h), (i, 2.0 / h**2), (i + 1, -1.0 / h**2 + s / h)):
+            if 0 <= j < n:
+                rows.append(i)
+                cols.append(j)
+                vals.append(complex(v))
+    rowptr = np.searchsorted(np.array(rows), np.arange(n + 1)).astype(np.int64)
+    mat = (rowptr, np.array(cols, np.int32), np.array(vals, np.complex128))
+    run_z("z8_zndrv2_si", mat, ["zndrv2", n, rho], 4, 20, "LM", 1e-10, mode=3, sigma=0j)
+    run_z("z9_zndrv2_si_shift", mat, ["zndrv2", n, rho], 4, 20, "LM", 1e-10, mode=3,
+          sigma=5000 + 2000j)
+
+
 def g7_dlarnv():
     lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
                                  "scipy.libs", "libscipy_openblas*.so"))[0]
@@ -277,6 +299,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["zmodes"]:
         zmode_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["zndrv2"]:
+        zndrv2_fixtures()
+        sys.exit(0)
     g7_dlarnv()
     r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
                  keep_z=True)
@@ -303,3 +328,4 @@ if __name__ == "__main__":
     complex_fixtures()
     mode_fixtures()
     zmode_fixtures()
+    zndrv2_fixtures()

@@ -119,3 +119,74 @@ def test_zshift_singular_shift_fails_loudly(pkg):
     s = pkg.ZRci(1000, 4, 12, "LM", 1e-8, mode=3, mxiter=50)
     assert s.aupd_zshift(S) == 99
     assert int(s.info[0]) == -9999
+
+
+def _tridiag(n, rho=10.0, seed=None):
+    """zndrv2's operator (1/h^2 scaling) or, with a seed, a random complex
+    tridiagonal that pivots."""
+    if seed is None:
+        h = 1.0 / (n + 1)
+        s = rho / 2.0
+        lo = np.full(n - 1, -1.0 / h**2 - s / h, np.complex128)
+        di = np.full(n, 2.0 / h**2, np.complex128)
+        up = np.full(n - 1, -1.0 / h**2 + s / h, np.complex128)
+    else:
+        rng = np.random.default_rng(seed)
+        c = lambda k: rng.standard_normal(k) + 1j * rng.standard_normal(k)  # noqa: E731
+        lo, di, up = c(n - 1), c(n), c(n - 1)
+    return sp.diags([lo, di, up], [-1, 0, 1], shape=(n, n), format="csr", dtype=np.complex128)
+
+
+@pytest.mark.parametrize("n,seed,sigma", [(1, 3, 0j), (2, 3, 0j), (3, 3, 0.5j), (17, 3, 0j),
+                                          (4099, 5, 1 - 1j), (100, None, 0j),
+                                          (1000003, 7, 0.25 + 0.5j)])
+def test_ztridiag_direct_solve(pkg, n, seed, sigma):
+    """ZShift method 1 (zgttrf on the host, the triangular solves as device
+    scans, csrc/ztri.hip) against SciPy's sparse LU of A - sigma I: the
+    relative true residual and the solution to LU's rounding."""
+    import scipy.sparse.linalg as spl
+    A = _tridiag(n, seed=seed)
+    A.sort_indices()
+    Z = pkg.ZCSR.from_arrays(A.indptr, A.indices, A.data)
+    S = pkg.ZShift(Z, sigma, method="tridiag")
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    y, it, rr = S.solve(x)
+    assert it == 0 and rr == 0.0
+    C = (A - sigma * sp.identity(n, format="csr", dtype=np.complex128)).tocsc()
+    yr = spl.splu(C).solve(x) if n > 1 else x / C.toarray()[0, 0]
+    assert np.linalg.norm(C @ y - x) <= 1e-10 * np.linalg.norm(x) * max(1.0, np.abs(C).max())
+    assert np.abs(y - yr).max() <= 1e-9 * np.abs(yr).max()
+
+
+def test_ztridiag_refuses_wider_operator(pkg):
+    Z = pkg.ZCSR.random(2000, 20, 5, 100.0)
+    with pytest.raises(ValueError):
+        pkg.ZShift(Z, 0j, method="tridiag")
+
+
+@pytest.mark.parametrize("name", ["z8_zndrv2_si", "z9_zndrv2_si_shift"])
+def test_znaupd_mode3_tridiag_zndrv2(pkg, golden, name):
+    """EXAMPLES/COMPLEX/zndrv2.f's shift-invert run, free on the device with
+    the direct tridiagonal solve (the driver's zgttrf / zgttrs): the
+    reference's info, nconv, restart cycles and OP*x count, eigenvalues within
+    1e-9 of the largest."""
+    g = golden(name)
+    n = int(g["spec"][1])
+    A = _tridiag(n, rho=float(g["spec"][2]))
+    A.sort_indices()
+    Z = pkg.ZCSR.from_arrays(A.indptr, A.indices, A.data)
+    sigma = complex(g["sigma"])
+    S = pkg.ZShift(Z, sigma, method="tridiag")
+    s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), mode=3,
+                 mxiter=int(g["mxiter"]), v0=g["v0"])
+    assert s.aupd_zshift(S) == 99
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    assert int(s.iparam[2]) == int(g["iparam"][2]), (int(s.iparam[2]), int(g["iparam"][2]))
+    assert int(s.iparam[8]) == int(g["iparam"][8])
+    assert S.stats()["solves"] == int(s.iparam[8])
+    d, z, nc = s.eupd(sigma=sigma)
+    dref = g["d"]
+    for x in dref:
+        assert np.abs(d - x).min() <= 1e-9 * np.abs(dref).max(), (x, d)
