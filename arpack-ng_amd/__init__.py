@@ -879,7 +879,7 @@ class ZGen:
     runs the whole loop with it."""
 
     def __init__(self, A: "ZCSR", M: "ZCSR", mode: int, sigma=0j, rtol: float = 1e-12,
-                 maxit: int = 5000):
+                 maxit: int = 5000, method: str = "bicgstab"):
         L = lib()
         L.arpack_hip_zgen_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_int,
                                              C.c_double, C.c_double, C.c_double, C.c_int]
@@ -891,6 +891,10 @@ class ZGen:
         if rc != 0:
             raise RuntimeError(f"arpack_hip_zgen_create failed ({rc})")
         self.h, self.A, self.M, self.mode, self.sigma = h, A, M, int(mode), sigma
+        if method != "bicgstab":  # "tridiag": A and M tridiagonal, a direct solve of C
+            L.arpack_hip_zgen_set_method.argtypes = [C.c_void_p, C.c_int]
+            if L.arpack_hip_zgen_set_method(self.h, {"tridiag": 1}[method]) != 0:
+                raise ValueError(method)
 
     def stats(self):
         L = lib()

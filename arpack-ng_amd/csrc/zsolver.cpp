@@ -1392,6 +1392,15 @@ int arpack_hip_zgen_create(arpack_hip_zgen** out, const arpack_hip_zcsr* A, cons
     return 0;
 }
 
+// 0: BiCGStab on C (the default), 1: the direct tridiagonal solve of C
+// (ztri.hip; A and M tridiagonal, as zndrv4.f's pair it factors with zgttrf)
+int arpack_hip_zgen_set_method(arpack_hip_zgen* Z, int method) {
+    if (!Z || method < 0 || method > 1) return -1;
+    ahip::zdev::zshift_tridiag_free(Z->G.S);
+    if (method == 1) return ahip::zdev::zshift_tridiag_factor(Z->G.S) == 0 ? 0 : -1;
+    return 0;
+}
+
 void arpack_hip_zgen_destroy(arpack_hip_zgen* Z) {
     if (!Z) return;
     ahip::zdev::zgen_destroy(Z->G);

@@ -374,6 +374,12 @@ typedef struct arpack_hip_zgen arpack_hip_zgen;
 int arpack_hip_zgen_create(arpack_hip_zgen** G, const arpack_hip_zcsr* A, const arpack_hip_zcsr* M,
                            int mode, double sigma_re, double sigma_im, double rtol, int maxit);
 void arpack_hip_zgen_destroy(arpack_hip_zgen* G);
+/* The inverse's method: 0 BiCGStab (the default), 1 the direct tridiagonal
+ * solve of C (zgttrf + device scans, as arpack_hip_zshift_set_method) when A and
+ * M are tridiagonal -- zndrv3/zndrv4.f's pairs, which the drivers factor with
+ * zgttrf.  0, or -1 (unknown method, C not tridiagonal or singular: the solve
+ * stays BiCGStab). */
+int arpack_hip_zgen_set_method(arpack_hip_zgen* G, int method);
 /* solves, BiCGStab iterations, failed solves, worst final relative residual */
 int arpack_hip_zgen_stats(const arpack_hip_zgen* G, long long* solves, long long* iters,
                           long long* failures, double* max_relres);

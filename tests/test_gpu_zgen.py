@@ -30,17 +30,23 @@ def _zdev(pkg, S):
     return pkg.ZCSR.from_arrays(S.indptr, S.indices, S.data)
 
 
-@pytest.mark.parametrize("name", ["z5_zgen", "z6_zgen_si", "z7_zgen_si_complex"])
-def test_znaupd_generalized_on_device(pkg, golden, name):
+@pytest.mark.parametrize("name,method", [("z5_zgen", "bicgstab"), ("z6_zgen_si", "bicgstab"),
+                                         ("z7_zgen_si_complex", "bicgstab"), ("z5_zgen", "tridiag"),
+                                         ("z6_zgen_si", "tridiag"), ("z7_zgen_si_complex", "tridiag")])
+def test_znaupd_generalized_on_device(pkg, golden, name, method):
+    """method "tridiag": the direct solve of the tridiagonal C (M in mode 2,
+    A - sigma M in mode 3), as zndrv3/zndrv4.f factor it with zgttrf."""
     g = golden(name)
     mode, n, sigma, rho = int(g["mode"]), int(g["n"]), complex(g["sigma"]), complex(g["rho"])
     A, Mm = modes.zconvdiff1d(n, rho)
-    G = pkg.ZGen(_zdev(pkg, A), _zdev(pkg, Mm), mode, sigma, rtol=1e-13, maxit=50 * n)
+    G = pkg.ZGen(_zdev(pkg, A), _zdev(pkg, Mm), mode, sigma, rtol=1e-13, maxit=50 * n,
+                 method=method)
     s = pkg.ZRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat="G",
                  mode=mode, mxiter=300, v0=g["v0"])
     assert s.aupd_gen(G) == 99
     st = G.stats()
     assert st["fails"] == 0 and st["solves"] > 0, st
+    assert (st["iters"] == 0) == (method == "tridiag"), st
     assert int(s.info[0]) == int(g["info"]) == 0
     assert int(s.iparam[4]) == int(g["iparam"][4])
     assert int(s.iparam[2]) == int(g["iparam"][2]), (int(s.iparam[2]), int(g["iparam"][2]))
