@@ -842,15 +842,27 @@ class DGen:
     MINRES (1) or BiCGStab (2: a nonsymmetric C, dnaupd's modes 2-3 through
     NsRci.aupd_gen) to relative residual rtol on C = A - sigma B."""
 
-    def __init__(self, A: CSR, B: CSR, mode: int, sigma: float = 0.0, rtol: float = 1e-12,
+    def __init__(self, A: CSR, B: CSR, mode: int, sigma=0.0, rtol: float = 1e-12,
                  maxit: int = 5000, method: int = 0):
+        """A complex sigma (nonzero imaginary part): dnaupd's complex-shift
+        modes 3 / 4 (OP = Re / Im of inv[A - sigma M] M; method 2 BiCGStab or 3
+        the direct tridiagonal solve, on the complex C)."""
         L = lib()
         L.arpack_hip_dgen_create.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_int,
                                              C.c_double, C.c_double, C.c_int, C.c_int]
+        L.arpack_hip_dgen_create_cshift.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p,
+                                                    C.c_int, C.c_double, C.c_double, C.c_double,
+                                                    C.c_int, C.c_int]
         L.arpack_hip_dgen_destroy.argtypes = [C.c_void_p]
         h = C.c_void_p()
-        rc = L.arpack_hip_dgen_create(C.byref(h), A.h, B.h, int(mode), float(sigma), float(rtol),
-                                      int(maxit), int(method))
+        sigma = complex(sigma)
+        if sigma.imag != 0.0:
+            rc = L.arpack_hip_dgen_create_cshift(C.byref(h), A.h, B.h, int(mode), sigma.real,
+                                                 sigma.imag, float(rtol), int(maxit),
+                                                 {2: 0, 3: 1}[int(method)])
+        else:
+            rc = L.arpack_hip_dgen_create(C.byref(h), A.h, B.h, int(mode), sigma.real, float(rtol),
+                                          int(maxit), int(method))
         if rc != 0:
             raise RuntimeError(f"arpack_hip_dgen_create failed ({rc})")
         self.h, self.A, self.B, self.mode = h, A, B, int(mode)

@@ -14,6 +14,7 @@
 
 #include "../../include/arpack_hip.h"
 #include "engine.hpp"
+#include "zsolve.hpp"
 
 const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A);
 const ahip::DistOp* ahip_dist_view(const arpack_hip_dist* D);
@@ -164,8 +165,10 @@ static void sym_aupd(int* ido, const char* bmat, int n, const char* which, int n
         // (symmetric only: CG); bmat = 'I'
         // (dnaupd: a nonsymmetric A needs the general solve, BiCGStab)
         if (gen) {  // the operator pair fixes the mode (bmat = 'G'); dnaupd: modes 2, 3
+            // (a complex-shift pair: dnaupd's modes 3 / 4 only)
             if (dist || bmat[0] != 'G' || mode != gen->mode || gen->n != n ||
-                (ns && mode != 2 && mode != 3))
+                (ns && mode != 2 && mode != 3 && !(gen->cshift && mode == 4)) ||
+                (!ns && gen->cshift))
                 ierr = (ierr ? ierr : -11);
         } else if (csr && ((shift ? mode != 3 || dist ||
                                         (ns && shift->method != dev::kDShiftBicgstab &&
@@ -548,6 +551,23 @@ int arpack_hip_dgen_create(arpack_hip_dgen** out, const arpack_hip_csr* A, const
     return 0;
 }
 
+// dnaupd's complex shifts (modes 3 / 4 with sigmai != 0): OP = Re / Im of
+// inv[A - sigma M] M, the complex solve by BiCGStab (method 0) or the direct
+// tridiagonal solve (method 1)
+int arpack_hip_dgen_create_cshift(arpack_hip_dgen** out, const arpack_hip_csr* A,
+                                  const arpack_hip_csr* B, int mode, double sigmar, double sigmai,
+                                  double rtol, int maxit, int method) {
+    if (!out || !(rtol > 0.0) || maxit < 1) return -1;
+    auto* D = new arpack_hip_dgen;
+    const int rc = ahip::dev::dgen_create_cshift(D->G, A, B, mode, sigmar, sigmai, rtol, maxit, method);
+    if (rc != 0) {
+        delete D;
+        return rc;
+    }
+    *out = D;
+    return 0;
+}
+
 void arpack_hip_dgen_destroy(arpack_hip_dgen* D) {
     if (!D) return;
     ahip::dev::dgen_destroy(D->G);
@@ -557,6 +577,14 @@ void arpack_hip_dgen_destroy(arpack_hip_dgen* D) {
 int arpack_hip_dgen_stats(const arpack_hip_dgen* D, long long* solves, long long* iters,
                           long long* fails, double* max_relres) {
     if (!D) return -1;
+    if (D->G.cshift) {
+        const auto& Z = *D->G.ZS;
+        *solves = Z.n_solves;
+        *iters = Z.n_iters;
+        *fails = Z.n_fail;
+        *max_relres = Z.max_relres;
+        return 0;
+    }
     const ahip::dev::DShift& S = D->G.S;
     *solves = S.n_solves;
     *iters = S.n_iters;

@@ -26,8 +26,10 @@
 
 #include "../../include/arpack_hip.h"
 #include "dgen.hpp"
+#include "zsolve.hpp"
 
 const ahip::dev::Csr* ahip_csr_view(const arpack_hip_csr* A);  // csr.hip
+const ahip::zdev::ZCsr* ahip_zcsr_view(const arpack_hip_zcsr* A);  // zsolver.cpp
 
 namespace ahip::dev {
 
@@ -124,7 +126,65 @@ int dgen_create(DGen& G, const arpack_hip_csr* A, const arpack_hip_csr* B, int m
     return 0;
 }
 
+int dgen_create_cshift(DGen& G, const arpack_hip_csr* A, const arpack_hip_csr* B, int mode,
+                       double sigmar, double sigmai, double rtol, int maxit, int method) {
+    G = DGen{};
+    int64_t na = 0, nb = 0, nz = 0;
+    if (!A || !B || (mode != 3 && mode != 4) || sigmai == 0.0 || method < 0 || method > 1 ||
+        arpack_hip_csr_info(A, &na, &nz) != 0 || arpack_hip_csr_info(B, &nb, &nz) != 0 || na != nb ||
+        na <= 0)
+        return -1;
+    G.A = ahip_csr_view(A);
+    G.B = ahip_csr_view(B);
+    G.mode = mode;
+    G.sigma = sigmar;
+    G.n = na;
+    G.cshift = true;
+    G.part = mode == 4 ? 1 : 0;
+    // C = A - sigma M over the union pattern, in complex arithmetic (the
+    // drivers' own: dndrv5.f forms A - (sigmar, sigmai) M entry by entry)
+    std::vector<int64_t> ap, bp, cp;
+    std::vector<int32_t> ac, bc, cc;
+    std::vector<double> av, bv, cvr, cvi;
+    if (!download(A, ap, ac, av) || !download(B, bp, bc, bv)) return -2;
+    csr_axpy_host(na, ap, ac, av, bp, bc, bv, sigmar, cp, cc, cvr);  // re: a - sigmar m
+    std::vector<double> zero(av.size(), 0.0);
+    std::vector<int64_t> cp2;
+    std::vector<int32_t> cc2;
+    csr_axpy_host(na, ap, ac, zero, bp, bc, bv, sigmai, cp2, cc2, cvi);  // im: -sigmai m
+    std::vector<double> cv(2 * cc.size());
+    for (size_t k = 0; k < cc.size(); ++k) {
+        cv[2 * k] = cvr[k];
+        cv[2 * k + 1] = cvi[k];
+    }
+    if (arpack_hip_zcsr_create(&G.ZC, na, (int64_t)cc.size(), cp.data(), cc.data(), cv.data()) != 0) {
+        G.ZC = nullptr;
+        return -2;
+    }
+    G.ZS = new zdev::ZShift;
+    if (zdev::zshift_create(*G.ZS, ahip_zcsr_view(G.ZC), std::complex<double>(0.0, 0.0), rtol, maxit) != 0) {
+        dgen_destroy(G);
+        return -2;
+    }
+    if (method == 1 && zdev::zshift_tridiag_factor(*G.ZS) != 0) {
+        dgen_destroy(G);
+        return -1;
+    }
+    if (hipMalloc(&G.t, sizeof(double) * 2 * (size_t)na) != hipSuccess ||
+        hipMalloc(&G.zb, sizeof(double) * 4 * (size_t)na) != hipSuccess) {
+        dgen_destroy(G);
+        return -2;
+    }
+    return 0;
+}
+
 void dgen_destroy(DGen& G) {
+    if (G.ZS) {
+        zdev::zshift_destroy(*G.ZS);
+        delete G.ZS;
+    }
+    if (G.ZC) arpack_hip_zcsr_destroy(G.ZC);
+    if (G.zb) (void)hipFree(G.zb);
     dshift_destroy(G.S);
     if (G.C) arpack_hip_csr_destroy(G.C);
     if (G.t) (void)hipFree(G.t);
@@ -148,6 +208,18 @@ int dgen_apply(DGen& G, hipStream_t s, int ido, const double* x, double* y, cons
     }
     double relres = 0.0;
     const double* rhs = t;
+    if (G.cshift) {  // y = Re / Im of inv[A - sigma M] (M x), M x given at ido = 1
+        if (ido == 1 && bx) rhs = bx;
+        else csr_spmv(s, *G.B, x, t);
+        const int64_t m2 = 2 * n;
+        zdev::zpack_real(s, n, rhs, G.zb);
+        if (hipGetLastError() != hipSuccess) return -2;
+        const int rc = zdev::zshift_apply(*G.ZS, s, G.zb, G.zb + m2, nullptr);
+        if (rc == -2) return -2;
+        if (rc < 0) return -1;
+        zdev::zextract(s, n, G.zb + m2, G.part, y);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     switch (G.mode) {
         case 2:  // y = inv[M] (A x), and (dsaupd) x <- A x
             csr_spmv(s, *G.A, x, t);

@@ -263,7 +263,35 @@ __global__ __launch_bounds__(kT) void k_bi_p(int64_t n, const double2* __restric
     }
 }
 
+// z = x + 0i (a real vector as complex128)
+__global__ __launch_bounds__(kT) void k_zpack_real(int64_t n, const double* __restrict__ x,
+                                                  double2* __restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT)
+        z[i] = make_double2(x[i], 0.0);
+}
+
+// y = Re z or Im z
+__global__ __launch_bounds__(kT) void k_zpart(int64_t n, const double2* __restrict__ z, int imag,
+                                             double* __restrict__ y) {
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT)
+        y[i] = imag ? z[i].y : z[i].x;
+}
+
 }  // namespace
+
+void zpack_real(hipStream_t s, int64_t n, const double* x, double* z) {
+    int64_t g = (n + kT - 1) / kT;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_zpack_real, dim3((unsigned)(g < 1 ? 1 : g)), dim3(kT), 0, s, n, x,
+                       reinterpret_cast<double2*>(z));
+}
+
+void zextract(hipStream_t s, int64_t n, const double* z, int imag, double* y) {
+    int64_t g = (n + kT - 1) / kT;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_zpart, dim3((unsigned)(g < 1 ? 1 : g)), dim3(kT), 0, s, n,
+                       reinterpret_cast<const double2*>(z), imag, y);
+}
 
 int zshift_create(ZShift& S, const ZCsr* A, std::complex<double> sigma, double rtol, int maxit) {
     S = ZShift{};

@@ -77,6 +77,9 @@ int zshift_tridiag_factor(ZShift& S);
 void zshift_tridiag_free(ZShift& S);
 // y = (A - sigma I)^{-1} b by the factors (b, y device, not aliased): 0 or -2
 int zshift_tridiag_apply(ZShift& S, hipStream_t s, const double* b, double* y);
+// z = x + 0i (x real, z interleaved complex); y = Re z (imag = 0) or Im z
+void zpack_real(hipStream_t s, int64_t n, const double* x, double* z);
+void zextract(hipStream_t s, int64_t n, const double* z, int imag, double* y);
 // algorithmic HBM bytes of one BiCGStab iteration (two CSR products at 20 B a
 // stored entry + rowptr + x/y vectors, and the fused vector passes)
 double zshift_iter_bytes(const ZShift& S);

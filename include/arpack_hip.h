@@ -458,6 +458,17 @@ void arpack_hip_dnaupd_shift(arpack_hip_dshift* S, int* ido, char const* bmat, i
 typedef struct arpack_hip_dgen arpack_hip_dgen;
 int arpack_hip_dgen_create(arpack_hip_dgen** G, const arpack_hip_csr* A, const arpack_hip_csr* B,
                            int mode, double sigma, double rtol, int maxit, int method);
+/* dnaupd's complex shifts (SRC/dnaupd.f:28-33; EXAMPLES/NONSYM/dndrv5.f, dndrv6.f):
+ * mode 3 OP = Real_Part{inv[A - sigma M] M}, mode 4 OP = Imag_Part{...}, B = M,
+ * sigma = (sigmar, sigmai) with sigmai != 0.  C = A - sigma M is formed once in
+ * complex arithmetic over the union pattern and solved on the device by the
+ * complex BiCGStab (method 0) or, for tridiagonal A and M as dndrv5/6's, the
+ * direct tridiagonal solve (method 1: zgttrf + device scans, the drivers' own
+ * factorization).  arpack_hip_dnaupd_gen then runs the loop (iparam[6] = mode);
+ * dneupd_c takes sigmar, sigmai.  Returns 0, -1 (bad arguments), -2. */
+int arpack_hip_dgen_create_cshift(arpack_hip_dgen** G, const arpack_hip_csr* A,
+                                  const arpack_hip_csr* M, int mode, double sigmar, double sigmai,
+                                  double rtol, int maxit, int method);
 void arpack_hip_dgen_destroy(arpack_hip_dgen* G);
 int arpack_hip_dgen_stats(const arpack_hip_dgen* G, long long* solves, long long* iters,
                           long long* fails, double* max_relres);

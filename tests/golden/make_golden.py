@@ -232,6 +232,29 @@ def zndrv2_fixtures():
           sigma=5000 + 2000j)
 
 
+def cshift_fixtures():
+    """dnaupd's complex shifts: EXAMPLES/NONSYM/dndrv5.f (mode 3, OP = Re
+    inv[A - sigma M] M) and dndrv6.f's operator (Im ...) in mode 4, sigma =
+    (0.4, 0.6), n = 100, nev 4, ncv 20, LM -- the drivers' zgttrf / zgttrs
+    solve stands as a complex sparse LU (tests/modes.py CShiftCaller)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import modes
+    n, sigma = 100, 0.4 + 0.6j
+    v0, _ = M.dlarnv_uniform(n)
+    for name, mode in (("m10_ns_cshift_re", 3), ("m11_ns_cshift_im", 4)):
+        c = modes.CShiftCaller(mode, n, sigma)
+        r = ref.dnaupd_solve(c.op, n, 4, 20, "LM", 1e-10, v0=v0, mxiter=300, mode=mode, bmat="G",
+                             bop=c.bop, sigmar=sigma.real, sigmai=sigma.imag)
+        assert r["info"] >= 0 and r["eupd_info"] == 0, (name, r["info"], r.get("eupd_info"))
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), family="ns", mode=mode,
+                            kind=np.array("dndrv5"), n=n, nev=4, ncv=20, which=np.array("LM"),
+                            tol=1e-10, sigmar=sigma.real, sigmai=sigma.imag, v0=v0,
+                            info=r["info"], iparam=r["iparam"], nopx=r["stats"]["nopx"],
+                            nbx=r["stats"]["nbx"], dr=r["dr"], di=r["di"], z=r["z"])
+        print(name, "mode", mode, "iparam", r["iparam"][[2, 4, 8, 9, 10]], "dr", r["dr"][:4],
+              "di", r["di"][:4])
+
+
 def g7_dlarnv():
     lib = glob.glob(os.path.join(os.path.dirname(__import__("scipy").__file__), "..",
                                  "scipy.libs", "libscipy_openblas*.so"))[0]
@@ -302,6 +325,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["zndrv2"]:
         zndrv2_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["cshift"]:
+        cshift_fixtures()
+        sys.exit(0)
     g7_dlarnv()
     r1 = run_sym("g1_dssimp", M.laplace2d(10, 121.0), ["laplace2d", 10, 121.0], 4, 20, "LM", 0.0,
                  keep_z=True)
@@ -329,3 +355,4 @@ if __name__ == "__main__":
     mode_fixtures()
     zmode_fixtures()
     zndrv2_fixtures()
+    cshift_fixtures()

@@ -100,6 +100,32 @@ class ZCaller:
         self.bop = lambda x: Mm @ x
 
 
+def dndrv5_pair(n):
+    """EXAMPLES/NONSYM/dndrv5.f / dndrv6.f pair: A = tridiag(-2, 2, 3),
+    M = tridiag(1, 4, 1)."""
+    e = np.ones(n)
+    A = sp.diags([-2.0 * e[1:], 2.0 * e, 3.0 * e[1:]], [-1, 0, 1], format="csc")
+    Mm = sp.diags([e[1:], 4.0 * e, e[1:]], [-1, 0, 1], format="csc")
+    return A, Mm
+
+
+class CShiftCaller:
+    """dnaupd's complex-shift modes (SRC/dnaupd.f:28-33): mode 3 OP =
+    Re{inv[A - sigma M] M}, mode 4 OP = Im{...}, B = M -- the caller loops of
+    dndrv5.f (real part) / dndrv6.f (imaginary part), the complex LU by SciPy."""
+
+    def __init__(self, mode, n, sigma):
+        self.mode, self.sigma, self.bmat = mode, complex(sigma), "G"
+        A, Mm = dndrv5_pair(n)
+        self.A, self.M = A, Mm
+        lu = spl.splu((A.astype(np.complex128) - self.sigma * Mm).tocsc())
+        part = np.real if mode == 3 else np.imag
+        self.op = lambda x, ido=None, bx=None: part(lu.solve((Mm @ x if bx is None or ido == -1
+                                                              else bx).astype(np.complex128)))
+        self.bop = lambda x: Mm @ x
+        self.ax = None
+
+
 class StdShiftInvert:
     """Standard shift-invert, bmat = 'I': OP = inv(A - sigma I) (dsdrv2 / dndrv2)."""
 

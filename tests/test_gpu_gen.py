@@ -123,3 +123,59 @@ def test_dgen_rejects_mismatch(pkg):
         assert int(s.info[0]) == -11
     with pytest.raises(RuntimeError):
         pkg.DGen(_dev(pkg, A), _dev(pkg, modes.fem1d(60)[1]), 3, 0.0)  # sizes differ
+
+
+# dnaupd's complex shifts (SRC/dnaupd.f:28-33): EXAMPLES/NONSYM/dndrv5.f's pair
+# A = tridiag(-2, 2, 3), M = tridiag(1, 4, 1), sigma = (0.4, 0.6): mode 3 OP =
+# Re{inv[A - sigma M] M} (dndrv5), mode 4 OP = Im{...} (dndrv6's operator);
+# the complex C solved directly on the device (the drivers' zgttrf)
+@pytest.mark.parametrize("name", ["m10_ns_cshift_re", "m11_ns_cshift_im"])
+def test_dnaupd_complex_shift_on_device(pkg, golden, name):
+    g = golden(name)
+    mode, n = int(g["mode"]), int(g["n"])
+    sigma = complex(float(g["sigmar"]), float(g["sigmai"]))
+    A, Mm = modes.dndrv5_pair(n)
+    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), mode, sigma, method=3)
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat="G",
+                  mode=mode, mxiter=300, v0=g["v0"], device=True)
+    assert s.aupd_gen(G) == 99
+    st = G.stats()
+    assert st["fails"] == 0 and st["solves"] > 0 and st["iters"] == 0, st
+    assert int(s.info[0]) == int(g["info"]) == 0
+    assert int(s.iparam[4]) == int(g["iparam"][4])
+    assert int(s.iparam[2]) == int(g["iparam"][2]), (int(s.iparam[2]), int(g["iparam"][2]))
+    assert (int(s.iparam[8]), int(s.iparam[9])) == (int(g["nopx"]), int(g["nbx"]))
+    dr, di, z, nconv = s.eupd(sigmar=sigma.real, sigmai=sigma.imag)
+    lam, ref = dr[:nconv] + 1j * di[:nconv], g["dr"] + 1j * g["di"]
+    for x in ref:
+        assert np.abs(lam - x).min() <= 1e-9 * np.abs(ref).max(), (x, lam)
+
+
+def test_dnaupd_complex_shift_krylov_fails_loudly_or_matches(pkg, golden):
+    """The same run with the complex BiCGStab on C (not diagonally dominant
+    here): it either gives the reference's cycles and eigenvalues or ends the
+    run with info = -9999 (a solve that missed rtol) -- never a wrong OP."""
+    g = golden("m10_ns_cshift_re")
+    n = int(g["n"])
+    sigma = complex(float(g["sigmar"]), float(g["sigmai"]))
+    A, Mm = modes.dndrv5_pair(n)
+    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), 3, sigma, rtol=1e-13, maxit=50 * n, method=2)
+    s = pkg.NsRci(n, int(g["nev"]), int(g["ncv"]), str(g["which"]), float(g["tol"]), bmat="G",
+                  mode=3, mxiter=300, v0=g["v0"], device=True)
+    assert s.aupd_gen(G) == 99
+    if int(s.info[0]) == -9999:
+        assert G.stats()["fails"] > 0
+        return
+    assert int(s.info[0]) == 0 and int(s.iparam[2]) == int(g["iparam"][2])
+    dr, di, z, nconv = s.eupd(sigmar=sigma.real, sigmai=sigma.imag)
+    lam, ref = dr[:nconv] + 1j * di[:nconv], g["dr"] + 1j * g["di"]
+    for x in ref:
+        assert np.abs(lam - x).min() <= 1e-9 * np.abs(ref).max(), (x, lam)
+
+
+def test_dsaupd_rejects_complex_shift_pair(pkg):
+    A, Mm = modes.dndrv5_pair(50)
+    G = pkg.DGen(_dev(pkg, A), _dev(pkg, Mm), 3, 0.4 + 0.6j, method=3)
+    s = pkg.SymRci(50, 4, 12, "LM", 1e-10, bmat="G", mode=3, device=True, v0=np.ones(50))
+    assert s.aupd_gen(G) == 99
+    assert int(s.info[0]) == -11
