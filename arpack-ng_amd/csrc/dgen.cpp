@@ -200,8 +200,9 @@ int dgen_apply(DGen& G, hipStream_t s, int ido, const double* x, double* y, cons
     const int64_t n = G.n;
     double* t = G.t;
     double* t2 = G.t + n;
-    // B*x: the mass matrix (mode 4: K, the user's first matrix)
-    const Csr* bop = G.mode == 4 ? G.A : G.B;
+    // B*x: the mass matrix (dsaupd's mode 4, buckling: K, the user's first
+    // matrix; dnaupd's complex-shift mode 4: M)
+    const Csr* bop = G.mode == 4 && !G.cshift ? G.A : G.B;
     if (ido == 2) {
         csr_spmv(s, *bop, x, y);
         return 0;
