@@ -152,7 +152,7 @@ __device__ __forceinline__ int wave_iscan(int v) {
     return v;
 }
 
-template <bool PK, int U>
+template <bool PK, int U, int T = 256>
 __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ idx,
                                            const int32_t* __restrict__ cbase,
                                            const double2* __restrict__ val, int (&row)[U], int (&col)[U],
@@ -163,12 +163,12 @@ __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ i
         int cb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // every load of the batch issued first
-            id[u] = __builtin_nontemporal_load(static_cast<const uint16_t*>(idx) + e + u * 256);
-            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+            id[u] = __builtin_nontemporal_load(static_cast<const uint16_t*>(idx) + e + u * T);
+            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * T);
             v[u] = make_double2(w.x, w.y);
             // one base a wave: the chunk index is wave-uniform (a segment
             // starts on a chunk, a wave loads one whole chunk), so a scalar load
-            cb[u] = cbase[__builtin_amdgcn_readfirstlane((int)((e + u * 256) >> 6))];
+            cb[u] = cbase[__builtin_amdgcn_readfirstlane((int)((e + u * T) >> 6))];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -179,8 +179,8 @@ __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ i
         uint32_t id[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            id[u] = __builtin_nontemporal_load(static_cast<const uint32_t*>(idx) + e + u * 256);
-            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * 256);
+            id[u] = __builtin_nontemporal_load(static_cast<const uint32_t*>(idx) + e + u * T);
+            const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(val) + e + u * T);
             v[u] = make_double2(w.x, w.y);
         }
 #pragma unroll
@@ -195,16 +195,16 @@ __device__ __forceinline__ void tile_batch(int64_t e, const void* __restrict__ i
 // gathers of the slice, then add(row, re, im) per entry (LDS row sums).  A
 // packed segment's length is a multiple of 64, so the tail loop's condition is
 // uniform across a wave (its scan needs every lane).
-template <bool PK, int TU, class Add>
+template <bool PK, int TU, class Add, int T = 256>
 __device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __restrict__ idx,
                                           const int32_t* __restrict__ cbase,
                                           const double2* __restrict__ val, const double2* __restrict__ xs,
                                           Add add) {
     int64_t e = e0 + threadIdx.x;
-    for (; e + (TU - 1) * 256 < e1; e += TU * 256) {
+    for (; e + (TU - 1) * T < e1; e += TU * T) {
         int row[TU], col[TU];
         double2 v[TU];
-        tile_batch<PK, TU>(e, idx, cbase, val, row, col, v);
+        tile_batch<PK, TU, T>(e, idx, cbase, val, row, col, v);
         double2 xv[TU];
 #pragma unroll
         for (int u = 0; u < TU; ++u) xv[u] = xs[col[u]];
@@ -212,17 +212,17 @@ __device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __
         for (int u = 0; u < TU; ++u)
             add(row[u], v[u].x * xv[u].x - v[u].y * xv[u].y, v[u].x * xv[u].y + v[u].y * xv[u].x);
     }
-    for (; e < e1; e += 256) {
+    for (; e < e1; e += T) {
         int row[1], col[1];
         double2 v[1];
-        tile_batch<PK, 1>(e, idx, cbase, val, row, col, v);
+        tile_batch<PK, 1, T>(e, idx, cbase, val, row, col, v);
         const double2 xv = xs[col[0]];
         add(row[0], v[0].x * xv.x - v[0].y * xv.y, v[0].x * xv.y + v[0].y * xv.x);
     }
 }
 
-template <int S, bool PK, int TU = kTileU>
-__global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+template <int S, bool PK, int TU = kTileU, int T = 256>
+__global__ __launch_bounds__(T) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
                                                int64_t nrb, const void* __restrict__ idx,
                                                const int32_t* __restrict__ cbase,
                                                const double2* __restrict__ val,
@@ -234,17 +234,17 @@ __global__ __launch_bounds__(256) void k_ztile(int64_t n, int64_t sw, const int6
     const int64_t rb = blockIdx.x / S;
     const int64_t r0 = rb * kTileRows;
     const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
-    for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0.0;
+    for (int i = threadIdx.x; i < 2 * rows; i += T) ylds[i] = 0.0;
     __syncthreads();
     const int64_t q = s * nrb + rb;
-    tile_walk<PK, TU>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
-                  [&](int r, double re, double im) {
-                      atomicAdd(&ylds[2 * r], re);
-                      atomicAdd(&ylds[2 * r + 1], im);
-                  });
+    auto add = [&](int r, double re, double im) {
+        atomicAdd(&ylds[2 * r], re);
+        atomicAdd(&ylds[2 * r + 1], im);
+    };
+    tile_walk<PK, TU, decltype(add), T>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw, add);
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
-    for (int i = threadIdx.x; i < rows; i += 256) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
+    for (int i = threadIdx.x; i < rows; i += T) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
 }
 
 constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid = k_ztile_det's block size
@@ -802,6 +802,15 @@ int tile_u() {
     }();
     return u;
 }
+// AHIP_ZTILE_T=512 | 1024: threads a tile workgroup (default 256; A/B)
+int tile_t() {
+    static const int t = [] {
+        const char* e = getenv("AHIP_ZTILE_T");
+        const int v = e ? atoi(e) : 256;
+        return v == 512 || v == 1024 ? v : 256;
+    }();
+    return t;
+}
 
 template <int S>
 void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp, const int* gate) {
@@ -811,8 +820,18 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
                                (const double2*)A.t_val, x2, yp, gate);
         };
-        if (A.t_pk) tile_u() == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
-        else go(k_ztile<S, false>);
+        if (A.t_pk && tile_t() == 512) {
+            hipLaunchKernelGGL((k_ztile<S, true, kTileU, 512>), tg, dim3(512), 0, s, A.n, A.s_w, A.t_seg,
+                               A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp, gate);
+        } else if (A.t_pk && tile_t() == 1024) {
+            hipLaunchKernelGGL((k_ztile<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n, A.s_w,
+                               A.t_seg, A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp,
+                               gate);
+        } else if (A.t_pk) {
+            tile_u() == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
+        } else {
+            go(k_ztile<S, false>);
+        }
         return;
     }
     if (A.tile && A.t_det) {  // deterministic: the fixed-point tile form (else the CSR split, kept)
