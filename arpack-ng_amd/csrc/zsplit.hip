@@ -802,12 +802,16 @@ int tile_u() {
     }();
     return u;
 }
-// AHIP_ZTILE_T=512 | 1024: threads a tile workgroup (default 256; A/B)
+// Threads a packed tile workgroup: 1,024 (default), AHIP_ZTILE_T=256 | 512
+// for A/B.  The 64 KB of LDS row sums hold two workgroups a CU whatever their
+// size, so the size sets the waves a SIMD that keep entries in flight: 2, 4 or
+// 8.  Config 5 in mode 3, same box (profiles/r06v_ztile_threads_ab.txt): 2.60
+// / 2.70 / 2.52 ms a solve at 256 / 512 / 1,024 threads (51 VGPRs in each).
 int tile_t() {
     static const int t = [] {
         const char* e = getenv("AHIP_ZTILE_T");
-        const int v = e ? atoi(e) : 256;
-        return v == 512 || v == 1024 ? v : 256;
+        const int v = e ? atoi(e) : 1024;
+        return v == 256 || v == 512 ? v : 1024;
     }();
     return t;
 }
@@ -827,7 +831,7 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL((k_ztile<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n, A.s_w,
                                A.t_seg, A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp,
                                gate);
-        } else if (A.t_pk) {
+        } else if (A.t_pk) {  // 256 threads (U = 8: AHIP_ZTILE_U A/B, with AHIP_ZTILE_T=256)
             tile_u() == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
         } else {
             go(k_ztile<S, false>);
