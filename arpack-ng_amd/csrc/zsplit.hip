@@ -247,8 +247,7 @@ __global__ __launch_bounds__(T) void k_ztile(int64_t n, int64_t sw, const int64_
     for (int i = threadIdx.x; i < rows; i += T) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
 }
 
-constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid = k_ztile_det's block size
-static_assert(kZMaxBlocks == 256, "k_ztile_det reduces one block maximum a thread");
+constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid (<= k_ztile_det's block size)
 
 // Deterministic mode's tile product (arpack_hip_set_deterministic): k_ztile
 // with the row sums as 64-bit FIXED-POINT integers (the scheme of
@@ -259,8 +258,8 @@ static_assert(kZMaxBlocks == 256, "k_ztile_det reduces one block maximum a threa
 // wave order; y_s = (double)(sum q) 2^(E-B).  B = min(51, 62 - bits(L)) for at
 // most L entries a row in a slice.  The slice partials are summed in
 // zc::slice_sum's fixed order as before.
-template <int S, bool PK, int TU = kTileU>
-__global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+template <int S, bool PK, int TU = kTileU, int T = 256>
+__global__ __launch_bounds__(T) void k_ztile_det(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
                                                    int64_t nrb, const void* __restrict__ idx,
                                                    const int32_t* __restrict__ cbase,
                                                    const double2* __restrict__ val,
@@ -272,19 +271,24 @@ __global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const 
     constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
     const unsigned long long kMagicBits = (unsigned long long)__double_as_longlong(kMagic);
     __shared__ unsigned long long ylds[2 * kTileRows];
-    __shared__ unsigned long long wmax[4];
+    static_assert(T >= kZMaxBlocks, "one block maximum a thread");
+    __shared__ unsigned long long wmax[T / 64];
     const int s = (int)(blockIdx.x % S);
     const int64_t rb = blockIdx.x / S;
     const int64_t r0 = rb * kTileRows;
     const int rows = (int)((n - r0) < kTileRows ? (n - r0) : kTileRows);
-    for (int i = threadIdx.x; i < 2 * rows; i += 256) ylds[i] = 0ull;
-    {  // max|x| from k_zabsmax's kZMaxBlocks block maxima (one a thread)
-        unsigned long long m = xmax[threadIdx.x];
+    for (int i = threadIdx.x; i < 2 * rows; i += T) ylds[i] = 0ull;
+    {  // max|x| from k_zabsmax's kZMaxBlocks block maxima (one a thread; a
+       // maximum, so the same in any order and at any block size)
+        unsigned long long m = threadIdx.x < kZMaxBlocks ? xmax[threadIdx.x] : 0ull;
         for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
     }
     __syncthreads();
-    const double X = __longlong_as_double((long long)max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+    unsigned long long wm = wmax[0];
+#pragma unroll
+    for (int w = 1; w < T / 64; ++w) wm = max(wm, wmax[w]);
+    const double X = __longlong_as_double((long long)wm);
     const int64_t q = s * nrb + rb;
     int ea = 0, ex = 0;
     (void)frexp(amax[q], &ea);
@@ -297,14 +301,14 @@ __global__ __launch_bounds__(256) void k_ztile_det(int64_t n, int64_t sw, const 
         const double f = fma(p, inv, kMagic);
         return (unsigned long long)__double_as_longlong(f) - kMagicBits;
     };
-    tile_walk<PK, TU>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw,
-                  [&](int r, double re, double im) {
-                      atomicAdd(&ylds[2 * r], q64(re));
-                      atomicAdd(&ylds[2 * r + 1], q64(im));
-                  });
+    auto add = [&](int r, double re, double im) {
+        atomicAdd(&ylds[2 * r], q64(re));
+        atomicAdd(&ylds[2 * r + 1], q64(im));
+    };
+    tile_walk<PK, TU, decltype(add), T>(seg[q], seg[q + 1], idx, cbase, val, x + (int64_t)s * sw, add);
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
-    for (int i = threadIdx.x; i < rows; i += 256)
+    for (int i = threadIdx.x; i < rows; i += T)
         y[i] = make_double2((double)(long long)ylds[2 * i] * sc, (double)(long long)ylds[2 * i + 1] * sc);
 }
 
@@ -847,8 +851,14 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
                                (const double2*)A.t_val, x2, yp, gate, A.t_amax, A.t_xmax, A.t_bits);
         };
-        if (A.t_pk) go(k_ztile_det<S, true>);
-        else go(k_ztile_det<S, false>);
+        if (A.t_pk && tile_t() == 1024)  // the default tile's block size (bitwise the same sums)
+            hipLaunchKernelGGL((k_ztile_det<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n, A.s_w,
+                               A.t_seg, A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp,
+                               gate, A.t_amax, A.t_xmax, A.t_bits);
+        else if (A.t_pk)
+            go(k_ztile_det<S, true>);
+        else
+            go(k_ztile_det<S, false>);
         return;
     }
     const int g = 1024;  // 128 workgroups a slice at S = 8 (tools/zspmv_split.hip)
