@@ -36,7 +36,20 @@ namespace ahip::zdev {
 
 namespace {
 using namespace zc;
-constexpr int kT = 256;      // threads a block
+#ifndef AHIP_BI_T
+#define AHIP_BI_T 256
+#endif
+constexpr int kT = AHIP_BI_T;  // threads a block
+static_assert(kT == 256 || kT == 512 || kT == 1024, "4, 8 or 16 waves a block");
+constexpr int kW = kT / 64;
+
+// the waves' values of slot q in one fixed pairwise order ((0 + 1) + (2 + 3))
+// + ((4 + 5) + (6 + 7)) ...
+template <int LO, int CNT, int NS>
+__device__ __forceinline__ double pair_sum(const double (&red)[kW][NS], int q) {
+    if constexpr (CNT == 1) return red[LO][q];
+    else return pair_sum<LO, CNT / 2, NS>(red, q) + pair_sum<LO + CNT / 2, CNT / 2, NS>(red, q);
+}
 constexpr int kMaxBlk = 512;  // blocks of the vector kernels (partials per slot)
 
 // a / b by Smith's algorithm (as the host kit's zla::cdiv): no overflow or
@@ -54,7 +67,7 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 template <int NS>
 __device__ __forceinline__ void put_partials(const double (&acc)[NS], double* __restrict__ part,
                                              int nblk) {
-    __shared__ double red[kT / 64][NS];
+    __shared__ double red[kW][NS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
@@ -64,14 +77,14 @@ __device__ __forceinline__ void put_partials(const double (&acc)[NS], double* __
     __syncthreads();
     if (threadIdx.x < NS) {
         const int q = threadIdx.x;
-        part[(int64_t)q * nblk + blockIdx.x] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+        part[(int64_t)q * nblk + blockIdx.x] = pair_sum<0, kW, NS>(red, q);
     }
 }
 
 // fixed-order total of NS slots of per-block partials (every block, same result)
 template <int NS>
 __device__ __forceinline__ void totals(const double* __restrict__ part, int nblk, double (&out)[NS]) {
-    __shared__ double red[kT / 64][NS];
+    __shared__ double red[kW][NS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
@@ -82,7 +95,7 @@ __device__ __forceinline__ void totals(const double* __restrict__ part, int nblk
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < NS; ++q) out[q] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+    for (int q = 0; q < NS; ++q) out[q] = pair_sum<0, kW, NS>(red, q);
 }
 
 __global__ __launch_bounds__(kT) void k_bi_init(int64_t n, const double2* __restrict__ b,
