@@ -221,13 +221,13 @@ __device__ __forceinline__ void tile_walk(int64_t e0, int64_t e1, const void* __
     }
 }
 
-template <int S, bool PK, int TU = kTileU, int T = 256>
-__global__ __launch_bounds__(T) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
-                                               int64_t nrb, const void* __restrict__ idx,
-                                               const int32_t* __restrict__ cbase,
-                                               const double2* __restrict__ val,
-                                               const double2* __restrict__ x,
-                                               double2* __restrict__ yp, const int* __restrict__ gate) {
+template <int S, bool PK, int TU, int T>
+__device__ __forceinline__ void ztile_body(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+                                           int64_t nrb, const void* __restrict__ idx,
+                                           const int32_t* __restrict__ cbase,
+                                           const double2* __restrict__ val,
+                                           const double2* __restrict__ x, double2* __restrict__ yp,
+                                           const int* __restrict__ gate) {
     if (gate && *gate) return;
     __shared__ double ylds[2 * kTileRows];
     const int s = (int)(blockIdx.x % S);  // the XCD (S = 4: one of two) this block runs on
@@ -245,6 +245,26 @@ __global__ __launch_bounds__(T) void k_ztile(int64_t n, int64_t sw, const int64_
     __syncthreads();
     double2* y = yp + (int64_t)s * n + r0;
     for (int i = threadIdx.x; i < rows; i += T) y[i] = make_double2(ylds[2 * i], ylds[2 * i + 1]);
+}
+
+template <int S, bool PK, int TU = kTileU, int T = 256>
+__global__ __launch_bounds__(T) void k_ztile(int64_t n, int64_t sw, const int64_t* __restrict__ seg,
+                                               int64_t nrb, const void* __restrict__ idx,
+                                               const int32_t* __restrict__ cbase,
+                                               const double2* __restrict__ val,
+                                               const double2* __restrict__ x,
+                                               double2* __restrict__ yp, const int* __restrict__ gate) {
+    ztile_body<S, PK, TU, T>(n, sw, seg, nrb, idx, cbase, val, x, yp, gate);
+}
+
+// the 1,024-thread packed walk held to 64 VGPRs (8 waves a SIMD: both LDS-sized
+// workgroups of a CU resident) where TU would otherwise take more
+template <int S, int TU>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_ztile_w8(
+    int64_t n, int64_t sw, const int64_t* __restrict__ seg, int64_t nrb, const void* __restrict__ idx,
+    const int32_t* __restrict__ cbase, const double2* __restrict__ val, const double2* __restrict__ x,
+    double2* __restrict__ yp, const int* __restrict__ gate) {
+    ztile_body<S, true, TU, 1024>(n, sw, seg, nrb, idx, cbase, val, x, yp, gate);
 }
 
 constexpr int kZMaxBlocks = 256;  // k_zabsmax's grid (<= k_ztile_det's block size)
@@ -798,13 +818,19 @@ int zcsr_build_split(ZCsr& A) {
 }
 
 namespace {
-// AHIP_ZTILE_U=8: the packed tile walk keeps 8 entries a lane in flight (A/B)
-int tile_u() {
+// Entries a lane of the packed tile walk keeps in flight: 6 at 1,024 threads
+// (62 VGPRs, under the 64 that 8 waves a SIMD allow), 4 at 256 / 512; A/B:
+// AHIP_ZTILE_U=8 (256 threads) | 2, 4, 5, 7, 8 (1,024 threads; 8 through
+// k_ztile_w8).  Config 5 in mode 3 at 1,024 threads, same-box pairs
+// (profiles/r06ab_ztile_unroll_ab.txt): 6 solves 3% faster than 4, 1-2% than 5,
+// 2% than 7 and 7% than 8; 2 is 8% slower than 4.
+constexpr int kTileU1k = 6;
+int tile_u(int dflt) {
     static const int u = [] {
         const char* e = getenv("AHIP_ZTILE_U");
-        return e && e[0] == '8' ? 8 : kTileU;
+        return e && e[0] >= '2' && e[0] <= '8' ? e[0] - '0' : 0;
     }();
-    return u;
+    return u ? u : dflt;
 }
 // Threads a packed tile workgroup: 1,024 (default), AHIP_ZTILE_T=256 | 512
 // for A/B.  The 64 KB of LDS row sums hold two workgroups a CU whatever their
@@ -832,11 +858,27 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL((k_ztile<S, true, kTileU, 512>), tg, dim3(512), 0, s, A.n, A.s_w, A.t_seg,
                                A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp, gate);
         } else if (A.t_pk && tile_t() == 1024) {
-            hipLaunchKernelGGL((k_ztile<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n, A.s_w,
-                               A.t_seg, A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp,
-                               gate);
+            auto go1k = [&](auto kern) {
+                hipLaunchKernelGGL(kern, tg, dim3(1024), 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx,
+                                   A.t_cbase, (const double2*)A.t_val, x2, yp, gate);
+            };
+            const int u = tile_u(kTileU1k);
+            if (u == 2)
+                go1k(k_ztile<S, true, 2, 1024>);
+            else if (u == 5)
+                go1k(k_ztile<S, true, 5, 1024>);
+            else if (u == 6)
+                go1k(k_ztile<S, true, 6, 1024>);
+            else if (u == 7)
+                go1k(k_ztile<S, true, 7, 1024>);
+            else if (u == 8)
+                go1k(k_ztile_w8<S, 8>);
+            else
+                hipLaunchKernelGGL((k_ztile<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n,
+                                   A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
+                                   (const double2*)A.t_val, x2, yp, gate);
         } else if (A.t_pk) {  // 256 threads (U = 8: AHIP_ZTILE_U A/B, with AHIP_ZTILE_T=256)
-            tile_u() == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
+            tile_u(kTileU) == 8 ? go(k_ztile<S, true, 8>) : go(k_ztile<S, true>);
         } else {
             go(k_ztile<S, false>);
         }
