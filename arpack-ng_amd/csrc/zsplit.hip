@@ -893,10 +893,15 @@ void split_partials(hipStream_t s, const ZCsr& A, const double2* x2, double2* yp
             hipLaunchKernelGGL(kern, tg, tb, 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx, A.t_cbase,
                                (const double2*)A.t_val, x2, yp, gate, A.t_amax, A.t_xmax, A.t_bits);
         };
-        if (A.t_pk && tile_t() == 1024)  // the default tile's block size (bitwise the same sums)
-            hipLaunchKernelGGL((k_ztile_det<S, true, kTileU, 1024>), tg, dim3(1024), 0, s, A.n, A.s_w,
-                               A.t_seg, A.t_nrb, A.t_idx, A.t_cbase, (const double2*)A.t_val, x2, yp,
-                               gate, A.t_amax, A.t_xmax, A.t_bits);
+        auto det1k = [&](auto kern) {  // the default tile's block size (bitwise the same sums)
+            hipLaunchKernelGGL(kern, tg, dim3(1024), 0, s, A.n, A.s_w, A.t_seg, A.t_nrb, A.t_idx,
+                               A.t_cbase, (const double2*)A.t_val, x2, yp, gate, A.t_amax, A.t_xmax,
+                               A.t_bits);
+        };
+        if (A.t_pk && tile_t() == 1024 && tile_u(kTileU1k) == 4)
+            det1k(k_ztile_det<S, true, 4, 1024>);
+        else if (A.t_pk && tile_t() == 1024)  // six entries a lane: 64 VGPRs
+            det1k(k_ztile_det<S, true, kTileU1k, 1024>);
         else if (A.t_pk)
             go(k_ztile_det<S, true>);
         else
