@@ -648,13 +648,16 @@ static void sb_row_caps(int64_t n, int64_t& cap0, int64_t& rest) {
         cap0 = rest = rcap;
         return;
     }
-    // (AHIP_LIGHT_SB=4: a quarter of the cap -- more room for the Arnoldi
-    // finalize's H staging, A/B)
+    // an eighth of the cap (AHIP_LIGHT_SB=1: half, 4: a quarter; A/B): the
+    // finalize -- the Arnoldi one with its H staging most -- then ends inside
+    // the other workgroups' stream.  Configs 2 / 3, same box
+    // (profiles/r06ak_light_sb8_ab.txt): SpMV 14.8 -> 14.2-14.5 / 18.0-18.3 ->
+    // 17.2-18.2 µs, cycles/s +0.8%; the rows' results do not depend on it.
     static const int div = [] {
         const char* e = getenv("AHIP_LIGHT_SB");
-        return e && e[0] == '4' ? 4 : 2;
+        return e && e[0] == '4' ? 4 : e && e[0] == '1' ? 2 : 8;
     }();
-    cap0 = rcap / div > 256 ? rcap / div : rcap;
+    cap0 = rcap / div > 128 ? rcap / div : rcap;
     rest = (n - cap0 + slots - 2) / (slots - 1);
     if (rest < rcap) rest = rcap;  // small n: the 1,024-row floor (fewer superblocks than slots)
     if (rest < cap0) rest = cap0;
